@@ -1,0 +1,82 @@
+"""ctypes binding of the gfx950 C ABI (include/matcha_gossip.h -> _native/libmatcha_gossip.so).
+
+There is no fallback: if the library is missing the package import fails loudly, and every
+compute entry point needs a HIP device.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_native", "libmatcha_gossip.so")
+
+c_int, c_i64, c_u64, c_f32, c_f64 = ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float, ctypes.c_double
+c_p = ctypes.c_void_p
+
+# name -> (restype, argtypes); mirrors include/matcha_gossip.h one to one
+SIGNATURES = {
+    "mx_version": (ctypes.c_char_p, []),
+    "mx_last_error": (ctypes.c_char_p, []),
+    "mx_flags_binomial": (c_int, [c_p, c_int, c_p, c_int, c_i64, c_p, c_p, c_p, c_p]),
+    "mx_flags_binomial_sequential": (c_int, [c_p, c_int, c_p, c_int, c_i64, c_p, c_p, c_p, c_p]),
+    "mx_plan_words": (c_i64, [c_int, c_int]),
+    "mx_plan_build": (c_int, [c_p, c_i64, c_int, c_p, c_int, c_p, c_int, c_int, c_int, c_f64, c_p, c_p]),
+    "mx_mix_tile": (c_int, [c_int]),
+    "mx_mix_layout": (c_int, [c_p, c_int, c_int, c_p]),
+    "mx_gossip_mix": (c_int, [c_p, c_p, c_p, c_p, c_int, c_i64, c_int, c_p, c_i64, c_int, c_int, c_f32, c_p]),
+    "mx_gather": (c_int, [c_p, c_p, c_int, c_i64, c_p, c_p]),
+    "mx_scatter": (c_int, [c_p, c_p, c_int, c_i64, c_p, c_p]),
+    "mx_topk_work_bytes": (ctypes.c_size_t, [c_i64]),
+    "mx_topk_abs_diff": (c_int, [c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p]),
+    "mx_choco_msg_bytes": (c_i64, [c_i64]),
+    "mx_choco_apply": (c_int, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_p, c_i64, c_int, c_int,
+                               c_f32, c_f32, c_p]),
+    "mx_rccl_unique_id": (c_int, [c_p]),
+    "mx_rccl_init": (c_int, [c_p, c_int, c_int, c_p]),
+    "mx_rccl_destroy": (c_int, [c_p]),
+    "mx_exchange_round": (c_int, [c_p, c_p, c_int, c_p, c_int, c_p, c_int, c_int, c_int, c_p, c_p, c_i64,
+                                  c_i64, c_p, c_p]),
+    "mx_allreduce_mean": (c_int, [c_p, c_p, c_i64, c_int, c_p]),
+    "mx_synth_fill": (c_int, [c_p, c_i64, c_u64, c_p]),
+}
+
+
+class MXError(RuntimeError):
+    """A negative status from the native library (message from mx_last_error)."""
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"native gossip library not built: {LIB_PATH} is missing. Build it with "
+            f"`make -C {_HERE}` (hipcc --offload-arch=gfx950) or __graft_entry__.build().")
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    return L
+
+
+lib = _load()
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib.mx_last_error().decode(errors="replace")
+        raise MXError(f"{what or 'matcha-gossip'} failed ({rc}): {msg}")
+    return rc
+
+
+def stream_ptr(stream=None):
+    """hipStream_t of a torch stream (default: torch's current stream on the current device)."""
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+def require_device():
+    import torch
+    if not torch.cuda.is_available():
+        raise RuntimeError(
+            "matcha-gossip runs on an MI355X (gfx950) GPU; no HIP device is visible. There is "
+            "no CPU path.")

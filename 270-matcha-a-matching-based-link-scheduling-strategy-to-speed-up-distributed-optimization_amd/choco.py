@@ -1,0 +1,107 @@
+"""ChocoSGD compressed gossip on the GPU (communicator.py:161-268, compressors.py:3-19).
+
+ChocoWorkerGroup keeps, for a block of workers on this GPU, the parameter arena x and the
+persistent Choco state x_hat and s (all [n_local, P] in HBM).  Per round:
+    q_r = top-k(|x_r - x_hat_r|)            mx_topk_abs_diff   (prepare_comm_buffer, 175-196)
+    [N > 1] RCCL exchange of the messages   mx_exchange_round  (12 k bytes per edge direction)
+    s / x_hat scatters + dense x update     mx_choco_apply     (averaging, 200-230)
+"""
+import time
+
+import numpy as np
+import torch
+
+from ._lib import check, lib, require_device, stream_ptr
+from .engine import GossipEngine, ROW_ALIGN, default_comm, owner_table, partition
+
+
+def topk_count(P, ratio):
+    """compressors.py:11 -- k = max(1, int(len * (1 - ratio)))."""
+    return max(1, int(P * (1 - ratio)))
+
+
+class ChocoWorkerGroup:
+    def __init__(self, topology, models=None, numel=None, *, ratio, consensus_lr, rank=0, nranks=1,
+                 comm=None, adopt=True):
+        require_device()
+        n = int(topology.size)
+        self.row_base, self.n_local = partition(n, nranks)[rank]
+        if nranks > 1 and comm is None:
+            comm = default_comm()
+        self.engine = GossipEngine(topology, self.row_base, self.n_local, comm=comm,
+                                   owner=owner_table(n, nranks))
+        self.topology = topology
+        self.ratio = ratio
+        self.consensus_lr = consensus_lr
+        self.iter = 0
+        if models is not None:
+            if len(models) != self.n_local:
+                raise ValueError(f"{len(models)} models for {self.n_local} local workers")
+            self.numel = int(sum(p.numel() for p in models[0].parameters()))
+        else:
+            self.numel = int(numel)
+        P = self.numel
+        self.ld = (P + ROW_ALIGN - 1) // ROW_ALIGN * ROW_ALIGN
+        self.x = torch.zeros((self.n_local, self.ld), dtype=torch.float32, device="cuda")
+        self.x_hat = torch.zeros_like(self.x)     # communicator.py:179-182 (lazy zeros)
+        self.s = torch.zeros_like(self.x)
+        if models is not None:
+            for r, m in enumerate(models):
+                off = 0
+                for p in m.parameters():
+                    if p.dtype != torch.float32 or p.device.type != "cuda":
+                        raise TypeError("worker parameters must be float32 CUDA tensors")
+                    k = p.numel()
+                    view = self.x[r, off:off + k].view(p.shape)
+                    view.copy_(p.data)
+                    if adopt:
+                        p.data = view
+                    off += k
+        self.k = topk_count(P, ratio)
+        self.kpad = (self.k + 1) // 2 * 2
+        self.msg_bytes = int(lib.mx_choco_msg_bytes(self.k))
+        self.msg_ld = (self.msg_bytes + 255) // 256 * 256
+        self.msgs = torch.empty(self.engine.n_slots * self.msg_ld, dtype=torch.uint8, device="cuda")
+        self.work = torch.empty(int(lib.mx_topk_work_bytes(P)), dtype=torch.uint8, device="cuda")
+        self.gamma32 = float(np.float32(consensus_lr))
+
+    @property
+    def rows(self):
+        return self.x[:, :self.numel]
+
+    def message(self, slot):
+        """(values float32[k], indices int64[k]) views of message `slot` (index-sorted)."""
+        base = slot * self.msg_ld
+        vals = self.msgs[base:base + 4 * self.k].view(torch.float32)
+        idx = self.msgs[base + 4 * self.kpad:base + 4 * self.kpad + 8 * self.k].view(torch.int64)
+        return vals, idx
+
+    def step(self, it, stream=None):
+        if not self.engine.any_active[it]:
+            return False
+        P = self.numel
+        st = stream_ptr(stream)
+        mbase = self.msgs.data_ptr()
+        for r in range(self.n_local):
+            check(lib.mx_topk_abs_diff(self.x[r].data_ptr(), self.x_hat[r].data_ptr(), P, self.k,
+                                       mbase + r * self.msg_ld, mbase + r * self.msg_ld + 4 * self.kpad,
+                                       self.work.data_ptr(), st), "mx_topk_abs_diff")
+        if self.engine.comm is not None:
+            self.engine.exchange(it, [mbase + r * self.msg_ld for r in range(self.n_local)],
+                                 mbase + self.n_local * self.msg_ld, self.msg_ld, self.msg_bytes, stream)
+        check(lib.mx_choco_apply(self.x.data_ptr(), self.x_hat.data_ptr(), self.s.data_ptr(), self.ld, P,
+                                 self.k, mbase, self.msg_ld, self.engine.plan.data_ptr(), int(it),
+                                 self.n_local, self.engine.M, self.engine.alpha32, self.gamma32, st),
+              "mx_choco_apply")
+        return True
+
+    def communicate(self):
+        it = self.iter
+        self.iter += 1
+        if np.sum(self.topology.active_flags[it]) == 0:
+            return 0
+        torch.cuda.synchronize()
+        tic = time.time()
+        self.step(it)
+        torch.cuda.synchronize()
+        return time.time() - tic

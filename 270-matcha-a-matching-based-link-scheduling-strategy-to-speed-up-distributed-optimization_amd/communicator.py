@@ -1,0 +1,214 @@
+"""Drop-in per-rank communicators (communicator.py:10-268 of the reference).
+
+    communicator = decenCommunicator(rank, size, GP)            # train_mpi.py:81
+    communicator = ChocoCommunicator(rank, size, GP, 0.9, lr)   # train_mpi.py:79
+    comm_time = communicator.communicate(model)                 # train_mpi.py:142
+
+One process per worker, as under mpirun.  The reference's MPI COMM_WORLD is replaced by
+torch.distributed (for bootstrap) plus an RCCL communicator owned by the native library; each
+rank's model is a one-row VirtualWorkerGroup / ChocoWorkerGroup on its GPU and partner rows
+travel over xGMI.  If torch.distributed is not initialised, it is initialised here from the
+environment (torchrun's RANK/WORLD_SIZE/MASTER_*, or the (rank, size) given, with
+MASTER_ADDR 127.0.0.1).
+
+Model parameters on the GPU are re-homed into the group's arena on the first call (views, so
+identity, shapes and optimizer references are kept) and mixed in place every round.  Models
+left on the CPU -- the reference's train_mpi.py keeps them there -- are staged: copied to the
+GPU row before and back after each round.  All arithmetic runs in the HIP kernels.
+"""
+import os
+import time
+
+import numpy as np
+import torch
+
+from ._lib import check, lib, require_device, stream_ptr
+from .choco import ChocoWorkerGroup
+from .comm_helpers import flatten_tensors, unflatten_tensors
+from .engine import VirtualWorkerGroup, default_comm
+
+
+def _same_params(model, params):
+    cur = list(model.parameters())
+    return params is not None and len(cur) == len(params) and all(a is b for a, b in zip(cur, params))
+
+
+def _ensure_process_group(rank, size):
+    import torch.distributed as dist
+    require_device()
+    if size > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        dist.init_process_group("gloo", rank=rank, world_size=size)
+    if size > 1:
+        if dist.get_world_size() != size or dist.get_rank() != rank:
+            raise RuntimeError(f"communicator rank/size ({rank}, {size}) do not match the process "
+                               f"group ({dist.get_rank()}, {dist.get_world_size()}): one process per worker")
+    if "LOCAL_RANK" in os.environ:
+        torch.cuda.set_device(int(os.environ["LOCAL_RANK"]))
+    elif size > 1:
+        torch.cuda.set_device(rank % torch.cuda.device_count())
+
+
+class _Staging:
+    """Moves a model's parameters into / out of a group row (device or host models)."""
+
+    def __init__(self, tensors, row):
+        self.tensors = tensors
+        self.row = row
+        self.on_gpu = all(t.device.type == "cuda" for t in tensors)
+
+    def load(self):
+        if not self.on_gpu:
+            flat = torch.cat([t.reshape(-1) for t in self.tensors]) if len(self.tensors) > 1 \
+                else self.tensors[0].reshape(-1)
+            self.row.copy_(flat, non_blocking=False)
+
+    def store(self):
+        if not self.on_gpu:
+            host = self.row.cpu()
+            with torch.no_grad():
+                for f, t in zip(unflatten_tensors(host, self.tensors), self.tensors):
+                    t.copy_(f)
+
+
+class Communicator(object):
+    """communicator.py:10-43 -- communicate(model) -> seconds spent averaging."""
+
+    def __init__(self, rank, size):
+        self.comm = None
+        self.rank = rank
+        self.size = size
+        _ensure_process_group(rank, size)
+
+    def communicate(self, model):
+        raise NotImplementedError
+
+
+class decenCommunicator(Communicator):
+    """communicator.py:79-158 -- decentralized averaging according to the topology's schedule."""
+
+    def __init__(self, rank, size, topology):
+        super(decenCommunicator, self).__init__(rank, size)
+        self.topology = topology
+        self.neighbor_weight = topology.neighbor_weight
+        self.iter = 0
+        self._group = None
+        self._stage = None
+        self._model_params = None
+
+    def _bind(self, model):
+        params = [p for p in model.parameters()]
+        on_gpu = all(p.device.type == "cuda" for p in params)
+        comm = default_comm() if self.size > 1 else None
+        if on_gpu:
+            self._group = VirtualWorkerGroup(self.topology, [model], rank=self.rank, nranks=self.size,
+                                             comm=comm)
+            self._stage = _Staging([p.data for p in params], self._group.rows[0])
+        else:
+            n = int(sum(p.numel() for p in params))
+            self._group = VirtualWorkerGroup(self.topology, numel=n, rank=self.rank, nranks=self.size,
+                                             comm=comm)
+            self._stage = _Staging([p.data for p in params], self._group.rows[0])
+        self._model_params = params
+
+    def communicate(self, model):
+        active_flags = self.topology.active_flags[self.iter]
+        it = self.iter
+        self.iter += 1
+        if np.sum(active_flags) == 0:            # communicator.py:140-141
+            return 0
+        if self._group is None or not _same_params(model, self._model_params):
+            self._bind(model)
+        else:
+            self._stage.tensors = [p.data for p in self._model_params]
+        self._stage.load()
+        torch.cuda.synchronize()
+        tic = time.time()
+        self._group.step(it)
+        torch.cuda.synchronize()
+        toc = time.time()
+        self._stage.store()
+        return toc - tic
+
+
+class ChocoCommunicator(Communicator):
+    """communicator.py:161-268 -- top-k compressed gossip with persistent x_hat / s."""
+
+    def __init__(self, rank, size, topology, ratio, consensus_lr):
+        super(ChocoCommunicator, self).__init__(rank, size)
+        self.topology = topology
+        self.neighbor_weight = topology.neighbor_weight
+        self.iter = 0
+        self.initialized = False
+        self.consensus_lr = consensus_lr
+        self.ratio = ratio
+        self._group = None
+        self._stage = None
+
+    @property
+    def x_hat(self):
+        return self._group.x_hat[0, :self._group.numel] if self._group is not None else None
+
+    @property
+    def s(self):
+        return self._group.s[0, :self._group.numel] if self._group is not None else None
+
+    def _bind(self, model):
+        params = [p for p in model.parameters()]
+        on_gpu = all(p.device.type == "cuda" for p in params)
+        comm = default_comm() if self.size > 1 else None
+        if on_gpu:
+            self._group = ChocoWorkerGroup(self.topology, [model], ratio=self.ratio,
+                                           consensus_lr=self.consensus_lr, rank=self.rank,
+                                           nranks=self.size, comm=comm)
+        else:
+            n = int(sum(p.numel() for p in params))
+            self._group = ChocoWorkerGroup(self.topology, numel=n, ratio=self.ratio,
+                                           consensus_lr=self.consensus_lr, rank=self.rank,
+                                           nranks=self.size, comm=comm)
+        self._stage = _Staging([p.data for p in params], self._group.rows[0])
+        self._model_params = params
+        self.initialized = True
+
+    def communicate(self, model):
+        active_flags = self.topology.active_flags[self.iter]
+        it = self.iter
+        self.iter += 1
+        if np.sum(active_flags) == 0:            # communicator.py:249-250
+            return 0
+        if self._group is None or not _same_params(model, self._model_params):
+            self._bind(model)
+        else:
+            self._stage.tensors = [p.data for p in self._model_params]
+        self._stage.load()
+        torch.cuda.synchronize()
+        tic = time.time()
+        self._group.step(it)
+        torch.cuda.synchronize()
+        toc = time.time()
+        self._stage.store()
+        return toc - tic
+
+
+class centralizedCommunicator(Communicator):
+    """communicator.py:46-76 -- all-reduce averaging: x = allreduce_sum(x) / size (RCCL)."""
+
+    def __init__(self, rank, size):
+        super(centralizedCommunicator, self).__init__(rank, size)
+
+    def communicate(self, model):
+        tensors = [p.data for p in model.parameters()]
+        on_gpu = all(t.device.type == "cuda" for t in tensors)
+        flat = flatten_tensors([t if on_gpu else t.cuda() for t in tensors])
+        torch.cuda.synchronize()
+        tic = time.time()
+        if self.size > 1:
+            check(lib.mx_allreduce_mean(default_comm().handle, flat.data_ptr(), flat.numel(), self.size,
+                                        stream_ptr()), "mx_allreduce_mean")
+        torch.cuda.synchronize()
+        toc = time.time()
+        with torch.no_grad():
+            for f, t in zip(unflatten_tensors(flat, tensors), tensors):
+                t.copy_(f)
+        return toc - tic

@@ -1,0 +1,24 @@
+"""Drop-in compressors (compressors.py:3-19 of the reference) on the GPU."""
+import torch
+
+from ._lib import check, lib, stream_ptr
+from .choco import topk_count
+
+
+def get_top_k(x, ratio):
+    """Top (1 - ratio) fraction of x by magnitude: k = max(1, int(len * (1 - ratio))).
+    Returns (x[indices], indices int64).  Indices come back in ascending order; among equal
+    magnitudes at the k-th threshold the lowest indices are kept (the reference's
+    torch.topk(sorted=False) / torch.max leave both unspecified)."""
+    x_data = x.view(-1)
+    if x_data.device.type != "cuda" or x_data.dtype != torch.float32:
+        raise TypeError("get_top_k runs on the GPU: a float32 CUDA tensor is required")
+    x_data = x_data.contiguous()
+    P = x_data.numel()
+    k = topk_count(P, ratio)
+    vals = torch.empty(k, dtype=torch.float32, device=x_data.device)
+    idx = torch.empty(k, dtype=torch.int64, device=x_data.device)
+    work = torch.empty(int(lib.mx_topk_work_bytes(P)), dtype=torch.uint8, device=x_data.device)
+    check(lib.mx_topk_abs_diff(x_data.data_ptr(), None, P, k, vals.data_ptr(), idx.data_ptr(),
+                               work.data_ptr(), stream_ptr()), "mx_topk_abs_diff")
+    return vals, idx

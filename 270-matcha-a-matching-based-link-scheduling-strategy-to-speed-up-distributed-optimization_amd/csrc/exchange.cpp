@@ -1,0 +1,128 @@
+// exchange.cpp -- cross-GPU transport over RCCL (xGMI within a node).
+//
+// The reference moves every active edge's full parameter vector with a pickled, blocking
+// comm.sendrecv in ascending matching order (communicator.py:99-112).  Here one process drives
+// one GPU holding a contiguous block of workers; per round, every active matching edge that
+// crosses GPUs becomes an ncclSend of the local row plus an ncclRecv of the partner's row into
+// a receive slab, all inside ONE ncclGroupStart/End so the <= 7 peers of a GPU stream over
+// their own xGMI links concurrently.  Edges inside a GPU are not moved at all: the mixing
+// kernel reads those rows straight from HBM.
+//
+// Posting order (both directions): matching ascending, then sender worker id ascending --
+// identical to the receive-slot numbering of plan_kernel (plan.hip), so slab slot k of the
+// round always holds the row the plan expects.  Sends to / receives from one peer pair up in
+// posting order, as RCCL point-to-point requires.
+#include <rccl/rccl.h>
+
+#include <vector>
+
+#include "mx_common.h"
+
+#define MX_NCCL(call)                                                                       \
+    do {                                                                                    \
+        ncclResult_t r_ = (call);                                                           \
+        if (r_ != ncclSuccess) {                                                            \
+            ::mx::set_error("%s:%d %s -> %s", __FILE__, __LINE__, #call, ncclGetErrorString(r_)); \
+            return MX_ERR_RCCL;                                                             \
+        }                                                                                   \
+    } while (0)
+
+static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is expected to be 128 bytes");
+
+extern "C" int mx_rccl_unique_id(void* id_out) {
+    MX_CHECK(id_out, "mx_rccl_unique_id: null pointer");
+    ncclUniqueId id;
+    MX_NCCL(ncclGetUniqueId(&id));
+    memcpy(id_out, &id, sizeof(id));
+    return MX_OK;
+}
+
+extern "C" int mx_rccl_init(const void* id, int nranks, int rank, void** comm_out) {
+    MX_CHECK(id && comm_out, "mx_rccl_init: null pointer");
+    MX_CHECK(nranks >= 1 && rank >= 0 && rank < nranks, "mx_rccl_init: rank %d of %d", rank, nranks);
+    ncclUniqueId uid;
+    memcpy(&uid, id, sizeof(uid));
+    ncclComm_t comm = nullptr;
+    MX_NCCL(ncclCommInitRank(&comm, nranks, uid, rank));
+    *comm_out = comm;
+    return MX_OK;
+}
+
+extern "C" int mx_rccl_destroy(void* comm) {
+    if (!comm) return MX_OK;
+    MX_NCCL(ncclCommDestroy(reinterpret_cast<ncclComm_t>(comm)));
+    return MX_OK;
+}
+
+extern "C" int mx_exchange_round(void* comm_v, const uint8_t* flags_row, int M,
+                                 const int32_t* partner, int n_global, const int32_t* owner,
+                                 int my_rank, int row_base, int n_local, void* const* rows,
+                                 void* slab, int64_t slab_ld_bytes, int64_t row_bytes,
+                                 int* n_remote_out, void* stream) {
+    MX_CHECK(comm_v && flags_row && partner && owner && rows, "mx_exchange_round: null pointer");
+    MX_CHECK(row_bytes > 0 && row_bytes % 4 == 0, "mx_exchange_round: row_bytes %lld", (long long)row_bytes);
+    ncclComm_t comm = reinterpret_cast<ncclComm_t>(comm_v);
+    hipStream_t st = mx::as_stream(stream);
+    auto is_local = [&](int w) { return w >= row_base && w < row_base + n_local; };
+
+    struct Op {
+        bool send;
+        int peer;
+        void* buf;
+    };
+    std::vector<Op> ops;
+    int remote = 0;
+    for (int g = 0; g < M; ++g) {
+        if (!flags_row[g]) continue;
+        for (int p = 0; p < n_global; ++p) {      // p = sender, ascending
+            const int q = partner[g * n_global + p];
+            if (q < 0) continue;
+            MX_CHECK(q < n_global && partner[g * n_global + q] == p,
+                     "mx_exchange_round: matching %d is not symmetric at %d", g, p);
+            const bool pl = is_local(p), ql = is_local(q);
+            if (pl && !ql) {                      // our row p goes to q's owner
+                ops.push_back({true, owner[q], rows[p - row_base]});
+            } else if (!pl && ql) {               // p's row comes into the next slab slot
+                MX_CHECK(slab, "mx_exchange_round: receive slab required");
+                ops.push_back({false, owner[p], static_cast<char*>(slab) + (int64_t)remote * slab_ld_bytes});
+                ++remote;
+            }
+        }
+    }
+    if (n_remote_out) *n_remote_out = remote;
+    if (ops.empty()) return MX_OK;
+    const size_t count = (size_t)(row_bytes / 4);
+    MX_NCCL(ncclGroupStart());
+    for (const Op& o : ops) {
+        MX_CHECK(o.peer >= 0 && o.peer != my_rank, "mx_exchange_round: bad peer %d", o.peer);
+        if (o.send) {
+            ncclResult_t r = ncclSend(o.buf, count, ncclFloat32, o.peer, comm, st);
+            if (r != ncclSuccess) { ncclGroupEnd(); mx::set_error("ncclSend: %s", ncclGetErrorString(r)); return MX_ERR_RCCL; }
+        } else {
+            ncclResult_t r = ncclRecv(o.buf, count, ncclFloat32, o.peer, comm, st);
+            if (r != ncclSuccess) { ncclGroupEnd(); mx::set_error("ncclRecv: %s", ncclGetErrorString(r)); return MX_ERR_RCCL; }
+        }
+    }
+    MX_NCCL(ncclGroupEnd());
+    return MX_OK;
+}
+
+namespace {
+__global__ void div_kernel(float* __restrict__ x, int64_t n, float d) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        x[i] = x[i] / d;
+}
+}  // namespace
+
+extern "C" int mx_allreduce_mean(void* comm_v, float* buf, int64_t count, int nranks, void* stream) {
+    MX_CHECK(comm_v && (buf || count == 0) && nranks >= 1, "mx_allreduce_mean: bad arguments");
+    if (count == 0) return MX_OK;
+    hipStream_t st = mx::as_stream(stream);
+    MX_NCCL(ncclAllReduce(buf, buf, (size_t)count, ncclFloat32, ncclSum,
+                          reinterpret_cast<ncclComm_t>(comm_v), st));
+    int64_t g = (count + 255) / 256;
+    if (g > 8192) g = 8192;
+    hipLaunchKernelGGL(div_kernel, dim3((unsigned)g), dim3(256), 0, st, buf, count, (float)nranks);
+    MX_LAUNCH_CHECK();
+    return MX_OK;
+}

@@ -1,0 +1,211 @@
+// mix.hip -- the hot path: one in-place decentralized averaging round over every local worker.
+//
+// Replaces, per round, decenCommunicator.prepare_comm_buffer / averaging / reset_model
+// (communicator.py:87-131) together with flatten_tensors / unflatten_tensors
+// (comm_helpers.py:12-56): the reference concatenates each worker's tensors, receives every
+// active partner's full vector, accumulates recv = fma(alpha, x_j, recv) in ascending matching
+// order, adds fma(1 - d*alpha, x_i, recv) and copies back.  Here the workers' tensors stay
+// where they are (a [nseg][n_slots] pointer table; one segment per tensor, or one segment per
+// flat arena row) and each 256-lane workgroup owns a column tile of EVERY slot:
+//
+//   1. stream the tile of each needed slot (local rows with degree > 0, received slab rows)
+//      from HBM into registers with 16-byte loads -- every byte read once;
+//   2. park them in a per-lane LDS column (LDS gives the data-dependent, wave-uniform row
+//      indexing of the partner walk; each lane reads only its own column: no barrier);
+//   3. per output row, run the reference FMA chain in matching order from LDS and store the
+//      tile back in place with 16-byte stores -- every byte written once.
+//
+// Traffic per round = 2 * n_active * P * 4 bytes (+ n_remote * P * 4 read of the slab): the
+// HBM roofline of the north star.  No MFMA: ~0.25 flop/byte.
+#include <stdlib.h>
+
+#include "mx_common.h"
+
+namespace {
+constexpr int kTPB = 256;
+constexpr int kMaxM = 32;
+
+template <int VEC>
+struct alignas(4 * VEC) FV {
+    float v[VEC];
+};
+
+template <int VEC, int NS>
+__global__ __launch_bounds__(kTPB) void mix_kernel(float* const* __restrict__ seg_ptrs,
+                                                   const int64_t* __restrict__ seg_len,
+                                                   const int64_t* __restrict__ tile_off,
+                                                   const uint8_t* __restrict__ seg_vec, int nseg,
+                                                   int64_t total_tiles, int n_slots, const int32_t* __restrict__ plan,
+                                                   int64_t iter, int n_local, int M, float alpha) {
+    using F = FV<VEC>;
+    constexpr int TILE = kTPB * VEC;
+    __shared__ F lds[NS][kTPB];
+    __shared__ int32_t sp[mx::kPlanHeader + 2 * NS + NS * kMaxM];
+
+    const int tid = threadIdx.x;
+    const int64_t W = mx::plan_words(n_local, M);
+    const int32_t* rec = plan + iter * W;
+    for (int i = tid; i < W; i += kTPB) sp[i] = rec[i];
+    __syncthreads();
+    if (sp[0] == 0) return;  // all flags zero: the reference returns before any I/O
+
+    const int n_remote = sp[1];
+    const int32_t* deg = sp + mx::kPlanHeader;
+    const float* sw = reinterpret_cast<const float*>(deg + n_local);
+    const int32_t* src = deg + 2 * n_local;
+    uint64_t need = 0;
+    for (int r = 0; r < n_local; ++r)
+        if (deg[r] > 0) need |= 1ull << r;
+    for (int k = 0; k < n_remote; ++k) need |= 1ull << (n_local + k);
+
+    for (int64_t tile = blockIdx.x; tile < total_tiles; tile += gridDim.x) {
+        int seg = 0;
+        if (nseg > 1) {
+            int lo = 0, hi = nseg;
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (tile_off[mid] <= tile) lo = mid; else hi = mid;
+            }
+            seg = lo;
+        }
+        const int64_t len = seg_len[seg];
+        const int64_t c = (tile - tile_off[seg]) * TILE + (int64_t)tid * VEC;
+        float* const* ptrs = seg_ptrs + (int64_t)seg * n_slots;
+        const bool full = (c + VEC <= len) && seg_vec[seg];
+
+        F v[NS];
+#pragma unroll
+        for (int k = 0; k < NS; ++k) {
+            if ((need >> k) & 1ull) {
+                const float* p = ptrs[k] + c;
+                if (full) {
+                    v[k] = *reinterpret_cast<const F*>(p);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < VEC; ++j) v[k].v[j] = (c + j < len) ? p[j] : 0.0f;
+                }
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NS; ++k)
+            if ((need >> k) & 1ull) lds[k][tid] = v[k];
+
+        for (int r = 0; r < n_local; ++r) {
+            const int d = deg[r];
+            if (d == 0) continue;
+            F acc;
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) acc.v[j] = 0.0f;
+            for (int e = 0; e < d; ++e) {
+                const F x = lds[src[r * M + e]][tid];
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) acc.v[j] = __builtin_fmaf(alpha, x.v[j], acc.v[j]);
+            }
+            const F xs = lds[r][tid];
+            const float s = sw[r];
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) acc.v[j] = __builtin_fmaf(s, xs.v[j], acc.v[j]);
+            float* p = ptrs[r] + c;
+            if (full) {
+                *reinterpret_cast<F*>(p) = acc;
+            } else {
+#pragma unroll
+                for (int j = 0; j < VEC; ++j)
+                    if (c + j < len) p[j] = acc.v[j];
+            }
+        }
+    }
+}
+
+struct Cfg {
+    int vec, ns;
+};
+
+Cfg pick(int n_slots) {
+    if (n_slots <= 8) return {4, 8};
+    if (n_slots <= 16) return {4, 16};
+    if (n_slots <= 32) return {2, 32};
+    if (n_slots <= 64) return {1, 64};
+    return {0, 0};
+}
+
+int blocks_per_cu() {
+    static int v = [] {
+        const char* e = getenv("MX_MIX_BLOCKS_PER_CU");
+        int x = e ? atoi(e) : 0;
+        return x > 0 ? x : 4;
+    }();
+    return v;
+}
+
+int cu_count() {
+    static int v = [] {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess) return 256;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 256;
+        return n > 0 ? n : 256;
+    }();
+    return v;
+}
+
+template <int VEC, int NS>
+int launch(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_off,
+           const uint8_t* seg_vec, int nseg, int n_slots, const int32_t* plan, int64_t iter,
+           int n_local, int M, float alpha, int64_t total_tiles, hipStream_t st) {
+    int64_t grid = (int64_t)cu_count() * blocks_per_cu();
+    if (grid > total_tiles) grid = total_tiles;
+    if (grid < 1) grid = 1;
+    hipLaunchKernelGGL((mix_kernel<VEC, NS>), dim3((unsigned)grid), dim3(kTPB), 0, st, seg_ptrs,
+                       seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan, iter, n_local,
+                       M, alpha);
+    MX_LAUNCH_CHECK();
+    return MX_OK;
+}
+}  // namespace
+
+extern "C" int mx_mix_tile(int n_slots) {
+    const Cfg c = pick(n_slots);
+    return c.vec * kTPB;
+}
+
+extern "C" int mx_mix_layout(const int64_t* seg_len_host, int nseg, int n_slots, int64_t* tile_off_host) {
+    MX_CHECK(seg_len_host && tile_off_host && nseg >= 1, "mx_mix_layout: bad arguments");
+    const int tile = mx_mix_tile(n_slots);
+    MX_CHECK(tile > 0, "mx_mix_layout: n_slots=%d exceeds 64", n_slots);
+    tile_off_host[0] = 0;
+    for (int s = 0; s < nseg; ++s) {
+        MX_CHECK(seg_len_host[s] >= 0, "mx_mix_layout: negative length");
+        tile_off_host[s + 1] = tile_off_host[s] + (seg_len_host[s] + tile - 1) / tile;
+    }
+    return MX_OK;
+}
+
+extern "C" int mx_gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev,
+                             const int64_t* tile_off_dev, const uint8_t* seg_vec_dev, int nseg,
+                             int64_t total_tiles, int n_slots, const int32_t* plan_dev,
+                             int64_t iter, int n_local, int M, float alpha, void* stream) {
+    MX_CHECK(seg_ptrs_dev && seg_len_dev && tile_off_dev && seg_vec_dev && plan_dev,
+             "mx_gossip_mix: null pointer");
+    MX_CHECK(nseg >= 1 && n_local >= 1 && n_slots >= n_local, "mx_gossip_mix: nseg=%d n_local=%d n_slots=%d",
+             nseg, n_local, n_slots);
+    MX_CHECK(M >= 1 && M <= kMaxM, "mx_gossip_mix: M=%d outside [1, %d]", M, kMaxM);
+    MX_CHECK(iter >= 0, "mx_gossip_mix: iter < 0");
+    const Cfg c = pick(n_slots);
+    MX_CHECK(c.vec > 0, "mx_gossip_mix: n_slots=%d exceeds 64", n_slots);
+    hipStream_t st = mx::as_stream(stream);
+    if (total_tiles <= 0) return MX_OK;
+    switch (c.ns) {
+        case 8:
+            return launch<4, 8>(seg_ptrs_dev, seg_len_dev, tile_off_dev, seg_vec_dev, nseg, n_slots,
+                                plan_dev, iter, n_local, M, alpha, total_tiles, st);
+        case 16:
+            return launch<4, 16>(seg_ptrs_dev, seg_len_dev, tile_off_dev, seg_vec_dev, nseg, n_slots,
+                                 plan_dev, iter, n_local, M, alpha, total_tiles, st);
+        case 32:
+            return launch<2, 32>(seg_ptrs_dev, seg_len_dev, tile_off_dev, seg_vec_dev, nseg, n_slots,
+                                 plan_dev, iter, n_local, M, alpha, total_tiles, st);
+        default:
+            return launch<1, 64>(seg_ptrs_dev, seg_len_dev, tile_off_dev, seg_vec_dev, nseg, n_slots,
+                                 plan_dev, iter, n_local, M, alpha, total_tiles, st);
+    }
+}

@@ -1,0 +1,71 @@
+// plan.hip -- per-iteration round plans, built on the GPU from the device-resident flag table.
+//
+// Restates the neighbour walk of decenCommunicator.averaging (communicator.py:99-117) once per
+// iteration, for all iterations in parallel (one lane per iteration):
+//     for graph_id, flag in enumerate(active_flags):              # ascending matchings
+//         if flag and neighbors_info[graph_id][rank] != -1: degree += 1; use that partner
+//     selfweight = 1 - degree * alpha
+// For each local row the record lists its partners' slots in matching order, so the mixing
+// kernel reproduces the reference's FMA order exactly.  Partners owned by another rank are
+// given receive-slab slots in (matching asc, sender id asc) order, the order in which
+// mx_exchange_round (exchange.cpp) posts its RCCL receives.
+#include "mx_common.h"
+
+namespace {
+__global__ __launch_bounds__(256) void plan_kernel(const uint8_t* __restrict__ flags, int64_t T,
+                                                   int M, const int32_t* __restrict__ partner,
+                                                   int n, int row_base, int n_local, double alpha,
+                                                   int32_t* __restrict__ plan) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= T) return;
+    const int64_t W = mx::plan_words(n_local, M);
+    int32_t* rec = plan + t * W;
+    const uint8_t* f = flags + t * M;
+    int32_t* deg = rec + mx::kPlanHeader;
+    int32_t* sw = deg + n_local;
+    int32_t* src = sw + n_local;
+    for (int r = 0; r < n_local; ++r) deg[r] = 0;
+    int any = 0, remote = 0;
+    for (int g = 0; g < M; ++g) {
+        if (!f[g]) continue;
+        any = 1;
+        for (int p = 0; p < n; ++p) {          // p = sender, ascending
+            const int q = partner[g * n + p];  // receiver
+            if (q < row_base || q >= row_base + n_local) continue;
+            const int r = q - row_base;
+            const bool p_local = (p >= row_base && p < row_base + n_local);
+            const int slot = p_local ? p - row_base : n_local + remote++;
+            src[r * M + deg[r]] = slot;
+            deg[r] += 1;
+        }
+    }
+    rec[0] = any;
+    rec[1] = remote;
+    rec[2] = 0;
+    rec[3] = 0;
+    for (int r = 0; r < n_local; ++r) {
+        const double s = 1.0 - (double)deg[r] * alpha;  // Python float arithmetic, then f32
+        const float s32 = (float)s;
+        sw[r] = __float_as_int(s32);
+    }
+}
+}  // namespace
+
+extern "C" int64_t mx_plan_words(int n_local, int M) { return mx::plan_words(n_local, M); }
+
+extern "C" int mx_plan_build(const uint8_t* flags_dev, int64_t T, int M, const int32_t* partner_dev,
+                             int n_global, const int32_t* owner_dev, int my_rank, int row_base,
+                             int n_local, double alpha, int32_t* plan_dev, void* stream) {
+    (void)owner_dev;  // local rows are the contiguous block [row_base, row_base + n_local)
+    (void)my_rank;
+    MX_CHECK(flags_dev && partner_dev && plan_dev, "mx_plan_build: null pointer");
+    MX_CHECK(M >= 1 && T >= 0 && n_global >= 1, "mx_plan_build: M=%d T=%lld n=%d", M, (long long)T, n_global);
+    MX_CHECK(n_local >= 1 && row_base >= 0 && row_base + n_local <= n_global,
+             "mx_plan_build: local block [%d, %d) outside [0, %d)", row_base, row_base + n_local, n_global);
+    if (T == 0) return MX_OK;
+    const int64_t grid = (T + 255) / 256;
+    hipLaunchKernelGGL(plan_kernel, dim3((unsigned)grid), dim3(256), 0, mx::as_stream(stream),
+                       flags_dev, T, M, partner_dev, n_global, row_base, n_local, alpha, plan_dev);
+    MX_LAUNCH_CHECK();
+    return MX_OK;
+}

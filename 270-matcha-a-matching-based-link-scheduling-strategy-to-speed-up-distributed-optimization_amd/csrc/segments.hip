@@ -1,0 +1,100 @@
+// segments.hip -- multi-tensor flatten / unflatten and the synthetic-input generator.
+//
+// mx_gather  = comm_helpers.flatten_tensors (comm_helpers.py:12-30): torch.cat of T tensors.
+// mx_scatter = reset_model's `t.copy_(f)` over unflatten_tensors views
+//              (communicator.py:124-131, comm_helpers.py:33-56).
+// One launch moves every tensor: 1024-element tiles of the flat index space, the owning tensor
+// found once per tile by binary search over the offset table and then walked forward, so small
+// tensors (biases) share tiles.  Not on the per-round path when the mixing kernel reads tensors
+// in place; used by flatten_tensors on device tensors and by host-staged models.
+#include "mx_common.h"
+
+namespace {
+constexpr int kTPB = 256;
+constexpr int kPer = 4;  // elements per lane per tile
+constexpr int64_t kTile = (int64_t)kTPB * kPer;
+
+__device__ __forceinline__ int find_seg(const int64_t* off, int nseg, int64_t i) {
+    int lo = 0, hi = nseg;  // largest s with off[s] <= i
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (off[mid] <= i) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+template <bool kGather>
+__global__ __launch_bounds__(kTPB) void seg_copy_kernel(float* const* __restrict__ ptrs,
+                                                        const int64_t* __restrict__ off, int nseg,
+                                                        int64_t total, float* __restrict__ flat) {
+    __shared__ int s_first;
+    for (int64_t t0 = (int64_t)blockIdx.x * kTile; t0 < total; t0 += (int64_t)gridDim.x * kTile) {
+        if (threadIdx.x == 0) s_first = find_seg(off, nseg, t0);
+        __syncthreads();
+        int s = s_first;
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            const int64_t i = t0 + (int64_t)j * kTPB + threadIdx.x;  // coalesced across lanes
+            if (i < total) {
+                while (off[s + 1] <= i) ++s;
+                const int64_t k = i - off[s];
+                if (kGather) flat[i] = ptrs[s][k];
+                else ptrs[s][k] = flat[i];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kTPB) void synth_kernel(float* __restrict__ dst, int64_t n, uint64_t seed) {
+    for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kTPB) {
+        uint64_t z = seed + (uint64_t)(i + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        dst[i] = (float)(z >> 40) * (1.0f / 8388608.0f) - 1.0f;
+    }
+}
+
+unsigned grid_for(int64_t total) {
+    int64_t g = (total + kTile - 1) / kTile;
+    if (g > 4096) g = 4096;
+    if (g < 1) g = 1;
+    return (unsigned)g;
+}
+}  // namespace
+
+extern "C" int mx_gather(const float* const* ptrs_dev, const int64_t* off_dev, int nseg,
+                         int64_t total, float* flat, void* stream) {
+    MX_CHECK(nseg >= 1 && total >= 0, "mx_gather: nseg=%d total=%lld", nseg, (long long)total);
+    if (total == 0) return MX_OK;
+    MX_CHECK(ptrs_dev && off_dev && flat, "mx_gather: null pointer");
+    hipLaunchKernelGGL(seg_copy_kernel<true>, dim3(grid_for(total)), dim3(kTPB), 0,
+                       mx::as_stream(stream), const_cast<float* const*>(ptrs_dev), off_dev, nseg,
+                       total, flat);
+    MX_LAUNCH_CHECK();
+    return MX_OK;
+}
+
+extern "C" int mx_scatter(float* const* ptrs_dev, const int64_t* off_dev, int nseg, int64_t total,
+                          const float* flat, void* stream) {
+    MX_CHECK(nseg >= 1 && total >= 0, "mx_scatter: nseg=%d total=%lld", nseg, (long long)total);
+    if (total == 0) return MX_OK;
+    MX_CHECK(ptrs_dev && off_dev && flat, "mx_scatter: null pointer");
+    hipLaunchKernelGGL(seg_copy_kernel<false>, dim3(grid_for(total)), dim3(kTPB), 0,
+                       mx::as_stream(stream), ptrs_dev, off_dev, nseg, total,
+                       const_cast<float*>(flat));
+    MX_LAUNCH_CHECK();
+    return MX_OK;
+}
+
+extern "C" int mx_synth_fill(float* dst, int64_t n, uint64_t seed, void* stream) {
+    MX_CHECK(n >= 0, "mx_synth_fill: n < 0");
+    if (n == 0) return MX_OK;
+    MX_CHECK(dst, "mx_synth_fill: null pointer");
+    int64_t g = (n + kTPB - 1) / kTPB;
+    if (g > 8192) g = 8192;
+    hipLaunchKernelGGL(synth_kernel, dim3((unsigned)g), dim3(kTPB), 0, mx::as_stream(stream), dst, n, seed);
+    MX_LAUNCH_CHECK();
+    return MX_OK;
+}

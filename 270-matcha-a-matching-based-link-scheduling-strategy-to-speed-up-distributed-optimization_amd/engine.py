@@ -1,0 +1,292 @@
+"""Gossip engine: the device-resident schedule, round plans, worker layout and transport.
+
+One process drives one GPU and a contiguous block of the topology's workers
+(rows [row_base, row_base + n_local)).  With one process (the "virtual worker" mode) the
+block is every worker; with N processes (torch.distributed, one per GPU) the workers are split
+into N contiguous blocks and edges that cross blocks go over RCCL (xGMI).
+
+Per round (reference: decenCommunicator.communicate, communicator.py:133-158):
+    1. [N > 1] mx_exchange_round: one ncclGroupStart/End with a send of every local row whose
+       active partner is remote and a receive of every remote partner row into the slab;
+    2. mx_gossip_mix: the in-place FMA-chain mixing kernel over local rows + slab rows, driven
+       by the precomputed plan record of this iteration.
+Everything is enqueued on one HIP stream; nothing is copied to or from the host per round.
+"""
+import ctypes
+import time
+
+import numpy as np
+import torch
+
+from ._lib import MXError, check, lib, require_device, stream_ptr
+
+ROW_ALIGN = 64  # arena rows padded to 256 B
+
+
+def partition(n, nranks):
+    """Contiguous worker blocks [(row_base, n_local)] per rank (sizes differ by at most 1)."""
+    base, extra = divmod(n, nranks)
+    out, start = [], 0
+    for r in range(nranks):
+        cnt = base + (1 if r < extra else 0)
+        out.append((start, cnt))
+        start += cnt
+    return out
+
+
+def owner_table(n, nranks):
+    own = np.empty(n, np.int32)
+    for r, (b, c) in enumerate(partition(n, nranks)):
+        own[b:b + c] = r
+    return own
+
+
+def validate_partner(partner):
+    """The drawer's table must describe matchings: symmetric, in range (graph_manager.py:157-180)."""
+    M, n = partner.shape
+    for g in range(M):
+        for i in range(n):
+            j = int(partner[g, i])
+            if j == -1:
+                continue
+            if not (0 <= j < n) or j == i or int(partner[g, j]) != i:
+                raise ValueError(f"neighbors_info[{g}] is not a matching at worker {i} -> {j}")
+
+
+def max_incoming_remote(partner, row_base, n_local):
+    """Receive-slab rows needed when every matching is active (upper bound over all rounds)."""
+    M, n = partner.shape
+    cnt = 0
+    for g in range(M):
+        for p in range(n):
+            q = int(partner[g, p])
+            if q < 0:
+                continue
+            if row_base <= q < row_base + n_local and not (row_base <= p < row_base + n_local):
+                cnt += 1
+    return cnt
+
+
+class RcclComm:
+    """An RCCL communicator owned by the C library (one per process), bootstrapped through
+    torch.distributed (which must be initialised; any backend) for the unique-id broadcast."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        require_device()
+        self.rank = dist.get_rank(group)
+        self.nranks = dist.get_world_size(group)
+        uid = (ctypes.c_char * 128)()
+        if self.rank == 0:
+            check(lib.mx_rccl_unique_id(ctypes.cast(uid, ctypes.c_void_p)), "mx_rccl_unique_id")
+        obj = [bytes(uid)]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        buf = (ctypes.c_char * 128).from_buffer_copy(obj[0])
+        h = ctypes.c_void_p()
+        check(lib.mx_rccl_init(ctypes.cast(buf, ctypes.c_void_p), self.nranks, self.rank,
+                               ctypes.byref(h)), "mx_rccl_init")
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            lib.mx_rccl_destroy(self.handle)
+            self.handle = None
+
+
+_DEFAULT_COMM = None
+
+
+def default_comm():
+    """Process-wide RCCL communicator over the default torch.distributed group."""
+    global _DEFAULT_COMM
+    if _DEFAULT_COMM is None:
+        _DEFAULT_COMM = RcclComm()
+    return _DEFAULT_COMM
+
+
+def topology_flags(topology):
+    """Device flag table uint8 [T][M] of a processor, consistent with its host active_flags."""
+    host = np.asarray(topology.active_flags, dtype=np.uint8)
+    if host.ndim != 2:
+        raise ValueError("active_flags must be a rectangular [iterations][matchings] table")
+    dev = getattr(topology, "flags_dev", None)
+    if dev is not None and tuple(dev.shape) == host.shape:
+        if np.array_equal(dev.cpu().numpy(), host):
+            return dev, host
+    return torch.from_numpy(np.ascontiguousarray(host)).to("cuda"), host
+
+
+class Layout:
+    """Pointer table of the mixing kernel: slot k's copy of segment s (include/matcha_gossip.h)."""
+
+    def __init__(self, seg_lens, slot_ptrs, n_slots):
+        nseg = len(seg_lens)
+        seg_len = np.asarray(seg_lens, dtype=np.int64)
+        table = np.zeros((nseg, n_slots), dtype=np.int64)
+        vec = np.ones(nseg, dtype=np.uint8)
+        for k, ptrs in enumerate(slot_ptrs):
+            for s in range(nseg):
+                table[s, k] = ptrs[s]
+                if ptrs[s] % 16:
+                    vec[s] = 0
+        tile_off = np.zeros(nseg + 1, dtype=np.int64)
+        check(lib.mx_mix_layout(seg_len.ctypes.data, nseg, n_slots, tile_off.ctypes.data), "mx_mix_layout")
+        self.nseg = nseg
+        self.n_slots = n_slots
+        self.total_tiles = int(tile_off[-1])
+        self.seg_ptrs = torch.from_numpy(table).to("cuda")
+        self.seg_len = torch.from_numpy(seg_len).to("cuda")
+        self.tile_off = torch.from_numpy(tile_off).to("cuda")
+        self.seg_vec = torch.from_numpy(vec).to("cuda")
+
+
+class GossipEngine:
+    """Schedule + plans for one block of workers of a FixedProcessor / MatchaProcessor."""
+
+    def __init__(self, topology, row_base=0, n_local=None, comm=None, owner=None):
+        require_device()
+        self.topology = topology
+        self.n = int(topology.size)
+        partner_all = np.asarray(topology.neighbors_info, dtype=np.int32).reshape(-1, self.n)
+        self.flags_dev, self.flags_host = topology_flags(topology)
+        self.T, self.M = self.flags_host.shape
+        if self.M > partner_all.shape[0]:
+            raise IndexError(f"active_flags has {self.M} columns but only {partner_all.shape[0]} "
+                             "matchings exist (neighbors_info[graph_id] would fail)")
+        self.partner = np.ascontiguousarray(partner_all[:self.M])
+        validate_partner(self.partner)
+        self.alpha = float(topology.neighbor_weight)
+        self.alpha32 = float(np.float32(self.alpha))
+        self.row_base = int(row_base)
+        self.n_local = self.n if n_local is None else int(n_local)
+        self.comm = comm
+        self.rank = comm.rank if comm is not None else 0
+        self.owner = (np.zeros(self.n, np.int32) if owner is None
+                      else np.ascontiguousarray(owner, dtype=np.int32))
+        self.max_remote = max_incoming_remote(self.partner, self.row_base, self.n_local)
+        if self.max_remote and comm is None:
+            raise ValueError("workers outside this block have partners inside it: an RCCL "
+                             "communicator is required")
+        self.n_slots = self.n_local + self.max_remote
+        if self.n_slots > 64:
+            raise MXError(f"{self.n_slots} slots per GPU exceed the mixing kernel's 64")
+        if self.M > 32:
+            raise MXError(f"{self.M} matchings exceed the mixing kernel's 32")
+        self.plan_words = int(lib.mx_plan_words(self.n_local, self.M))
+        self.partner_dev = torch.from_numpy(self.partner).to("cuda")
+        self.plan = torch.empty(max(1, self.T) * self.plan_words, dtype=torch.int32, device="cuda")
+        check(lib.mx_plan_build(self.flags_dev.data_ptr(), self.T, self.M, self.partner_dev.data_ptr(),
+                                self.n, None, self.rank, self.row_base, self.n_local, self.alpha,
+                                self.plan.data_ptr(), stream_ptr()), "mx_plan_build")
+        self.any_active = self.flags_host.any(axis=1)
+
+    # ------------------------------------------------------------------ per round
+    def exchange(self, it, row_ptrs, slab_ptr, slab_ld_bytes, row_bytes, stream=None):
+        """RCCL sends/receives of iteration `it` (no-op with one process)."""
+        if self.comm is None:
+            return 0
+        row_arr = (ctypes.c_void_p * self.n_local)(*row_ptrs)
+        nrem = ctypes.c_int(0)
+        fr = np.ascontiguousarray(self.flags_host[it])
+        check(lib.mx_exchange_round(self.comm.handle, fr.ctypes.data, self.M, self.partner.ctypes.data,
+                                    self.n, self.owner.ctypes.data, self.rank, self.row_base,
+                                    self.n_local, row_arr, slab_ptr, int(slab_ld_bytes), int(row_bytes),
+                                    ctypes.byref(nrem), stream_ptr(stream)), "mx_exchange_round")
+        return nrem.value
+
+    def mix(self, it, layout, stream=None):
+        check(lib.mx_gossip_mix(layout.seg_ptrs.data_ptr(), layout.seg_len.data_ptr(),
+                                layout.tile_off.data_ptr(), layout.seg_vec.data_ptr(), layout.nseg,
+                                layout.total_tiles, layout.n_slots, self.plan.data_ptr(), int(it),
+                                self.n_local, self.M, self.alpha32, stream_ptr(stream)),
+              "mx_gossip_mix")
+
+
+def _params(model):
+    return [p for p in model.parameters()]
+
+
+class VirtualWorkerGroup:
+    """A block of the topology's workers resident on this process's GPU as rows of an
+    [n_local, P] HBM arena (the "all virtual workers on one MI355X" mode, and each rank's share
+    in the multi-GPU mode).
+
+    models  -- optional list of n_local torch modules on the GPU (identical architectures);
+               with adopt=True their parameters are re-homed into the arena as views (identity
+               and shapes kept, so optimizers stay valid) and every round mixes them in place.
+    numel   -- arena width when no models are given (synthetic workloads / benchmarks).
+    """
+
+    def __init__(self, topology, models=None, numel=None, *, rank=0, nranks=1, comm=None, adopt=True):
+        require_device()
+        n = int(topology.size)
+        blocks = partition(n, nranks)
+        self.row_base, self.n_local = blocks[rank]
+        if nranks > 1 and comm is None:
+            comm = default_comm()
+        self.engine = GossipEngine(topology, self.row_base, self.n_local, comm=comm,
+                                   owner=owner_table(n, nranks))
+        self.topology = topology
+        self.iter = 0
+        if models is not None:
+            if len(models) != self.n_local:
+                raise ValueError(f"{len(models)} models for {self.n_local} local workers")
+            shapes = [tuple(p.shape) for p in _params(models[0])]
+            for m in models[1:]:
+                if [tuple(p.shape) for p in _params(m)] != shapes:
+                    raise ValueError("all workers must share one architecture")
+            self.numel = int(sum(p.numel() for p in _params(models[0])))
+        else:
+            if numel is None:
+                raise ValueError("give models or numel")
+            self.numel = int(numel)
+        self.ld = (self.numel + ROW_ALIGN - 1) // ROW_ALIGN * ROW_ALIGN
+        self.arena = torch.zeros((self.n_local, self.ld), dtype=torch.float32, device="cuda")
+        self.slab = (torch.empty((self.engine.max_remote, self.ld), dtype=torch.float32, device="cuda")
+                     if self.engine.max_remote else None)
+        if models is not None:
+            for r, m in enumerate(models):
+                off = 0
+                for p in _params(m):
+                    if p.dtype != torch.float32 or p.device.type != "cuda":
+                        raise TypeError("worker parameters must be float32 CUDA tensors")
+                    k = p.numel()
+                    view = self.arena[r, off:off + k].view(p.shape)
+                    view.copy_(p.data)
+                    if adopt:
+                        p.data = view
+                    off += k
+        slot_ptrs = [[self.arena[r].data_ptr()] for r in range(self.n_local)]
+        if self.slab is not None:
+            slot_ptrs += [[self.slab[k].data_ptr()] for k in range(self.engine.max_remote)]
+        self.layout = Layout([self.numel], slot_ptrs, self.engine.n_slots)
+        self._row_ptrs = [self.arena[r].data_ptr() for r in range(self.n_local)]
+
+    @property
+    def rows(self):
+        """[n_local, P] view of the workers' flat parameter vectors."""
+        return self.arena[:, :self.numel]
+
+    def step(self, it, stream=None):
+        """Enqueue round `it` (exchange + mix) on `stream`; returns False for an all-zero round."""
+        if not self.engine.any_active[it]:
+            return False
+        if self.engine.comm is not None:
+            self.engine.exchange(it, self._row_ptrs,
+                                 self.slab.data_ptr() if self.slab is not None else None,
+                                 self.ld * 4, self.numel * 4, stream)
+        self.engine.mix(it, self.layout, stream)
+        return True
+
+    def communicate(self):
+        """One round at the group's own iteration counter; returns seconds like the reference's
+        communicate() (0 for a skipped round)."""
+        it = self.iter
+        self.iter += 1
+        if np.sum(self.topology.active_flags[it]) == 0:
+            return 0
+        torch.cuda.synchronize()
+        tic = time.time()
+        self.step(it)
+        torch.cuda.synchronize()
+        return time.time() - tic

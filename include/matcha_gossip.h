@@ -1,0 +1,166 @@
+/*
+ * matcha_gossip.h -- C ABI of the MI355X (gfx950) gossip hot path.
+ *
+ * Plain pointers and sizes only.  "dev" pointers are HIP device pointers; "host" pointers are
+ * ordinary host memory.  `stream` is a hipStream_t passed as void* (0 = legacy default).
+ * Every entry point returns MX_OK (0) or a negative MX_ERR_* code; mx_last_error() returns
+ * a thread-local message describing the last failure.
+ *
+ * The reference is pure Python over mpi4py.  Each entry point names the
+ * reference function(s) it replaces; the binding a maintainer would add on the reference side
+ * (a ctypes stub) is in INTEGRATION.md.
+ */
+#ifndef MATCHA_GOSSIP_H
+#define MATCHA_GOSSIP_H
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MX_OK 0
+#define MX_ERR_INVALID (-1)   /* bad argument (shape, alignment, range)               */
+#define MX_ERR_HIP (-2)       /* HIP runtime error                                     */
+#define MX_ERR_RCCL (-3)      /* RCCL error                                            */
+#define MX_ERR_RNG (-4)       /* MT19937 word stream exhausted by resample events      */
+#define MX_ERR_UNSUPPORTED (-5)
+
+/* ---------------------------------------------------------------- library */
+const char* mx_version(void);
+const char* mx_last_error(void);
+
+/* ---------------------------------------------------------------- schedule (L2)
+ * Per-iteration activation flags on the GPU, bit-exact with numpy's legacy global RNG.
+ *
+ * mx_flags_binomial replaces MatchaProcessor.set_flags (graph_manager.py:298-309):
+ *   for m in 0..M-1: flags[:, m] = np.random.binomial(1, p[m], T)   (matching-major draws)
+ * and, with M == 1 and the output ignored, the discarded draw of FixedProcessor.set_flags
+ * (graph_manager.py:213).
+ *   key_in/pos_in   numpy MT19937 state (np.random.get_state()[1:3]) before the draws (host)
+ *   p               activation probabilities (host, float64[M]); NaN / negative -> 0 as
+ *                   graph_manager.py:305-306 does; values > 1 are rejected
+ *   flags_dev       uint8 [T][M] output, row t = active_flags[t]
+ *   key_out/pos_out MT19937 state after the draws (host) -- hand back to np.random.set_state
+ * Blocking (synchronises `stream`).
+ */
+int mx_flags_binomial(const uint32_t* key_in, int pos_in, const double* p, int M, int64_t T,
+                      uint8_t* flags_dev, uint32_t* key_out, int* pos_out, void* stream);
+
+/* Same, but forces the sequential (resample-aware) walk; used by tests to pin the fix-up path. */
+int mx_flags_binomial_sequential(const uint32_t* key_in, int pos_in, const double* p, int M,
+                                 int64_t T, uint8_t* flags_dev, uint32_t* key_out, int* pos_out,
+                                 void* stream);
+
+/* ---------------------------------------------------------------- round plans
+ * Precomputes, for every iteration t of a device-resident flag table, the per-row neighbour
+ * walk of decenCommunicator.averaging (communicator.py:99-117): for each local row r
+ * (global worker row_base + r) the source slots of its active partners in ascending matching
+ * order, its degree and selfweight f32(1 - degree * alpha).  Partners held by another rank
+ * get receive-slab slots numbered in (matching asc, sender id asc) order -- the same order
+ * mx_exchange_round posts its RCCL receives in.
+ *   partner_dev  int32 [M][n_global]   (GraphProcessor.neighbors_info, graph_manager.py:157-180)
+ *   owner_dev    int32 [n_global]      rank owning each worker; NULL = all local
+ *   plan_dev     int32 [T][mx_plan_words(n_local, M)]
+ * Plan record layout (int32 words): [0] any flag set, [1] n_remote, [2..3] reserved,
+ *   [4, 4+n_local) degree, [4+n_local, 4+2n_local) selfweight (f32 bits),
+ *   [4+2n_local + r*M + e] source slot of row r's e-th partner (slot < n_local: local row,
+ *   slot >= n_local: receive slab row slot - n_local).
+ */
+int64_t mx_plan_words(int n_local, int M);
+int mx_plan_build(const uint8_t* flags_dev, int64_t T, int M, const int32_t* partner_dev,
+                  int n_global, const int32_t* owner_dev, int my_rank, int row_base,
+                  int n_local, double alpha, int32_t* plan_dev, void* stream);
+
+/* ---------------------------------------------------------------- the hot path
+ * One decentralized averaging round, in place, for every local worker:
+ *   y_r = fma(f32(1-d_r*alpha), x_r, fma(f32(alpha), x_{j_d}, ... fma(f32(alpha), x_{j_1}, 0)))
+ * with the partners j_1..j_d in ascending matching order -- decenCommunicator.averaging +
+ * prepare_comm_buffer + reset_model (communicator.py:87-131), with flatten_tensors /
+ * unflatten_tensors (comm_helpers.py:12-56) fused away: the kernel reads and writes the
+ * workers' tensors where they live.
+ *   seg_ptrs_dev  float* [nseg][n_slots] device table: worker slot k's copy of tensor s.
+ *                 Slots [0, n_local) are the local workers (read + written in place);
+ *                 slots [n_local, n_slots) are receive-slab rows (read only).
+ *   seg_len_dev   int64 [nseg] floats per tensor;  tile_off_dev int64 [nseg+1] prefix of
+ *                 ceil(len / mx_mix_tile(n_slots)) per tensor (see mx_mix_layout);
+ *                 total_tiles = tile_off[nseg] (host copy, sizes the grid)
+ *   seg_vec_dev   uint8 [nseg]: 1 if every slot pointer of that tensor is 16-byte aligned
+ *   plan_dev      plan table from mx_plan_build; iter selects the record
+ * Rows with degree 0 are neither read nor written.  No-op when the record's flags are all 0.
+ */
+int mx_mix_tile(int n_slots);
+int mx_mix_layout(const int64_t* seg_len_host, int nseg, int n_slots, int64_t* tile_off_host);
+int mx_gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev,
+                  const int64_t* tile_off_dev, const uint8_t* seg_vec_dev, int nseg,
+                  int64_t total_tiles, int n_slots, const int32_t* plan_dev, int64_t iter,
+                  int n_local, int M, float alpha, void* stream);
+
+/* ---------------------------------------------------------------- flatten / unflatten
+ * mx_gather replaces flatten_tensors (comm_helpers.py:12-30): flat[off[s] + i] = src[s][i].
+ * mx_scatter is the copy_ loop of reset_model over unflatten_tensors views
+ * (communicator.py:124-131, comm_helpers.py:33-56): dst[s][i] = flat[off[s] + i].
+ *   ptrs_dev  float* [nseg] device;  off_dev int64 [nseg+1] device (off[nseg] = total)
+ */
+int mx_gather(const float* const* ptrs_dev, const int64_t* off_dev, int nseg, int64_t total,
+              float* flat, void* stream);
+int mx_scatter(float* const* ptrs_dev, const int64_t* off_dev, int nseg, int64_t total,
+               const float* flat, void* stream);
+
+/* ---------------------------------------------------------------- ChocoSGD (compressors.py)
+ * mx_topk_abs_diff: q = topk(|x - x_hat|, k) of compressors.get_top_k (compressors.py:3-19)
+ * applied to the send buffer of ChocoCommunicator.prepare_comm_buffer (communicator.py:188-190).
+ * Writes vals[k] = (x - x_hat)[idx] and idx[k] (int64) sorted by index.  Among equal
+ * magnitudes at the k-th threshold the lowest indices are taken (torch.topk(sorted=False)
+ * leaves that unspecified).  x_hat may be NULL (treated as zeros: get_top_k on x itself).
+ * `work` is a device scratch of mx_topk_work_bytes(P) bytes.
+ */
+size_t mx_topk_work_bytes(int64_t P);
+int mx_topk_abs_diff(const float* x, const float* x_hat, int64_t P, int64_t k, float* vals,
+                     int64_t* idx, void* work, void* stream);
+
+/* ChocoCommunicator.averaging (communicator.py:200-230) for one round of n_local workers,
+ * in place on the state rows (a round whose flags are all zero must not be applied):
+ *   for each partner j of row r (ascending matching): s_r[idx_j] = s_r[idx_j] + f32(alpha)*v_j
+ *   s_r[idx_r] += f32(1-d*alpha) * v_r ; x_hat_r[idx_r] += v_r
+ *   x_r = fma(gamma, s_r, x_r) ; x_r = fma(-gamma, x_hat_r, x_r)
+ *   x/xhat/s  float [n_local][P] rows with stride ld (floats)
+ *   msgs      compressed messages, one per plan slot, msg_ld_bytes apart: slot k holds
+ *             vals float[k] at +0 and idx int64[k] at +4*round_up(k, 2) (mx_choco_msg_bytes);
+ *             slots [0, n_local) are the local rows' own messages, the rest received ones
+ */
+int64_t mx_choco_msg_bytes(int64_t k);
+int mx_choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t k,
+                   const void* msgs, int64_t msg_ld_bytes, const int32_t* plan_dev, int64_t iter,
+                   int n_local, int M, float alpha, float gamma, void* stream);
+
+/* ---------------------------------------------------------------- cross-GPU exchange (RCCL)
+ * One process per GPU; workers partitioned by owner[].  mx_exchange_round posts, inside one
+ * ncclGroupStart/End, an ncclSend of every local row whose active partner lives on another
+ * rank and an ncclRecv of every remote partner row into the receive slab -- the pairwise
+ * comm.sendrecv of decenCommunicator.averaging (communicator.py:110) over xGMI.
+ * Order: matching ascending, then sender worker id ascending (matches mx_plan_build).
+ *   flags_row  uint8 [M] host;  partner int32 [M][n_global] host;  owner int32 [n_global] host
+ *   rows       device float* [n_local] (host array of device pointers), P floats each
+ *   slab       device base; slot k at slab + k * slab_ld
+ *   elem_bytes 4 for fp32 rows; also used with 12-byte Choco messages (values + int64 idx)
+ */
+int mx_rccl_unique_id(void* id_out /* 128 bytes */);
+int mx_rccl_init(const void* id /* 128 bytes */, int nranks, int rank, void** comm_out);
+int mx_rccl_destroy(void* comm);
+int mx_exchange_round(void* comm, const uint8_t* flags_row, int M, const int32_t* partner,
+                      int n_global, const int32_t* owner, int my_rank, int row_base, int n_local,
+                      void* const* rows, void* slab, int64_t slab_ld_bytes, int64_t row_bytes,
+                      int* n_remote_out, void* stream);
+/* centralizedCommunicator.averaging (communicator.py:56-67): buf = allreduce_sum(buf) / size */
+int mx_allreduce_mean(void* comm, float* buf, int64_t count, int nranks, void* stream);
+
+/* ---------------------------------------------------------------- utilities
+ * splitmix64 -> fp32 uniform[-1,1) synthetic inputs, x[i] for counter i+1. */
+int mx_synth_fill(float* dst, int64_t n, uint64_t seed, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MATCHA_GOSSIP_H */

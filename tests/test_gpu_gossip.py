@@ -1,0 +1,262 @@
+"""GPU parity: the HIP path against the golden fixtures and the CPU oracle (bit-exact)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+from conftest import Topo, golden_json, golden_npz
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def _set_state(key, pos):
+    np.random.set_state(("MT19937", np.asarray(key, np.uint32), int(pos), 0, 0.0))
+
+
+# ------------------------------------------------------------------------------------ flags
+@pytest.mark.parametrize("ci", range(8))
+def test_gpu_flags_vs_reference(pkg, ci):
+    g, meta = golden_npz("flags"), golden_json("flags")["matcha"][ci]
+    gp = object.__new__(pkg.GraphProcessor)
+    p = np.array(meta["p"], np.float64)
+    p[np.isnan(p) | (p < 0)] = 0
+    _set_state(g[f"matcha{ci}_key0"], meta["pos0"])
+    flags = gp._draw_flags_on_gpu(p, meta["T"] + 1)
+    assert np.array_equal(flags.cpu().numpy(), g[f"matcha{ci}_flags"])
+    st = np.random.get_state()
+    assert np.array_equal(st[1], g[f"matcha{ci}_key1"]) and st[2] == meta["pos1"]
+
+
+@pytest.mark.parametrize("ci", [0, 4, 7])
+def test_gpu_flags_sequential_path(pkg, ci):
+    """The resample-aware sequential walk gives the same flags and state as the parallel path."""
+    g, meta = golden_npz("flags"), golden_json("flags")["matcha"][ci]
+    p = np.ascontiguousarray(np.nan_to_num(np.array(meta["p"], np.float64), nan=0.0).clip(0, None))
+    T = meta["T"] + 1
+    key = np.ascontiguousarray(g[f"matcha{ci}_key0"])
+    out = torch.empty((T, len(p)), dtype=torch.uint8, device="cuda")
+    k1 = np.empty(624, np.uint32)
+    pos = ctypes.c_int(0)
+    rc = pkg.lib.mx_flags_binomial_sequential(key.ctypes.data, meta["pos0"], p.ctypes.data, len(p), T,
+                                              out.data_ptr(), k1.ctypes.data, ctypes.byref(pos), None)
+    assert rc == 0
+    assert np.array_equal(out.cpu().numpy(), g[f"matcha{ci}_flags"])
+    assert np.array_equal(k1, g[f"matcha{ci}_key1"]) and pos.value == meta["pos1"]
+
+
+def test_matcha_processor_gpu_flags_and_state(pkg, O):
+    np.random.seed(1234)
+    st0 = np.random.get_state()
+    GP = pkg.MatchaProcessor(pkg.select_graph(0), 0.5, 0, 8, 500, True)
+    flags, key, pos = O.matcha_flags(st0[1], st0[2], np.asarray(GP.probabilities), 501)
+    assert np.array_equal(np.asarray(GP.active_flags, np.uint8), flags)
+    assert np.array_equal(GP.flags_dev.cpu().numpy(), flags)
+    st1 = np.random.get_state()
+    assert np.array_equal(st1[1], key) and st1[2] == pos
+    assert isinstance(GP.active_flags[0][0], np.int64)
+
+
+def test_fixed_processor_gpu(pkg, O):
+    np.random.seed(77)
+    st0 = np.random.get_state()
+    GP = pkg.FixedProcessor(pkg.select_graph(0), 0.37, 0, 8, 99, True)
+    flags, key, pos = O.fixed_flags(st0[1], st0[2], 0.37, 100)
+    assert GP.active_flags == flags.tolist()
+    st1 = np.random.get_state()
+    assert np.array_equal(st1[1], key) and st1[2] == pos
+    assert GP.neighbor_weight == 0.2857142857142856
+
+
+# ------------------------------------------------------------------------------------ plans
+def _py_plan(flags_row, partner, row_base, n_local, alpha):
+    M, n = partner.shape
+    src = [[] for _ in range(n_local)]
+    remote = 0
+    for g in range(M):
+        if not flags_row[g]:
+            continue
+        for p in range(n):
+            q = int(partner[g, p])
+            if not (row_base <= q < row_base + n_local):
+                continue
+            if row_base <= p < row_base + n_local:
+                src[q - row_base].append(p - row_base)
+            else:
+                src[q - row_base].append(n_local + remote)
+                remote += 1
+    sw = [np.float32(1.0 - len(s) * alpha) for s in src]
+    return int(any(flags_row)), remote, src, sw
+
+
+@pytest.mark.parametrize("gid,nranks", [(0, 1), (0, 2), (0, 8), (2, 4), (3, 3)])
+def test_plan_vs_python(pkg, gid, nranks):
+    n = pkg.GRAPH_SIZES[gid]
+    gp = pkg.GraphProcessor(pkg.select_graph(gid), 1.0, 0, n, 4, True)
+    partner = np.asarray(gp.neighbors_info, np.int32)
+    M = partner.shape[0]
+    rng = np.random.RandomState(gid * 10 + nranks)
+    flags = (rng.uniform(size=(64, M)) < 0.5).astype(np.uint8)
+    flags[0] = 1
+    flags[1] = 0
+    alpha = 0.123456789
+    fd = torch.from_numpy(flags).cuda()
+    pd = torch.from_numpy(partner).cuda()
+    for row_base, n_local in pkg.partition(n, nranks):
+        W = pkg.lib.mx_plan_words(n_local, M)
+        plan = torch.empty(64 * W, dtype=torch.int32, device="cuda")
+        assert pkg.lib.mx_plan_build(fd.data_ptr(), 64, M, pd.data_ptr(), n, None, 0, row_base, n_local,
+                                     alpha, plan.data_ptr(), None) == 0
+        P = plan.cpu().numpy().reshape(64, W)
+        for t in range(64):
+            any_, remote, src, sw = _py_plan(flags[t], partner, row_base, n_local, alpha)
+            rec = P[t]
+            assert rec[0] == any_ and rec[1] == remote
+            deg = rec[4:4 + n_local]
+            assert deg.tolist() == [len(s) for s in src]
+            assert np.array_equal(rec[4 + n_local:4 + 2 * n_local].view(np.float32), np.array(sw, np.float32))
+            S = rec[4 + 2 * n_local:].reshape(n_local, M)
+            for r in range(n_local):
+                assert S[r, :len(src[r])].tolist() == src[r]
+
+
+# ------------------------------------------------------------------------------------ mixing
+@pytest.mark.parametrize("case", ["g0", "g5", "g2"])
+def test_mix_vs_reference_golden(pkg, case):
+    d = golden_npz("decen")
+    meta = {m["name"]: m for m in golden_json("decen")}[case]
+    topo = Topo(d[case + "_partner"], meta["alpha"], d[case + "_flags"])
+    grp = pkg.VirtualWorkerGroup(topo, numel=meta["P"])
+    grp.rows.copy_(torch.from_numpy(d[case + "_X0"]))
+    for r in range(meta["rounds"]):
+        grp.communicate()
+        got = grp.rows.cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), d[case + "_Y"][r].view(np.uint32)), f"round {r}"
+
+
+def test_mix_models_adopted_in_place(pkg, O):
+    """Workers as nn.Modules: parameters re-homed into the arena (identity kept), mixed in place."""
+    n = 8
+    torch.manual_seed(0)
+    models = [torch.nn.Sequential(torch.nn.Linear(33, 17), torch.nn.ReLU(), torch.nn.Linear(17, 5)).cuda()
+              for _ in range(n)]
+    ids = [[id(p) for p in m.parameters()] for m in models]
+    X = np.stack([torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy() for m in models])
+    flags = np.array([[1, 1, 1, 1, 1], [1, 0, 0, 1, 0], [0, 0, 0, 0, 0], [0, 1, 1, 0, 1]], np.uint8)
+    gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, n, 4, True)
+    topo = Topo(gp.neighbors_info, 2 / 7, flags)
+    grp = pkg.VirtualWorkerGroup(topo, models)
+    for f in flags:
+        grp.communicate()
+        X = O.decen_round(X, topo.neighbors_info, f, 2 / 7)
+    got = np.stack([torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy() for m in models])
+    assert np.array_equal(got, X)
+    assert ids == [[id(p) for p in m.parameters()] for m in models]
+    out = models[3](torch.ones(2, 33, device="cuda"))          # still a working module
+    assert out.shape == (2, 5)
+
+
+def test_mix_segmented_unaligned_layout(pkg, O):
+    """Per-tensor pointer table (no arena): odd lengths, unaligned bases, multi-segment tiles."""
+    n = 8
+    lens = [1, 3, 1024, 1027, 5, 4096 + 3, 0, 77]
+    gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, n, 4, True)
+    flags = np.array([[1, 1, 1, 1, 1], [0, 1, 0, 1, 0]], np.uint8)
+    topo = Topo(gp.neighbors_info, 0.3, flags)
+    eng = pkg.GossipEngine(topo)
+    P = sum(lens)
+    X = np.stack([O.synth(900 + i, P) for i in range(n)])
+    big = torch.from_numpy(np.concatenate([X, X[:, :3]], axis=1)).cuda()   # odd offsets
+    base = 1                                                            # misalign by 4 bytes
+    ptrs, cuts = [], np.cumsum([0] + lens)
+    for i in range(n):
+        ptrs.append([big[i].data_ptr() + 4 * (base + int(cuts[s])) for s in range(len(lens))])
+    big[:, base:base + P] = torch.from_numpy(X).cuda()
+    lay = pkg.Layout(lens, ptrs, eng.n_slots)
+    for it, f in enumerate(flags):
+        eng.mix(it, lay)
+        X = O.decen_round(X, topo.neighbors_info, f, 0.3)
+    torch.cuda.synchronize()
+    got = big[:, base:base + P].cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), X.view(np.uint32))
+
+
+@pytest.mark.parametrize("gid", [0, 3])
+def test_mix_full_size_headline(pkg, O, gid):
+    """25.6M params x n workers (the headline shape) bit-exact vs the oracle."""
+    n = pkg.GRAPH_SIZES[gid]
+    P = 25_600_000 if gid == 0 else 3_000_001
+    gp = pkg.GraphProcessor(pkg.select_graph(gid), 1.0, 0, n, 4, True)
+    M = len(gp.neighbors_info)
+    flags = np.ones((2, M), np.uint8)
+    flags[1, ::2] = 0
+    topo = Topo(gp.neighbors_info, 0.2857142857142856, flags)
+    grp = pkg.VirtualWorkerGroup(topo, numel=P)
+    for i in range(n):
+        assert pkg.lib.mx_synth_fill(grp.rows[i].data_ptr(), P, 1234 + i, None) == 0
+    X = np.stack([O.synth(1234 + i, P) for i in range(n)])
+    assert np.array_equal(grp.rows.cpu().numpy(), X)
+    for f in flags:
+        grp.communicate()
+        X = O.decen_round(X, topo.neighbors_info, f, topo.neighbor_weight)
+    got = grp.rows.cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), X.view(np.uint32))
+
+
+# ------------------------------------------------------------------------------------ choco
+@pytest.mark.parametrize("case", ["c0", "c1", "c2"])
+def test_choco_vs_reference_golden(pkg, case):
+    c = golden_npz("choco")
+    m = {x["name"]: x for x in golden_json("choco")}[case]
+    topo = Topo(c[case + "_partner"], m["alpha"], c[case + "_flags"])
+    grp = pkg.ChocoWorkerGroup(topo, numel=m["P"], ratio=m["ratio"], consensus_lr=m["consensus_lr"])
+    assert grp.k == m["k"]
+    grp.rows.copy_(torch.from_numpy(c[case + "_X0"]))
+    for r in range(m["rounds"]):
+        grp.rows.add_(torch.from_numpy(c[case + "_D"][r]).cuda())
+        assert np.array_equal(grp.rows.cpu().numpy(), c[case + "_Xin"][r])
+        grp.communicate()
+        got = grp.rows.cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), c[case + "_Y"][r].view(np.uint32)), f"round {r}"
+    assert np.array_equal(grp.x_hat[:, :m["P"]].cpu().numpy(), c[case + "_xhat"])
+    assert np.array_equal(grp.s[:, :m["P"]].cpu().numpy(), c[case + "_s"])
+
+
+def test_topk_vs_reference_golden(pkg):
+    t = golden_npz("topk")
+    import oracle as O
+    for row in golden_json("topk"):
+        key = f"P{row['P']}_r{row['ratio']}_idx"
+        if key not in t:
+            continue
+        x = torch.from_numpy(O.synth(row["P"], row["P"])).cuda()
+        v, i = pkg.get_top_k(x, row["ratio"])
+        assert i.dtype == torch.int64 and i.numel() == row["k"]
+        assert np.array_equal(i.cpu().numpy(), t[key])
+        assert np.array_equal(v.cpu().numpy(), t[f"P{row['P']}_r{row['ratio']}_val"])
+
+
+@pytest.mark.parametrize("P,ratio", [(14_774_436, 0.99), (1_000_003, 0.9), (4097, 0.5)])
+def test_topk_large_and_ties_vs_oracle(pkg, O, P, ratio):
+    x = O.synth(P + 1, P)
+    x[::7] = np.float32(0.5)          # many exact ties at one magnitude
+    x[::11] = np.float32(-0.5)
+    k = O.topk_k(P, ratio)
+    ov, oi = O.topk_abs(x, k)
+    v, i = pkg.get_top_k(torch.from_numpy(x).cuda(), ratio)
+    assert np.array_equal(i.cpu().numpy(), oi)
+    assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32))
+
+
+# ------------------------------------------------------------------------------------ helpers
+def test_flatten_unflatten_scatter(pkg):
+    ts = [torch.randn(s, device="cuda") for s in ((3, 5), (7,), (0,), (64, 33), (1,))]
+    flat = pkg.flatten_tensors(ts)
+    assert torch.equal(flat, torch.cat([t.reshape(-1) for t in ts]))
+    one = pkg.flatten_tensors([ts[0]])
+    assert torch.equal(one, ts[0].reshape(-1)) and one.data_ptr() != ts[0].data_ptr()
+    views = pkg.unflatten_tensors(flat, ts)
+    assert all(torch.equal(a, b) for a, b in zip(views, ts))
+    dst = [torch.zeros_like(t) for t in ts]
+    pkg.scatter_tensors(flat * 2, dst)
+    assert all(torch.equal(a, 2 * b) for a, b in zip(dst, ts))
