@@ -54,53 +54,78 @@ extern "C" int mx_rccl_destroy(void* comm) {
     return MX_OK;
 }
 
-extern "C" int mx_exchange_round(void* comm_v, const uint8_t* flags_row, int M,
-                                 const int32_t* partner, int n_global, const int32_t* owner,
-                                 int my_rank, int row_base, int n_local, void* const* rows,
-                                 void* slab, int64_t slab_ld_bytes, int64_t row_bytes,
-                                 int* n_remote_out, void* stream) {
-    MX_CHECK(comm_v && flags_row && partner && owner && rows, "mx_exchange_round: null pointer");
-    MX_CHECK(row_bytes > 0 && row_bytes % 4 == 0, "mx_exchange_round: row_bytes %lld", (long long)row_bytes);
-    ncclComm_t comm = reinterpret_cast<ncclComm_t>(comm_v);
-    hipStream_t st = mx::as_stream(stream);
+extern "C" int mx_exchange_plan(const uint8_t* flags_row, int M, const int32_t* partner, int n_global,
+                                const int32_t* owner, int my_rank, int row_base, int n_local,
+                                int32_t* ops, int cap, int* n_ops) {
+    MX_CHECK(flags_row && partner && owner && n_ops, "mx_exchange_plan: null pointer");
+    MX_CHECK(M >= 1 && n_global >= 1 && n_local >= 1 && row_base >= 0 && row_base + n_local <= n_global,
+             "mx_exchange_plan: M=%d n=%d block [%d, %d)", M, n_global, row_base, row_base + n_local);
     auto is_local = [&](int w) { return w >= row_base && w < row_base + n_local; };
-
-    struct Op {
-        bool send;
-        int peer;
-        void* buf;
-    };
-    std::vector<Op> ops;
-    int remote = 0;
+    int cnt = 0, remote = 0;
     for (int g = 0; g < M; ++g) {
         if (!flags_row[g]) continue;
         for (int p = 0; p < n_global; ++p) {      // p = sender, ascending
             const int q = partner[g * n_global + p];
             if (q < 0) continue;
             MX_CHECK(q < n_global && partner[g * n_global + q] == p,
-                     "mx_exchange_round: matching %d is not symmetric at %d", g, p);
+                     "mx_exchange_plan: matching %d is not symmetric at %d", g, p);
             const bool pl = is_local(p), ql = is_local(q);
-            if (pl && !ql) {                      // our row p goes to q's owner
-                ops.push_back({true, owner[q], rows[p - row_base]});
-            } else if (!pl && ql) {               // p's row comes into the next slab slot
-                MX_CHECK(slab, "mx_exchange_round: receive slab required");
-                ops.push_back({false, owner[p], static_cast<char*>(slab) + (int64_t)remote * slab_ld_bytes});
-                ++remote;
+            if (pl == ql) continue;
+            const int peer = pl ? owner[q] : owner[p];
+            MX_CHECK(peer >= 0 && peer != my_rank, "mx_exchange_plan: worker owned by bad rank %d", peer);
+            if (ops) {
+                MX_CHECK(cnt < cap, "mx_exchange_plan: more than %d operations", cap);
+                int32_t* o = ops + 4 * cnt;
+                o[0] = pl ? 0 : 1;                  // 0 = send our row p, 1 = receive p's row
+                o[1] = peer;
+                o[2] = pl ? p - row_base : remote;  // local row / receive slab slot
+                o[3] = p;                           // the worker whose row travels
             }
+            if (!pl) ++remote;
+            ++cnt;
         }
     }
+    *n_ops = cnt;
+    return MX_OK;
+}
+
+extern "C" int mx_exchange_round(void* comm_v, const uint8_t* flags_row, int M,
+                                 const int32_t* partner, int n_global, const int32_t* owner,
+                                 int my_rank, int row_base, int n_local, void* const* rows,
+                                 void* slab, int64_t slab_ld_bytes, int64_t row_bytes,
+                                 int* n_remote_out, void* stream) {
+    MX_CHECK(comm_v && rows, "mx_exchange_round: null pointer");
+    MX_CHECK(row_bytes > 0 && row_bytes % 4 == 0, "mx_exchange_round: row_bytes %lld", (long long)row_bytes);
+    int nops = 0;
+    int rc = mx_exchange_plan(flags_row, M, partner, n_global, owner, my_rank, row_base, n_local,
+                              nullptr, 0, &nops);
+    if (rc != MX_OK) return rc;
+    std::vector<int32_t> ops(4 * (size_t)(nops > 0 ? nops : 1));
+    rc = mx_exchange_plan(flags_row, M, partner, n_global, owner, my_rank, row_base, n_local,
+                          ops.data(), nops, &nops);
+    if (rc != MX_OK) return rc;
+    int remote = 0;
+    for (int i = 0; i < nops; ++i) remote += ops[4 * i] == 1;
     if (n_remote_out) *n_remote_out = remote;
-    if (ops.empty()) return MX_OK;
+    if (nops == 0) return MX_OK;
+    MX_CHECK(remote == 0 || slab, "mx_exchange_round: receive slab required");
+    ncclComm_t comm = reinterpret_cast<ncclComm_t>(comm_v);
+    hipStream_t st = mx::as_stream(stream);
     const size_t count = (size_t)(row_bytes / 4);
     MX_NCCL(ncclGroupStart());
-    for (const Op& o : ops) {
-        MX_CHECK(o.peer >= 0 && o.peer != my_rank, "mx_exchange_round: bad peer %d", o.peer);
-        if (o.send) {
-            ncclResult_t r = ncclSend(o.buf, count, ncclFloat32, o.peer, comm, st);
-            if (r != ncclSuccess) { ncclGroupEnd(); mx::set_error("ncclSend: %s", ncclGetErrorString(r)); return MX_ERR_RCCL; }
+    for (int i = 0; i < nops; ++i) {
+        const int32_t* o = &ops[4 * i];
+        ncclResult_t r;
+        if (o[0] == 0) {
+            r = ncclSend(rows[o[2]], count, ncclFloat32, o[1], comm, st);
         } else {
-            ncclResult_t r = ncclRecv(o.buf, count, ncclFloat32, o.peer, comm, st);
-            if (r != ncclSuccess) { ncclGroupEnd(); mx::set_error("ncclRecv: %s", ncclGetErrorString(r)); return MX_ERR_RCCL; }
+            r = ncclRecv(static_cast<char*>(slab) + (int64_t)o[2] * slab_ld_bytes, count, ncclFloat32,
+                         o[1], comm, st);
+        }
+        if (r != ncclSuccess) {
+            ncclGroupEnd();
+            mx::set_error("%s: %s", o[0] == 0 ? "ncclSend" : "ncclRecv", ncclGetErrorString(r));
+            return MX_ERR_RCCL;
         }
     }
     MX_NCCL(ncclGroupEnd());

@@ -17,29 +17,48 @@
 //
 // Traffic per round = 2 * n_active * P * 4 bytes (+ n_remote * P * 4 read of the slab): the
 // HBM roofline of the north star.  No MFMA: ~0.25 flop/byte.
-#include <stdlib.h>
-
 #include "mx_common.h"
 
 namespace {
 constexpr int kTPB = 256;
 constexpr int kMaxM = 32;
 
+// VEC-wide float vectors as clang ext vectors (16-byte global_load/store_dwordx4 for VEC = 4;
+// the non-temporal builtins accept them)
 template <int VEC>
-struct alignas(4 * VEC) FV {
-    float v[VEC];
-};
+struct VT;
+template <>
+struct VT<4> { typedef float type __attribute__((ext_vector_type(4))); };
+template <>
+struct VT<2> { typedef float type __attribute__((ext_vector_type(2))); };
+template <>
+struct VT<1> { typedef float type __attribute__((ext_vector_type(1))); };
 
-template <int VEC, int NS>
+template <bool NT, typename F>
+__device__ __forceinline__ F ld(const float* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const F*>(p));
+    else return *reinterpret_cast<const F*>(p);
+}
+
+template <bool NT, typename F>
+__device__ __forceinline__ void st(float* p, const F& v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<F*>(p));
+    else *reinterpret_cast<F*>(p) = v;
+}
+
+// VEC floats per lane access (16 B for VEC = 4), NS slots (LDS rows), U accesses per lane per
+// row per tile (U * 256 * VEC floats per tile), NT: non-temporal (streaming) loads/stores.
+template <int VEC, int NS, int U, bool NT>
 __global__ __launch_bounds__(kTPB) void mix_kernel(float* const* __restrict__ seg_ptrs,
                                                    const int64_t* __restrict__ seg_len,
                                                    const int64_t* __restrict__ tile_off,
                                                    const uint8_t* __restrict__ seg_vec, int nseg,
-                                                   int64_t total_tiles, int n_slots, const int32_t* __restrict__ plan,
-                                                   int64_t iter, int n_local, int M, float alpha) {
-    using F = FV<VEC>;
-    constexpr int TILE = kTPB * VEC;
-    __shared__ F lds[NS][kTPB];
+                                                   int64_t total_tiles, int n_slots,
+                                                   const int32_t* __restrict__ plan, int64_t iter,
+                                                   int n_local, int M, float alpha) {
+    using F = typename VT<VEC>::type;
+    constexpr int TILE = kTPB * VEC * U;
+    __shared__ F lds[NS][U][kTPB];
     __shared__ int32_t sp[mx::kPlanHeader + 2 * NS + NS * kMaxM];
 
     const int tid = threadIdx.x;
@@ -69,49 +88,67 @@ __global__ __launch_bounds__(kTPB) void mix_kernel(float* const* __restrict__ se
             seg = lo;
         }
         const int64_t len = seg_len[seg];
-        const int64_t c = (tile - tile_off[seg]) * TILE + (int64_t)tid * VEC;
+        const int64_t c0 = (tile - tile_off[seg]) * TILE + (int64_t)tid * VEC;
         float* const* ptrs = seg_ptrs + (int64_t)seg * n_slots;
-        const bool full = (c + VEC <= len) && seg_vec[seg];
+        const bool full = (c0 + (int64_t)(U - 1) * kTPB * VEC + VEC <= len) && seg_vec[seg];
 
-        F v[NS];
+        F v[NS][U];
 #pragma unroll
         for (int k = 0; k < NS; ++k) {
             if ((need >> k) & 1ull) {
-                const float* p = ptrs[k] + c;
-                if (full) {
-                    v[k] = *reinterpret_cast<const F*>(p);
-                } else {
+                const float* p = ptrs[k] + c0;
 #pragma unroll
-                    for (int j = 0; j < VEC; ++j) v[k].v[j] = (c + j < len) ? p[j] : 0.0f;
+                for (int u = 0; u < U; ++u) {
+                    if (full) {
+                        v[k][u] = ld<NT, F>(p + u * kTPB * VEC);
+                    } else {
+                        const int64_t c = c0 + (int64_t)u * kTPB * VEC;
+#pragma unroll
+                        for (int j = 0; j < VEC; ++j)
+                            v[k][u][j] = (c + j < len) ? p[u * kTPB * VEC + j] : 0.0f;
+                    }
                 }
             }
         }
 #pragma unroll
         for (int k = 0; k < NS; ++k)
-            if ((need >> k) & 1ull) lds[k][tid] = v[k];
+            if ((need >> k) & 1ull) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) lds[k][u][tid] = v[k][u];
+            }
 
         for (int r = 0; r < n_local; ++r) {
             const int d = deg[r];
             if (d == 0) continue;
-            F acc;
+            F acc[U];
 #pragma unroll
-            for (int j = 0; j < VEC; ++j) acc.v[j] = 0.0f;
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int j = 0; j < VEC; ++j) acc[u][j] = 0.0f;
             for (int e = 0; e < d; ++e) {
-                const F x = lds[src[r * M + e]][tid];
+                const int sl = src[r * M + e];
 #pragma unroll
-                for (int j = 0; j < VEC; ++j) acc.v[j] = __builtin_fmaf(alpha, x.v[j], acc.v[j]);
+                for (int u = 0; u < U; ++u) {
+                    const F x = lds[sl][u][tid];
+#pragma unroll
+                    for (int j = 0; j < VEC; ++j) acc[u][j] = __builtin_fmaf(alpha, x[j], acc[u][j]);
+                }
             }
-            const F xs = lds[r][tid];
             const float s = sw[r];
+            float* p = ptrs[r] + c0;
 #pragma unroll
-            for (int j = 0; j < VEC; ++j) acc.v[j] = __builtin_fmaf(s, xs.v[j], acc.v[j]);
-            float* p = ptrs[r] + c;
-            if (full) {
-                *reinterpret_cast<F*>(p) = acc;
-            } else {
+            for (int u = 0; u < U; ++u) {
+                const F xs = lds[r][u][tid];
 #pragma unroll
-                for (int j = 0; j < VEC; ++j)
-                    if (c + j < len) p[j] = acc.v[j];
+                for (int j = 0; j < VEC; ++j) acc[u][j] = __builtin_fmaf(s, xs[j], acc[u][j]);
+                if (full) {
+                    st<NT, F>(p + u * kTPB * VEC, acc[u]);
+                } else {
+                    const int64_t c = c0 + (int64_t)u * kTPB * VEC;
+#pragma unroll
+                    for (int j = 0; j < VEC; ++j)
+                        if (c + j < len) p[u * kTPB * VEC + j] = acc[u][j];
+                }
             }
         }
     }
@@ -129,14 +166,15 @@ Cfg pick(int n_slots) {
     return {0, 0};
 }
 
-int blocks_per_cu() {
-    static int v = [] {
-        const char* e = getenv("MX_MIX_BLOCKS_PER_CU");
-        int x = e ? atoi(e) : 0;
-        return x > 0 ? x : 4;
-    }();
-    return v;
-}
+// tuning state (mx_mix_tune); defaults chosen from measurements on MI355X
+struct Tune {
+    int blocks_per_cu = 4;
+    int unroll = 1;      // 1 or 2 accesses per lane per row per tile (NS = 8 config only)
+    int nontemporal = 0;
+};
+Tune g_tune;
+
+int unroll_for(int ns) { return ns == 8 ? g_tune.unroll : 1; }
 
 int cu_count() {
     static int v = [] {
@@ -148,14 +186,14 @@ int cu_count() {
     return v;
 }
 
-template <int VEC, int NS>
+template <int VEC, int NS, int U, bool NT>
 int launch(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_off,
            const uint8_t* seg_vec, int nseg, int n_slots, const int32_t* plan, int64_t iter,
            int n_local, int M, float alpha, int64_t total_tiles, hipStream_t st) {
-    int64_t grid = (int64_t)cu_count() * blocks_per_cu();
+    int64_t grid = (int64_t)cu_count() * g_tune.blocks_per_cu;
     if (grid > total_tiles) grid = total_tiles;
     if (grid < 1) grid = 1;
-    hipLaunchKernelGGL((mix_kernel<VEC, NS>), dim3((unsigned)grid), dim3(kTPB), 0, st, seg_ptrs,
+    hipLaunchKernelGGL((mix_kernel<VEC, NS, U, NT>), dim3((unsigned)grid), dim3(kTPB), 0, st, seg_ptrs,
                        seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan, iter, n_local,
                        M, alpha);
     MX_LAUNCH_CHECK();
@@ -165,7 +203,16 @@ int launch(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_o
 
 extern "C" int mx_mix_tile(int n_slots) {
     const Cfg c = pick(n_slots);
-    return c.vec * kTPB;
+    return c.vec * kTPB * unroll_for(c.ns);
+}
+
+extern "C" int mx_mix_tune(int blocks_per_cu, int unroll, int nontemporal) {
+    MX_CHECK(blocks_per_cu >= 1 && blocks_per_cu <= 64, "mx_mix_tune: blocks_per_cu %d", blocks_per_cu);
+    MX_CHECK(unroll == 1 || unroll == 2, "mx_mix_tune: unroll %d", unroll);
+    g_tune.blocks_per_cu = blocks_per_cu;
+    g_tune.unroll = unroll;
+    g_tune.nontemporal = nontemporal ? 1 : 0;
+    return MX_OK;
 }
 
 extern "C" int mx_mix_layout(const int64_t* seg_len_host, int nseg, int n_slots, int64_t* tile_off_host) {
@@ -194,18 +241,20 @@ extern "C" int mx_gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_
     MX_CHECK(c.vec > 0, "mx_gossip_mix: n_slots=%d exceeds 64", n_slots);
     hipStream_t st = mx::as_stream(stream);
     if (total_tiles <= 0) return MX_OK;
+    const bool nt = g_tune.nontemporal != 0;
+#define MX_ARGS seg_ptrs_dev, seg_len_dev, tile_off_dev, seg_vec_dev, nseg, n_slots, plan_dev, iter, \
+                n_local, M, alpha, total_tiles, st
     switch (c.ns) {
         case 8:
-            return launch<4, 8>(seg_ptrs_dev, seg_len_dev, tile_off_dev, seg_vec_dev, nseg, n_slots,
-                                plan_dev, iter, n_local, M, alpha, total_tiles, st);
+            if (unroll_for(8) == 2)
+                return nt ? launch<4, 8, 2, true>(MX_ARGS) : launch<4, 8, 2, false>(MX_ARGS);
+            return nt ? launch<4, 8, 1, true>(MX_ARGS) : launch<4, 8, 1, false>(MX_ARGS);
         case 16:
-            return launch<4, 16>(seg_ptrs_dev, seg_len_dev, tile_off_dev, seg_vec_dev, nseg, n_slots,
-                                 plan_dev, iter, n_local, M, alpha, total_tiles, st);
+            return nt ? launch<4, 16, 1, true>(MX_ARGS) : launch<4, 16, 1, false>(MX_ARGS);
         case 32:
-            return launch<2, 32>(seg_ptrs_dev, seg_len_dev, tile_off_dev, seg_vec_dev, nseg, n_slots,
-                                 plan_dev, iter, n_local, M, alpha, total_tiles, st);
+            return nt ? launch<2, 32, 1, true>(MX_ARGS) : launch<2, 32, 1, false>(MX_ARGS);
         default:
-            return launch<1, 64>(seg_ptrs_dev, seg_len_dev, tile_off_dev, seg_vec_dev, nseg, n_slots,
-                                 plan_dev, iter, n_local, M, alpha, total_tiles, st);
+            return nt ? launch<1, 64, 1, true>(MX_ARGS) : launch<1, 64, 1, false>(MX_ARGS);
     }
+#undef MX_ARGS
 }

@@ -133,6 +133,7 @@ class Layout:
         check(lib.mx_mix_layout(seg_len.ctypes.data, nseg, n_slots, tile_off.ctypes.data), "mx_mix_layout")
         self.nseg = nseg
         self.n_slots = n_slots
+        self.tile = int(lib.mx_mix_tile(n_slots))
         self.total_tiles = int(tile_off[-1])
         self.seg_ptrs = torch.from_numpy(table).to("cuda")
         self.seg_len = torch.from_numpy(seg_len).to("cuda")
@@ -195,6 +196,8 @@ class GossipEngine:
         return nrem.value
 
     def mix(self, it, layout, stream=None):
+        if layout.tile != lib.mx_mix_tile(layout.n_slots):
+            raise MXError("layout built for another mixing tile size (mx_mix_tune changed it)")
         check(lib.mx_gossip_mix(layout.seg_ptrs.data_ptr(), layout.seg_len.data_ptr(),
                                 layout.tile_off.data_ptr(), layout.seg_vec.data_ptr(), layout.nseg,
                                 layout.total_tiles, layout.n_slots, self.plan.data_ptr(), int(it),

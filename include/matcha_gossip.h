@@ -91,6 +91,10 @@ int mx_plan_build(const uint8_t* flags_dev, int64_t T, int M, const int32_t* par
  * Rows with degree 0 are neither read nor written.  No-op when the record's flags are all 0.
  */
 int mx_mix_tile(int n_slots);
+/* Tuning hook of the mixing kernel (grid = CUs x blocks_per_cu persistent workgroups; unroll =
+ * 16-byte accesses per lane per row per tile, 1 or 2; nontemporal = streaming load/store hints).
+ * Changes the tile size: rebuild layouts (mx_mix_layout) after calling it. */
+int mx_mix_tune(int blocks_per_cu, int unroll, int nontemporal);
 int mx_mix_layout(const int64_t* seg_len_host, int nseg, int n_slots, int64_t* tile_off_host);
 int mx_gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev,
                   const int64_t* tile_off_dev, const uint8_t* seg_vec_dev, int nseg,
@@ -149,6 +153,12 @@ int mx_choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64
 int mx_rccl_unique_id(void* id_out /* 128 bytes */);
 int mx_rccl_init(const void* id /* 128 bytes */, int nranks, int rank, void** comm_out);
 int mx_rccl_destroy(void* comm);
+/* The ordered operations mx_exchange_round posts for this rank, host only (no GPU, no RCCL):
+ * ops[4i..4i+3] = {kind (0 send / 1 recv), peer rank, local row (send) or slab slot (recv),
+ * global id of the worker whose row travels}.  ops == NULL: count only. */
+int mx_exchange_plan(const uint8_t* flags_row, int M, const int32_t* partner, int n_global,
+                     const int32_t* owner, int my_rank, int row_base, int n_local, int32_t* ops,
+                     int cap, int* n_ops);
 int mx_exchange_round(void* comm, const uint8_t* flags_row, int M, const int32_t* partner,
                       int n_global, const int32_t* owner, int my_rank, int row_base, int n_local,
                       void* const* rows, void* slab, int64_t slab_ld_bytes, int64_t row_bytes,

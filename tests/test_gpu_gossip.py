@@ -5,6 +5,7 @@ import numpy as np
 import pytest
 
 from conftest import Topo, golden_json, golden_npz
+from planref import py_plan
 
 torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
@@ -69,26 +70,6 @@ def test_fixed_processor_gpu(pkg, O):
 
 
 # ------------------------------------------------------------------------------------ plans
-def _py_plan(flags_row, partner, row_base, n_local, alpha):
-    M, n = partner.shape
-    src = [[] for _ in range(n_local)]
-    remote = 0
-    for g in range(M):
-        if not flags_row[g]:
-            continue
-        for p in range(n):
-            q = int(partner[g, p])
-            if not (row_base <= q < row_base + n_local):
-                continue
-            if row_base <= p < row_base + n_local:
-                src[q - row_base].append(p - row_base)
-            else:
-                src[q - row_base].append(n_local + remote)
-                remote += 1
-    sw = [np.float32(1.0 - len(s) * alpha) for s in src]
-    return int(any(flags_row)), remote, src, sw
-
-
 @pytest.mark.parametrize("gid,nranks", [(0, 1), (0, 2), (0, 8), (2, 4), (3, 3)])
 def test_plan_vs_python(pkg, gid, nranks):
     n = pkg.GRAPH_SIZES[gid]
@@ -109,7 +90,7 @@ def test_plan_vs_python(pkg, gid, nranks):
                                      alpha, plan.data_ptr(), None) == 0
         P = plan.cpu().numpy().reshape(64, W)
         for t in range(64):
-            any_, remote, src, sw = _py_plan(flags[t], partner, row_base, n_local, alpha)
+            any_, remote, src, sw, _ = py_plan(flags[t], partner, row_base, n_local, alpha)
             rec = P[t]
             assert rec[0] == any_ and rec[1] == remote
             deg = rec[4:4 + n_local]

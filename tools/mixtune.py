@@ -1,0 +1,55 @@
+"""Sweep mixing-kernel tunings on the headline shape (8 workers x 25.6M, graph 0, full rounds)."""
+import ctypes
+import importlib
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+pkg = importlib.import_module("270-matcha-a-matching-based-link-scheduling-strategy-to-speed-up-distributed-optimization_amd")
+from tests.conftest import Topo  # noqa: E402
+
+n, P = 8, 25_600_000
+gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, n, 4, True)
+topo = Topo(gp.neighbors_info, 2 / 7, np.ones((4, 5), np.uint8))
+grp = pkg.VirtualWorkerGroup(topo, numel=P)
+for i in range(n):
+    pkg.lib.mx_synth_fill(grp.rows[i].data_ptr(), P, 1234 + i, None)
+BYTES = 2 * n * P * 4
+
+
+def timeit(fn, reps=30, warm=5):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in ev:
+        a.record()
+        fn()
+        b.record()
+    torch.cuda.synchronize()
+    ms = np.array([a.elapsed_time(b) for a, b in ev])
+    return float(np.median(ms)), float(ms.min())
+
+
+res = []
+src = torch.empty((n, P), device="cuda")
+dst = torch.empty_like(src)
+med, mn = timeit(lambda: dst.copy_(src))
+res.append({"cfg": "torch copy_ (same bytes)", "med_us": med * 1e3, "TBps": BYTES / med / 1e9})
+for bpc in (1, 2, 3, 4, 6, 8, 16):
+    for U in (1, 2):
+        for NT in (0, 1):
+            assert pkg.lib.mx_mix_tune(bpc, U, NT) == 0
+            lay = pkg.Layout([P], [[grp.arena[r].data_ptr()] for r in range(n)], grp.engine.n_slots)
+            med, mn = timeit(lambda: grp.engine.mix(0, lay))
+            res.append({"cfg": f"bpc={bpc} U={U} NT={NT}", "med_us": med * 1e3, "min_us": mn * 1e3,
+                        "TBps": BYTES / med / 1e9})
+            print(json.dumps(res[-1]), flush=True)
+print(json.dumps(res[0]))
+best = min(res[1:], key=lambda r: r["med_us"])
+print("BEST", json.dumps(best))
