@@ -22,6 +22,10 @@ from ._lib import MXError, check, lib, require_device, stream_ptr
 
 ROW_ALIGN = 64  # arena rows padded to 256 B
 
+# mixing-kernel tuning (blocks per CU, unroll, non-temporal, prefetch, register-indexed); the
+# library's own defaults match, this is what tests restore after sweeping variants
+DEFAULT_TUNE = (4, 1, 1, 0, 0)
+
 
 def partition(n, nranks):
     """Contiguous worker blocks [(row_base, n_local)] per rank (sizes differ by at most 1)."""

@@ -92,9 +92,11 @@ int mx_plan_build(const uint8_t* flags_dev, int64_t T, int M, const int32_t* par
  */
 int mx_mix_tile(int n_slots);
 /* Tuning hook of the mixing kernel (grid = CUs x blocks_per_cu persistent workgroups; unroll =
- * 16-byte accesses per lane per row per tile, 1 or 2; nontemporal = streaming load/store hints).
+ * 16-byte accesses per lane per row per tile, 1 or 2; nontemporal = streaming load/store hints;
+ * prefetch = issue the next tile's loads before mixing/storing the current one; regidx = use
+ * the register-indexed kernel instead of the LDS-column one when n_slots <= 8).
  * Changes the tile size: rebuild layouts (mx_mix_layout) after calling it. */
-int mx_mix_tune(int blocks_per_cu, int unroll, int nontemporal);
+int mx_mix_tune(int blocks_per_cu, int unroll, int nontemporal, int prefetch, int regidx);
 int mx_mix_layout(const int64_t* seg_len_host, int nseg, int n_slots, int64_t* tile_off_host);
 int mx_gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev,
                   const int64_t* tile_off_dev, const uint8_t* seg_vec_dev, int nseg,

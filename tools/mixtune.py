@@ -1,5 +1,4 @@
 """Sweep mixing-kernel tunings on the headline shape (8 workers x 25.6M, graph 0, full rounds)."""
-import ctypes
 import importlib
 import json
 import os
@@ -10,10 +9,11 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
 pkg = importlib.import_module("270-matcha-a-matching-based-link-scheduling-strategy-to-speed-up-distributed-optimization_amd")
-from tests.conftest import Topo  # noqa: E402
+from conftest import Topo  # noqa: E402
 
-n, P = 8, 25_600_000
+n, P = 8, int(os.environ.get("MIXTUNE_P", 25_600_000))
 gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, n, 4, True)
 topo = Topo(gp.neighbors_info, 2 / 7, np.ones((4, 5), np.uint8))
 grp = pkg.VirtualWorkerGroup(topo, numel=P)
@@ -22,7 +22,7 @@ for i in range(n):
 BYTES = 2 * n * P * 4
 
 
-def timeit(fn, reps=30, warm=5):
+def timeit(fn, reps=40, warm=5):
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
@@ -36,20 +36,26 @@ def timeit(fn, reps=30, warm=5):
     return float(np.median(ms)), float(ms.min())
 
 
+configs = []
+for spec in sys.argv[1:] or ["sweep"]:
+    if spec == "sweep":
+        for rg in (0, 1):
+            for pf in (0, 1):
+                for bpc in (2, 3, 4, 5, 6, 8):
+                    configs.append((bpc, 1, 1, pf, rg))
+    else:
+        configs.append(tuple(int(x) for x in spec.split(",")))
 res = []
+for cfg in configs:
+    assert pkg.lib.mx_mix_tune(*cfg) == 0
+    lay = pkg.Layout([P], [[grp.arena[r].data_ptr()] for r in range(n)], grp.engine.n_slots)
+    med, mn = timeit(lambda: grp.engine.mix(0, lay))
+    res.append({"cfg": "bpc=%d U=%d NT=%d PF=%d REG=%d" % cfg, "med_us": med * 1e3, "min_us": mn * 1e3,
+                "TBps": BYTES / med / 1e9, "frac": BYTES / med / 1e9 / 8.0})
+    print(json.dumps(res[-1]), flush=True)
 src = torch.empty((n, P), device="cuda")
 dst = torch.empty_like(src)
 med, mn = timeit(lambda: dst.copy_(src))
-res.append({"cfg": "torch copy_ (same bytes)", "med_us": med * 1e3, "TBps": BYTES / med / 1e9})
-for bpc in (1, 2, 3, 4, 6, 8, 16):
-    for U in (1, 2):
-        for NT in (0, 1):
-            assert pkg.lib.mx_mix_tune(bpc, U, NT) == 0
-            lay = pkg.Layout([P], [[grp.arena[r].data_ptr()] for r in range(n)], grp.engine.n_slots)
-            med, mn = timeit(lambda: grp.engine.mix(0, lay))
-            res.append({"cfg": f"bpc={bpc} U={U} NT={NT}", "med_us": med * 1e3, "min_us": mn * 1e3,
-                        "TBps": BYTES / med / 1e9})
-            print(json.dumps(res[-1]), flush=True)
-print(json.dumps(res[0]))
-best = min(res[1:], key=lambda r: r["med_us"])
+print(json.dumps({"cfg": "torch copy_ (same bytes)", "med_us": med * 1e3, "TBps": BYTES / med / 1e9}))
+best = min(res, key=lambda r: r["med_us"])
 print("BEST", json.dumps(best))
