@@ -17,6 +17,12 @@
 //
 // Traffic per round = 2 * n_active * P * 4 bytes (+ n_remote * P * 4 read of the slab): the
 // HBM roofline of the north star.  No MFMA: ~0.25 flop/byte.
+//
+// Scheduling: a single-segment layout (the flat arena) is split into one contiguous, equal
+// (+-16 B) column range per workgroup -- no tail imbalance, long sequential streams per row;
+// multi-segment layouts (per-tensor pointers) walk tiles that never straddle a tensor.
+// A register-indexed variant (mix_kernel_reg) replaces the LDS column by one register vector
+// indexed through s_set_gpr_idx (uniform slot) when n_slots <= 8.
 #include "mx_common.h"
 
 namespace {
@@ -46,8 +52,109 @@ __device__ __forceinline__ void st(float* p, const F& v) {
     else *reinterpret_cast<F*>(p) = v;
 }
 
-// VEC floats per lane access (16 B for VEC = 4), NS slots (LDS rows), U accesses per lane per
-// row per tile (U * 256 * VEC floats per tile), NT: non-temporal (streaming) loads/stores.
+
+// Plan record of this iteration, decoded into LDS (see mx_plan_build); returns the bit mask of
+// slots that must be loaded, or 0 when every flag of the round is 0.
+template <int NS>
+struct PlanLds {
+    int32_t w[mx::kPlanHeader + 2 * NS + NS * kMaxM];
+};
+
+template <int NS>
+__device__ __forceinline__ uint64_t load_plan(PlanLds<NS>& sp, const int32_t* plan, int64_t iter,
+                                              int n_local, int M) {
+    const int64_t W = mx::plan_words(n_local, M);
+    const int32_t* rec = plan + iter * W;
+    for (int i = threadIdx.x; i < W; i += kTPB) sp.w[i] = rec[i];
+    __syncthreads();
+    if (sp.w[0] == 0) return 0;
+    const int n_remote = sp.w[1];
+    const int32_t* deg = sp.w + mx::kPlanHeader;
+    uint64_t need = 0;
+    for (int r = 0; r < n_local; ++r)
+        if (deg[r] > 0) need |= 1ull << r;
+    for (int k = 0; k < n_remote; ++k) need |= 1ull << (n_local + k);
+    return need;
+}
+
+// Where this lane works in the workgroup's i-th iteration.  A lane's u-th access covers columns
+// [(g + u*256) * VEC, +VEC) of segment `seg`; columns >= lim are outside its range.
+struct Sched {
+    bool chunked;
+    int nseg;
+    const int64_t* seg_len;
+    const int64_t* tile_off;
+    int64_t total_tiles, gb, ge, niter;
+
+    template <int VEC, int U>
+    __device__ __forceinline__ void init(bool chunked_, int nseg_, const int64_t* seg_len_,
+                                         const int64_t* tile_off_, int64_t total_tiles_) {
+        chunked = chunked_;
+        nseg = nseg_;
+        seg_len = seg_len_;
+        tile_off = tile_off_;
+        total_tiles = total_tiles_;
+        if (chunked) {   // equal contiguous group ranges per workgroup
+            const int64_t G = (seg_len[0] + VEC - 1) / VEC;
+            gb = (int64_t)blockIdx.x * G / gridDim.x;
+            ge = ((int64_t)blockIdx.x + 1) * G / gridDim.x;
+            niter = (ge - gb + U * kTPB - 1) / (U * kTPB);
+        } else {         // tiles strided over the grid
+            niter = total_tiles > blockIdx.x ? (total_tiles - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
+        }
+    }
+
+    template <int VEC, int U>
+    __device__ __forceinline__ void at(int64_t i, int& seg, int64_t& g, int64_t& lim) const {
+        if (chunked) {
+            seg = 0;
+            g = gb + i * (U * kTPB) + threadIdx.x;
+            const int64_t e = ge * VEC;
+            lim = seg_len[0] < e ? seg_len[0] : e;
+        } else {
+            const int64_t tile = blockIdx.x + i * gridDim.x;
+            int lo = 0, hi = nseg;
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (tile_off[mid] <= tile) lo = mid; else hi = mid;
+            }
+            seg = lo;
+            g = (tile - tile_off[seg]) * (U * kTPB) + threadIdx.x;
+            lim = seg_len[seg];
+        }
+    }
+};
+
+// one lane's U accesses of one slot: 16-byte vector loads when the whole span is in range and
+// aligned, element loads (zero-filled beyond lim) otherwise
+template <int VEC, int U, bool NT, typename F>
+__device__ __forceinline__ void load_slot(F (&v)[U], const float* row, int64_t g, int64_t lim, bool vec_ok) {
+    const bool full = vec_ok && (g + (U - 1) * kTPB) * VEC + VEC <= lim;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t c = (g + (int64_t)u * kTPB) * VEC;
+        if (full) {
+            v[u] = ld<NT, F>(row + c);
+        } else {
+#pragma unroll
+            for (int j = 0; j < VEC; ++j) v[u][j] = (c + j < lim) ? row[c + j] : 0.0f;
+        }
+    }
+}
+
+template <int VEC, bool NT, typename F>
+__device__ __forceinline__ void store_one(float* row, int64_t c, int64_t lim, bool full, const F& a) {
+    if (full) {
+        st<NT, F>(row + c, a);
+    } else {
+#pragma unroll
+        for (int j = 0; j < VEC; ++j)
+            if (c + j < lim) row[c + j] = a[j];
+    }
+}
+
+// LDS-column kernel.  VEC floats per access (16 B for VEC = 4), NS slots, U accesses per lane
+// per slot per iteration, NT non-temporal loads/stores, PF prefetch of the next iteration.
 template <int VEC, int NS, int U, bool NT, bool PF>
 __global__ __launch_bounds__(kTPB) void mix_kernel(float* const* __restrict__ seg_ptrs,
                                                    const int64_t* __restrict__ seg_len,
@@ -55,92 +162,49 @@ __global__ __launch_bounds__(kTPB) void mix_kernel(float* const* __restrict__ se
                                                    const uint8_t* __restrict__ seg_vec, int nseg,
                                                    int64_t total_tiles, int n_slots,
                                                    const int32_t* __restrict__ plan, int64_t iter,
-                                                   int n_local, int M, float alpha) {
+                                                   int n_local, int M, float alpha, int chunked) {
     using F = typename VT<VEC>::type;
-    constexpr int TILE = kTPB * VEC * U;
     __shared__ F lds[NS][U][kTPB];
-    __shared__ int32_t sp[mx::kPlanHeader + 2 * NS + NS * kMaxM];
-
+    __shared__ PlanLds<NS> sp;
     const int tid = threadIdx.x;
-    const int64_t W = mx::plan_words(n_local, M);
-    const int32_t* rec = plan + iter * W;
-    for (int i = tid; i < W; i += kTPB) sp[i] = rec[i];
-    __syncthreads();
-    if (sp[0] == 0) return;  // all flags zero: the reference returns before any I/O
-
-    const int n_remote = sp[1];
-    const int32_t* deg = sp + mx::kPlanHeader;
+    const uint64_t need = load_plan<NS>(sp, plan, iter, n_local, M);
+    if (need == 0) return;                    // all flags zero: the reference does no I/O
+    const int32_t* deg = sp.w + mx::kPlanHeader;
     const float* sw = reinterpret_cast<const float*>(deg + n_local);
     const int32_t* src = deg + 2 * n_local;
-    uint64_t need = 0;
-    for (int r = 0; r < n_local; ++r)
-        if (deg[r] > 0) need |= 1ull << r;
-    for (int k = 0; k < n_remote; ++k) need |= 1ull << (n_local + k);
 
-    // tile -> (segment, first column of this lane, full-vector flag)
-    auto locate = [&](int64_t tile, int& seg, int64_t& c0, bool& full) {
-        seg = 0;
-        if (nseg > 1) {
-            int lo = 0, hi = nseg;
-            while (hi - lo > 1) {
-                const int mid = (lo + hi) >> 1;
-                if (tile_off[mid] <= tile) lo = mid; else hi = mid;
-            }
-            seg = lo;
-        }
-        const int64_t len = seg_len[seg];
-        c0 = (tile - tile_off[seg]) * TILE + (int64_t)tid * VEC;
-        full = (c0 + (int64_t)(U - 1) * kTPB * VEC + VEC <= len) && seg_vec[seg];
-    };
+    Sched sc;
+    sc.init<VEC, U>(chunked != 0, nseg, seg_len, tile_off, total_tiles);
+    if (sc.niter == 0) return;
     F v[NS][U];
-    auto load = [&](int seg, int64_t c0, bool full) {
-        const int64_t len = seg_len[seg];
+    auto load_all = [&](int seg, int64_t g, int64_t lim) {
         float* const* ptrs = seg_ptrs + (int64_t)seg * n_slots;
+        const bool vec_ok = seg_vec[seg] != 0;
 #pragma unroll
-        for (int k = 0; k < NS; ++k) {
-            if ((need >> k) & 1ull) {
-                const float* p = ptrs[k] + c0;
-#pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    if (full) {
-                        v[k][u] = ld<NT, F>(p + u * kTPB * VEC);
-                    } else {
-                        const int64_t c = c0 + (int64_t)u * kTPB * VEC;
-#pragma unroll
-                        for (int j = 0; j < VEC; ++j)
-                            v[k][u][j] = (c + j < len) ? p[u * kTPB * VEC + j] : 0.0f;
-                    }
-                }
-            }
-        }
+        for (int k = 0; k < NS; ++k)
+            if ((need >> k) & 1ull) load_slot<VEC, U, NT>(v[k], ptrs[k], g, lim, vec_ok);
     };
-
-    int64_t tile = blockIdx.x;
-    if (tile >= total_tiles) return;
     int seg;
-    int64_t c0;
-    bool full;
-    locate(tile, seg, c0, full);
-    load(seg, c0, full);
-    while (true) {
+    int64_t g, lim;
+    sc.at<VEC, U>(0, seg, g, lim);
+    load_all(seg, g, lim);
+    for (int64_t i = 0; i < sc.niter; ++i) {
 #pragma unroll
         for (int k = 0; k < NS; ++k)
             if ((need >> k) & 1ull) {
 #pragma unroll
                 for (int u = 0; u < U; ++u) lds[k][u][tid] = v[k][u];
             }
-        // registers are free again: with PF, start streaming the next tile before this one is
-        // mixed and stored, so its loads are older than this tile's stores in vmcnt order
-        const int64_t next = tile + gridDim.x;
+        // registers are free again: with PF the next iteration's loads are issued now, ahead of
+        // (older than) this iteration's stores in vmcnt order
         int nseg_i = 0;
-        int64_t nc0 = 0;
-        bool nfull = false;
-        if (PF && next < total_tiles) {
-            locate(next, nseg_i, nc0, nfull);
-            load(nseg_i, nc0, nfull);
+        int64_t ng = 0, nlim = 0;
+        if (PF && i + 1 < sc.niter) {
+            sc.at<VEC, U>(i + 1, nseg_i, ng, nlim);
+            load_all(nseg_i, ng, nlim);
         }
-        const int64_t len = seg_len[seg];
         float* const* ptrs = seg_ptrs + (int64_t)seg * n_slots;
+        const bool full = seg_vec[seg] && (g + (U - 1) * kTPB) * VEC + VEC <= lim;
         for (int r = 0; r < n_local; ++r) {
             const int d = deg[r];
             if (d == 0) continue;
@@ -159,40 +223,30 @@ __global__ __launch_bounds__(kTPB) void mix_kernel(float* const* __restrict__ se
                 }
             }
             const float s = sw[r];
-            float* p = ptrs[r] + c0;
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const F xs = lds[r][u][tid];
 #pragma unroll
                 for (int j = 0; j < VEC; ++j) acc[u][j] = __builtin_fmaf(s, xs[j], acc[u][j]);
-                if (full) {
-                    st<NT, F>(p + u * kTPB * VEC, acc[u]);
-                } else {
-                    const int64_t c = c0 + (int64_t)u * kTPB * VEC;
-#pragma unroll
-                    for (int j = 0; j < VEC; ++j)
-                        if (c + j < len) p[u * kTPB * VEC + j] = acc[u][j];
-                }
+                store_one<VEC, NT>(ptrs[r], (g + (int64_t)u * kTPB) * VEC, lim, full, acc[u]);
             }
         }
-        if (next >= total_tiles) break;
-        tile = next;
-        if (PF) {
-            seg = nseg_i;
-            c0 = nc0;
-            full = nfull;
-        } else {
-            locate(tile, seg, c0, full);
-            load(seg, c0, full);
+        if (i + 1 < sc.niter) {
+            if (PF) {
+                seg = nseg_i;
+                g = ng;
+                lim = nlim;
+            } else {
+                sc.at<VEC, U>(i + 1, seg, g, lim);
+                load_all(seg, g, lim);
+            }
         }
     }
 }
 
-
-// Register-indexed variant (VEC = 4): the tile of every slot is kept in ONE register vector of
-// NS*4 floats; the wave-uniform partner slot indexes it through s_set_gpr_idx (VGPR indexing
-// mode), so no LDS is used and occupancy is bounded by VGPRs only.  PF double-buffers the
-// vector so the next tile's loads are in flight while this one is mixed and stored.
+// Register-indexed kernel (VEC = 4, NS <= 8): every slot's column lives in ONE register vector
+// of NS*4 floats; the wave-uniform partner slot indexes it through s_set_gpr_idx (VGPR
+// indexing), so no LDS is used and occupancy is bounded by VGPRs only.
 template <int NS>
 using RegVec = float __attribute__((ext_vector_type(NS * 4)));
 
@@ -203,78 +257,48 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_reg(float* const* __restrict_
                                                        const uint8_t* __restrict__ seg_vec, int nseg,
                                                        int64_t total_tiles, int n_slots,
                                                        const int32_t* __restrict__ plan, int64_t iter,
-                                                       int n_local, int M, float alpha) {
+                                                       int n_local, int M, float alpha, int chunked) {
     using F = typename VT<4>::type;
-    constexpr int TILE = kTPB * 4;
-    __shared__ int32_t sp[mx::kPlanHeader + 2 * NS + NS * kMaxM];
-    const int tid = threadIdx.x;
-    const int64_t W = mx::plan_words(n_local, M);
-    const int32_t* rec = plan + iter * W;
-    for (int i = tid; i < W; i += kTPB) sp[i] = rec[i];
-    __syncthreads();
-    if (sp[0] == 0) return;
-    const int n_remote = sp[1];
-    const int32_t* deg = sp + mx::kPlanHeader;
+    __shared__ PlanLds<NS> sp;
+    const uint64_t need = load_plan<NS>(sp, plan, iter, n_local, M);
+    if (need == 0) return;
+    const int32_t* deg = sp.w + mx::kPlanHeader;
     const float* sw = reinterpret_cast<const float*>(deg + n_local);
     const int32_t* src = deg + 2 * n_local;
-    uint64_t need = 0;
-    for (int r = 0; r < n_local; ++r)
-        if (deg[r] > 0) need |= 1ull << r;
-    for (int k = 0; k < n_remote; ++k) need |= 1ull << (n_local + k);
 
-    auto locate = [&](int64_t tile, int& seg, int64_t& c0, bool& full) {
-        seg = 0;
-        if (nseg > 1) {
-            int lo = 0, hi = nseg;
-            while (hi - lo > 1) {
-                const int mid = (lo + hi) >> 1;
-                if (tile_off[mid] <= tile) lo = mid; else hi = mid;
-            }
-            seg = lo;
-        }
-        c0 = (tile - tile_off[seg]) * TILE + (int64_t)tid * 4;
-        full = (c0 + 4 <= seg_len[seg]) && seg_vec[seg];
-    };
-    auto load = [&](RegVec<NS>& a, int seg, int64_t c0, bool full) {
-        const int64_t len = seg_len[seg];
+    Sched sc;
+    sc.init<4, 1>(chunked != 0, nseg, seg_len, tile_off, total_tiles);
+    if (sc.niter == 0) return;
+    auto load_all = [&](RegVec<NS>& a, int seg, int64_t g, int64_t lim) {
         float* const* ptrs = seg_ptrs + (int64_t)seg * n_slots;
+        const bool vec_ok = seg_vec[seg] != 0;
 #pragma unroll
         for (int k = 0; k < NS; ++k) {
             if ((need >> k) & 1ull) {
-                const float* p = ptrs[k] + c0;
-                if (full) {
-                    const F q = ld<NT, F>(p);
-                    a[4 * k + 0] = q[0];
-                    a[4 * k + 1] = q[1];
-                    a[4 * k + 2] = q[2];
-                    a[4 * k + 3] = q[3];
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) a[4 * k + j] = (c0 + j < len) ? p[j] : 0.0f;
-                }
+                F q[1];
+                load_slot<4, 1, NT>(q, ptrs[k], g, lim, vec_ok);
+                a[4 * k + 0] = q[0][0];
+                a[4 * k + 1] = q[0][1];
+                a[4 * k + 2] = q[0][2];
+                a[4 * k + 3] = q[0][3];
             }
         }
     };
-
-    int64_t tile = blockIdx.x;
-    if (tile >= total_tiles) return;
     int seg;
-    int64_t c0;
-    bool full;
-    locate(tile, seg, c0, full);
+    int64_t g, lim;
+    sc.at<4, 1>(0, seg, g, lim);
     RegVec<NS> cur, nxt;
-    load(cur, seg, c0, full);
-    while (true) {
-        const int64_t next = tile + gridDim.x;
+    load_all(cur, seg, g, lim);
+    for (int64_t i = 0; i < sc.niter; ++i) {
         int nseg_i = 0;
-        int64_t nc0 = 0;
-        bool nfull = false;
-        if (PF && next < total_tiles) {
-            locate(next, nseg_i, nc0, nfull);
-            load(nxt, nseg_i, nc0, nfull);
+        int64_t ng = 0, nlim = 0;
+        if (PF && i + 1 < sc.niter) {
+            sc.at<4, 1>(i + 1, nseg_i, ng, nlim);
+            load_all(nxt, nseg_i, ng, nlim);
         }
-        const int64_t len = seg_len[seg];
         float* const* ptrs = seg_ptrs + (int64_t)seg * n_slots;
+        const int64_t c = g * 4;
+        const bool full = seg_vec[seg] && c + 4 <= lim;
         for (int r = 0; r < n_local; ++r) {
             const int d = deg[r];
             if (d == 0) continue;
@@ -292,25 +316,18 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_reg(float* const* __restrict_
             acc[1] = __builtin_fmaf(s, cur[r4 + 1], acc[1]);
             acc[2] = __builtin_fmaf(s, cur[r4 + 2], acc[2]);
             acc[3] = __builtin_fmaf(s, cur[r4 + 3], acc[3]);
-            float* p = ptrs[r] + c0;
-            if (full) {
-                st<NT, F>(p, acc);
-            } else {
-#pragma unroll
-                for (int j = 0; j < 4; ++j)
-                    if (c0 + j < len) p[j] = acc[j];
-            }
+            store_one<4, NT>(ptrs[r], c, lim, full, acc);
         }
-        if (next >= total_tiles) break;
-        tile = next;
-        if (PF) {
-            seg = nseg_i;
-            c0 = nc0;
-            full = nfull;
-            cur = nxt;
-        } else {
-            locate(tile, seg, c0, full);
-            load(cur, seg, c0, full);
+        if (i + 1 < sc.niter) {
+            if (PF) {
+                seg = nseg_i;
+                g = ng;
+                lim = nlim;
+                cur = nxt;
+            } else {
+                sc.at<4, 1>(i + 1, seg, g, lim);
+                load_all(cur, seg, g, lim);
+            }
         }
     }
 }
@@ -349,29 +366,32 @@ int cu_count() {
     return v;
 }
 
+// grid: CUs x blocks_per_cu persistent workgroups, never more than there are tiles; a single
+// segment is split into equal contiguous chunks (chunked = 1)
+inline int64_t grid_for(int64_t total_tiles) {
+    int64_t grid = (int64_t)cu_count() * g_tune.blocks_per_cu;
+    if (grid > total_tiles) grid = total_tiles;
+    return grid < 1 ? 1 : grid;
+}
+
 template <int VEC, int NS, int U, bool NT, bool PF>
 int launch(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_off,
            const uint8_t* seg_vec, int nseg, int n_slots, const int32_t* plan, int64_t iter,
            int n_local, int M, float alpha, int64_t total_tiles, hipStream_t st) {
-    int64_t grid = (int64_t)cu_count() * g_tune.blocks_per_cu;
-    if (grid > total_tiles) grid = total_tiles;
-    if (grid < 1) grid = 1;
-    hipLaunchKernelGGL((mix_kernel<VEC, NS, U, NT, PF>), dim3((unsigned)grid), dim3(kTPB), 0, st, seg_ptrs,
-                       seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan, iter, n_local,
-                       M, alpha);
+    hipLaunchKernelGGL((mix_kernel<VEC, NS, U, NT, PF>), dim3((unsigned)grid_for(total_tiles)), dim3(kTPB),
+                       0, st, seg_ptrs, seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan,
+                       iter, n_local, M, alpha, nseg == 1 ? 1 : 0);
     MX_LAUNCH_CHECK();
     return MX_OK;
 }
+
 template <int NS, bool NT, bool PF>
 int launch_reg(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_off,
                const uint8_t* seg_vec, int nseg, int n_slots, const int32_t* plan, int64_t iter,
                int n_local, int M, float alpha, int64_t total_tiles, hipStream_t st) {
-    int64_t grid = (int64_t)cu_count() * g_tune.blocks_per_cu;
-    if (grid > total_tiles) grid = total_tiles;
-    if (grid < 1) grid = 1;
-    hipLaunchKernelGGL((mix_kernel_reg<NS, NT, PF>), dim3((unsigned)grid), dim3(kTPB), 0, st, seg_ptrs,
-                       seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan, iter, n_local,
-                       M, alpha);
+    hipLaunchKernelGGL((mix_kernel_reg<NS, NT, PF>), dim3((unsigned)grid_for(total_tiles)), dim3(kTPB),
+                       0, st, seg_ptrs, seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan,
+                       iter, n_local, M, alpha, nseg == 1 ? 1 : 0);
     MX_LAUNCH_CHECK();
     return MX_OK;
 }
