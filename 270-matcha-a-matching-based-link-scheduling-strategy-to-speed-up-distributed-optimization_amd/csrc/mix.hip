@@ -351,6 +351,7 @@ struct Tune {
     int nontemporal = 1;
     int prefetch = 0;
     int regidx = 0;      // 1: register-indexed kernel (n_slots <= 8; wider spills), 0: LDS-column kernel
+    int chunked = 1;     // single-segment layouts: 1 = equal contiguous chunk per workgroup, 0 = tile stride
 };
 Tune g_tune;
 
@@ -380,7 +381,7 @@ int launch(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_o
            int n_local, int M, float alpha, int64_t total_tiles, hipStream_t st) {
     hipLaunchKernelGGL((mix_kernel<VEC, NS, U, NT, PF>), dim3((unsigned)grid_for(total_tiles)), dim3(kTPB),
                        0, st, seg_ptrs, seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan,
-                       iter, n_local, M, alpha, nseg == 1 ? 1 : 0);
+                       iter, n_local, M, alpha, (nseg == 1 && g_tune.chunked) ? 1 : 0);
     MX_LAUNCH_CHECK();
     return MX_OK;
 }
@@ -391,7 +392,7 @@ int launch_reg(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* ti
                int n_local, int M, float alpha, int64_t total_tiles, hipStream_t st) {
     hipLaunchKernelGGL((mix_kernel_reg<NS, NT, PF>), dim3((unsigned)grid_for(total_tiles)), dim3(kTPB),
                        0, st, seg_ptrs, seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan,
-                       iter, n_local, M, alpha, nseg == 1 ? 1 : 0);
+                       iter, n_local, M, alpha, (nseg == 1 && g_tune.chunked) ? 1 : 0);
     MX_LAUNCH_CHECK();
     return MX_OK;
 }
@@ -403,15 +404,43 @@ extern "C" int mx_mix_tile(int n_slots) {
     return c.vec * kTPB * unroll_for(c.ns);
 }
 
-extern "C" int mx_mix_tune(int blocks_per_cu, int unroll, int nontemporal, int prefetch, int regidx) {
-    MX_CHECK(blocks_per_cu >= 1 && blocks_per_cu <= 64, "mx_mix_tune: blocks_per_cu %d", blocks_per_cu);
-    MX_CHECK(unroll == 1 || unroll == 2, "mx_mix_tune: unroll %d", unroll);
-    g_tune.blocks_per_cu = blocks_per_cu;
-    g_tune.unroll = unroll;
-    g_tune.nontemporal = nontemporal ? 1 : 0;
-    g_tune.prefetch = prefetch ? 1 : 0;
-    g_tune.regidx = regidx ? 1 : 0;
+extern "C" int mx_mix_set(const char* key, int value) {
+    MX_CHECK(key, "mx_mix_set: null key");
+    int* slot = nullptr;
+    if (!strcmp(key, "blocks_per_cu")) {
+        MX_CHECK(value >= 1 && value <= 64, "mx_mix_set: blocks_per_cu %d", value);
+        slot = &g_tune.blocks_per_cu;
+    } else if (!strcmp(key, "unroll")) {
+        MX_CHECK(value == 1 || value == 2, "mx_mix_set: unroll %d", value);
+        slot = &g_tune.unroll;
+    } else if (!strcmp(key, "nontemporal")) {
+        slot = &g_tune.nontemporal;
+        value = value ? 1 : 0;
+    } else if (!strcmp(key, "prefetch")) {
+        slot = &g_tune.prefetch;
+        value = value ? 1 : 0;
+    } else if (!strcmp(key, "regidx")) {
+        slot = &g_tune.regidx;
+        value = value ? 1 : 0;
+    } else if (!strcmp(key, "chunked")) {
+        slot = &g_tune.chunked;
+        value = value ? 1 : 0;
+    }
+    MX_CHECK(slot, "mx_mix_set: unknown key '%s'", key);
+    *slot = value;
     return MX_OK;
+}
+
+extern "C" int mx_mix_get(const char* key) {
+    if (!key) return MX_ERR_INVALID;
+    if (!strcmp(key, "blocks_per_cu")) return g_tune.blocks_per_cu;
+    if (!strcmp(key, "unroll")) return g_tune.unroll;
+    if (!strcmp(key, "nontemporal")) return g_tune.nontemporal;
+    if (!strcmp(key, "prefetch")) return g_tune.prefetch;
+    if (!strcmp(key, "regidx")) return g_tune.regidx;
+    if (!strcmp(key, "chunked")) return g_tune.chunked;
+    mx::set_error("mx_mix_get: unknown key '%s'", key);
+    return MX_ERR_INVALID;
 }
 
 extern "C" int mx_mix_layout(const int64_t* seg_len_host, int nseg, int n_slots, int64_t* tile_off_host) {

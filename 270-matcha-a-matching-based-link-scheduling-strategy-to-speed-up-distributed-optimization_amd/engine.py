@@ -22,9 +22,17 @@ from ._lib import MXError, check, lib, require_device, stream_ptr
 
 ROW_ALIGN = 64  # arena rows padded to 256 B
 
-# mixing-kernel tuning (blocks per CU, unroll, non-temporal, prefetch, register-indexed); the
-# library's own defaults match, this is what tests restore after sweeping variants
-DEFAULT_TUNE = (4, 1, 1, 0, 0)
+TUNE_KEYS = ("blocks_per_cu", "unroll", "nontemporal", "prefetch", "regidx", "chunked")
+
+
+def mix_tuning():
+    """Current mixing-kernel knobs (include/matcha_gossip.h, mx_mix_set)."""
+    return {k: int(lib.mx_mix_get(k.encode())) for k in TUNE_KEYS}
+
+
+def set_mix_tuning(**knobs):
+    for k, v in knobs.items():
+        check(lib.mx_mix_set(k.encode(), int(v)), "mx_mix_set")
 
 
 def partition(n, nranks):

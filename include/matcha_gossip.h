@@ -91,13 +91,17 @@ int mx_plan_build(const uint8_t* flags_dev, int64_t T, int M, const int32_t* par
  * Rows with degree 0 are neither read nor written.  No-op when the record's flags are all 0.
  */
 int mx_mix_tile(int n_slots);
-/* Tuning hook of the mixing kernel (grid = CUs x blocks_per_cu persistent workgroups; unroll =
- * 16-byte accesses per lane per row per tile, 1 or 2; nontemporal = streaming load/store hints;
- * prefetch = issue the next tile's loads before mixing/storing the current one; regidx = use
- * the register-indexed kernel instead of the LDS-column one when n_slots <= 8).
- * Changes the tile size: rebuild layouts (mx_mix_layout) after calling it. */
-int mx_mix_tune(int blocks_per_cu, int unroll, int nontemporal, int prefetch, int regidx);
-int mx_mix_layout(const int64_t* seg_len_host, int nseg, int n_slots, int64_t* tile_off_host);
+/* Tuning knobs of the mixing kernel (process-wide), by name:
+ *   blocks_per_cu  persistent workgroups per CU (grid = CUs x this, capped by the tile count)
+ *   unroll         16-byte accesses per lane per slot per iteration, 1 or 2 (LDS kernel, n_slots <= 8)
+ *   nontemporal    streaming (non-temporal) load/store hints
+ *   prefetch       issue the next iteration's loads before mixing/storing the current one
+ *   regidx         register-indexed kernel (no LDS) instead of the LDS-column one, n_slots <= 8
+ *   chunked        single-segment layouts: equal contiguous chunk per workgroup (1) or tile stride (0)
+ * "unroll" changes the tile size: rebuild layouts (mx_mix_layout) after setting it.
+ * mx_mix_get returns the current value (negative on an unknown key). */
+int mx_mix_set(const char* key, int value);
+int mx_mix_get(const char* key);
 int mx_gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev,
                   const int64_t* tile_off_dev, const uint8_t* seg_vec_dev, int nseg,
                   int64_t total_tiles, int n_slots, const int32_t* plan_dev, int64_t iter,

@@ -244,19 +244,21 @@ def test_flatten_unflatten_scatter(pkg):
 
 
 # ------------------------------------------------------------------------------------ tuning variants
-VARIANTS = [(bpc, u, nt, pf, rg) for bpc in (1, 3) for u in (1, 2) for nt in (0, 1) for pf in (0, 1)
-            for rg in (0, 1) if not (rg and u == 2)]
+VARIANTS = [(bpc, u, nt, pf, rg, ch) for bpc in (1, 5) for u in (1, 2) for nt in (0, 1) for pf in (0, 1)
+            for rg in (0, 1) for ch in (0, 1) if not (rg and u == 2)]
 
 
-@pytest.mark.parametrize("bpc,u,nt,pf,rg", VARIANTS)
-def test_mix_every_tuning_variant(pkg, O, bpc, u, nt, pf, rg):
-    """Each kernel variant (LDS / register-indexed, unroll, non-temporal, prefetch, grid) is
-    bit-exact on ragged multi-segment layouts and a 16-slot graph."""
+@pytest.mark.parametrize("bpc,u,nt,pf,rg,ch", VARIANTS)
+def test_mix_every_tuning_variant(pkg, O, bpc, u, nt, pf, rg, ch):
+    """Each kernel variant (LDS / register-indexed, unroll, non-temporal, prefetch, grid, chunked
+    vs tile-strided) is bit-exact on a flat arena, ragged multi-segment layouts and a 16-slot graph."""
+    saved = pkg.engine.mix_tuning()
     try:
-        assert pkg.lib.mx_mix_tune(bpc, u, nt, pf, rg) == 0
-        for gid in (0, 2):
+        pkg.engine.set_mix_tuning(blocks_per_cu=bpc, unroll=u, nontemporal=nt, prefetch=pf, regidx=rg,
+                                  chunked=ch)
+        for gid, lens in ((0, [1, 3, 1024, 1027, 5, 4096 + 3, 0, 77, 10_000]), (2, [1, 3, 1027, 5, 9000]),
+                          (0, [300_001])):
             n = pkg.GRAPH_SIZES[gid]
-            lens = [1, 3, 1024, 1027, 5, 4096 + 3, 0, 77, 10_000]
             gp = pkg.GraphProcessor(pkg.select_graph(gid), 1.0, 0, n, 4, True)
             M = len(gp.neighbors_info)
             flags = np.ones((3, M), np.uint8)
@@ -267,7 +269,7 @@ def test_mix_every_tuning_variant(pkg, O, bpc, u, nt, pf, rg):
             P = sum(lens)
             X = np.stack([O.synth(300 + i, P) for i in range(n)])
             big = torch.from_numpy(np.concatenate([X, X[:, :4]], axis=1)).cuda()
-            base = 0 if gid == 0 else 1
+            base = 1 if gid == 2 else 0
             cuts = np.cumsum([0] + lens)
             ptrs = [[big[i].data_ptr() + 4 * (base + int(cuts[s])) for s in range(len(lens))] for i in range(n)]
             big[:, base:base + P] = torch.from_numpy(X).cuda()
@@ -277,6 +279,6 @@ def test_mix_every_tuning_variant(pkg, O, bpc, u, nt, pf, rg):
                 X = O.decen_round(X, topo.neighbors_info, f, 0.21)
             torch.cuda.synchronize()
             got = big[:, base:base + P].cpu().numpy()
-            assert np.array_equal(got.view(np.uint32), X.view(np.uint32)), f"graph {gid}"
+            assert np.array_equal(got.view(np.uint32), X.view(np.uint32)), f"graph {gid} lens {lens}"
     finally:
-        pkg.lib.mx_mix_tune(*pkg.engine.DEFAULT_TUNE)
+        pkg.engine.set_mix_tuning(**saved)

@@ -36,26 +36,32 @@ def timeit(fn, reps=40, warm=5):
     return float(np.median(ms)), float(ms.min())
 
 
+KEYS = ("blocks_per_cu", "unroll", "nontemporal", "prefetch", "regidx", "chunked")
 configs = []
 for spec in sys.argv[1:] or ["sweep"]:
     if spec == "sweep":
-        for rg in (0, 1):
-            for pf in (0, 1):
-                for bpc in (2, 3, 4, 5, 6, 8):
-                    configs.append((bpc, 1, 1, pf, rg))
+        for rg, pf in ((0, 0), (0, 1), (1, 0), (1, 1)):
+            for ch in (0, 1):
+                for bpc in (3, 4, 5, 6, 8):
+                    configs.append((bpc, 1, 1, pf, rg, ch))
     else:
         configs.append(tuple(int(x) for x in spec.split(",")))
-res = []
-for cfg in configs:
-    assert pkg.lib.mx_mix_tune(*cfg) == 0
-    lay = pkg.Layout([P], [[grp.arena[r].data_ptr()] for r in range(n)], grp.engine.n_slots)
-    med, mn = timeit(lambda: grp.engine.mix(0, lay))
-    res.append({"cfg": "bpc=%d U=%d NT=%d PF=%d REG=%d" % cfg, "med_us": med * 1e3, "min_us": mn * 1e3,
-                "TBps": BYTES / med / 1e9, "frac": BYTES / med / 1e9 / 8.0})
-    print(json.dumps(res[-1]), flush=True)
 src = torch.empty((n, P), device="cuda")
 dst = torch.empty_like(src)
+refs = []
 med, mn = timeit(lambda: dst.copy_(src))
-print(json.dumps({"cfg": "torch copy_ (same bytes)", "med_us": med * 1e3, "TBps": BYTES / med / 1e9}))
+refs.append(med)
+res = []
+for cfg in configs:
+    pkg.engine.set_mix_tuning(**dict(zip(KEYS, cfg)))
+    lay = pkg.Layout([P], [[grp.arena[r].data_ptr()] for r in range(n)], grp.engine.n_slots)
+    med, mn = timeit(lambda: grp.engine.mix(0, lay))
+    res.append({"cfg": "bpc=%d U=%d NT=%d PF=%d REG=%d CH=%d" % cfg, "med_us": med * 1e3, "min_us": mn * 1e3,
+                "TBps": BYTES / med / 1e9, "frac": BYTES / med / 1e9 / 8.0})
+    print(json.dumps(res[-1]), flush=True)
+med, mn = timeit(lambda: dst.copy_(src))
+refs.append(med)
+print(json.dumps({"cfg": "torch copy_ (same bytes), before/after", "med_us": [r * 1e3 for r in refs],
+                  "TBps": [BYTES / r / 1e9 for r in refs]}))
 best = min(res, key=lambda r: r["med_us"])
 print("BEST", json.dumps(best))
