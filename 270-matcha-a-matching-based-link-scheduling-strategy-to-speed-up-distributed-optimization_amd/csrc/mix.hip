@@ -344,7 +344,7 @@ Cfg pick(int n_slots) {
     return {0, 0};
 }
 
-// tuning state (mx_mix_tune); defaults chosen from measurements on MI355X
+// tuning state (mx_mix_set / mx_mix_get); defaults chosen from measurements on MI355X
 struct Tune {
     int blocks_per_cu = 4;
     int unroll = 1;      // 1 or 2 accesses per lane per row per tile (NS = 8 config only)

@@ -209,7 +209,7 @@ class GossipEngine:
 
     def mix(self, it, layout, stream=None):
         if layout.tile != lib.mx_mix_tile(layout.n_slots):
-            raise MXError("layout built for another mixing tile size (mx_mix_tune changed it)")
+            raise MXError("layout built for another mixing tile size (the unroll knob changed it)")
         check(lib.mx_gossip_mix(layout.seg_ptrs.data_ptr(), layout.seg_len.data_ptr(),
                                 layout.tile_off.data_ptr(), layout.seg_vec.data_ptr(), layout.nseg,
                                 layout.total_tiles, layout.n_slots, self.plan.data_ptr(), int(it),

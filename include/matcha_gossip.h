@@ -102,6 +102,7 @@ int mx_mix_tile(int n_slots);
  * mx_mix_get returns the current value (negative on an unknown key). */
 int mx_mix_set(const char* key, int value);
 int mx_mix_get(const char* key);
+int mx_mix_layout(const int64_t* seg_len_host, int nseg, int n_slots, int64_t* tile_off_host);
 int mx_gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev,
                   const int64_t* tile_off_dev, const uint8_t* seg_vec_dev, int nseg,
                   int64_t total_tiles, int n_slots, const int32_t* plan_dev, int64_t iter,
