@@ -18,11 +18,11 @@
 // Traffic per round = 2 * n_active * P * 4 bytes (+ n_remote * P * 4 read of the slab): the
 // HBM roofline of the north star.  No MFMA: ~0.25 flop/byte.
 //
-// Scheduling: a single-segment layout (the flat arena) is split into one contiguous, equal
-// (+-16 B) column range per workgroup -- no tail imbalance, long sequential streams per row;
-// multi-segment layouts (per-tensor pointers) walk tiles that never straddle a tensor.
-// A register-indexed variant (mix_kernel_reg) replaces the LDS column by one register vector
-// indexed through s_set_gpr_idx (uniform slot) when n_slots <= 8.
+// Scheduling: by default tiles (never straddling a tensor) are strided over a persistent grid,
+// so at any moment the whole chip streams one narrow window of every row (DRAM row locality);
+// optionally (knob "chunked") a single-segment layout is split into equal contiguous ranges.
+// The default kernel for n_slots <= 8 is the register-indexed variant (mix_kernel_reg): one
+// register vector per lane indexed through s_set_gpr_idx by the wave-uniform slot, no LDS.
 #include "mx_common.h"
 
 namespace {
@@ -344,14 +344,18 @@ Cfg pick(int n_slots) {
     return {0, 0};
 }
 
-// tuning state (mx_mix_set / mx_mix_get); defaults chosen from measurements on MI355X
+// tuning state (mx_mix_set / mx_mix_get); defaults from tools/mixtune.py sweeps on MI355X
+// (8 x 25.6M graph-0 rounds): register-indexed + non-temporal + tile stride at 4 WGs/CU ran at
+// 0.95x the time of torch's copy_ of the same bytes; balanced chunks were 20-30% slower (every
+// workgroup streaming its own far-apart range loses the chip-wide DRAM row locality of the
+// tile sweep); prefetch did not pay at this occupancy.
 struct Tune {
     int blocks_per_cu = 4;
     int unroll = 1;      // 1 or 2 accesses per lane per row per tile (NS = 8 config only)
     int nontemporal = 1;
     int prefetch = 0;
-    int regidx = 0;      // 1: register-indexed kernel (n_slots <= 8; wider spills), 0: LDS-column kernel
-    int chunked = 1;     // single-segment layouts: 1 = equal contiguous chunk per workgroup, 0 = tile stride
+    int regidx = 1;      // 1: register-indexed kernel (n_slots <= 8; wider spills), 0: LDS-column kernel
+    int chunked = 0;     // single-segment layouts: 1 = equal contiguous chunk per workgroup, 0 = tile stride
 };
 Tune g_tune;
 

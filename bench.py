@@ -62,6 +62,31 @@ def cpu_baseline(pkg, partner, alpha, n, P, seconds):
                       f"(one per worker, like the mpirun ranks) of {os.cpu_count()} host CPUs"}
 
 
+def pmc_traffic(kernel_prefix="mix_kernel"):
+    """HBM bytes per launch of the mixing kernel from the newest committed rocprofv3 PMC summary
+    (tools/profile_round.sh -> profiles/rocprof_<round>.json; FETCH_SIZE x2 + WRITE_SIZE)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "rocprof_*.json")))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    vals = [v.get("hbm_bytes_per_launch") for k, v in d.get("mix_pmc", {}).items() if kernel_prefix in k]
+    vals = [v for v in vals if v]
+    return (max(vals) if vals else None), os.path.relpath(files[-1], ROOT)
+
+
+def timed_rounds(group, first, K):
+    """K rounds from iteration `first` with per-round HIP events on the launch stream."""
+    stream = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    for j in range(K):
+        ev[j][0].record(stream)
+        group.step(first + j)
+        ev[j][1].record(stream)
+    return ev
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -79,7 +104,7 @@ def main():
     n, P = args.workers, args.params
     K, W = args.steps, args.warmup
     np.random.seed(1234)
-    GP = pkg.MatchaProcessor(pkg.select_graph(args.graph), args.budget, rank, n, W + K, True)
+    GP = pkg.MatchaProcessor(pkg.select_graph(args.graph), args.budget, rank, n, W + 2 * K, True)
     group = pkg.VirtualWorkerGroup(GP, numel=P, rank=rank, nranks=world)
     for r in range(group.n_local):
         pkg._lib.check(pkg.lib.mx_synth_fill(group.rows[r].data_ptr(), P, 1234 + group.row_base + r, None))
@@ -91,13 +116,8 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    stream = torch.cuda.current_stream()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
     t0 = time.perf_counter()
-    for j in range(K):
-        ev[j][0].record(stream)
-        group.step(W + j)
-        ev[j][1].record(stream)
+    ev = timed_rounds(group, W, K)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -108,6 +128,44 @@ def main():
         tt = torch.tensor([elapsed], device="cuda")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
+    # mixing kernel alone (N > 1: without the RCCL exchange) -> its HBM roofline
+    stream = torch.cuda.current_stream()
+    mev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    for j in range(K):
+        mev[j][0].record(stream)
+        group.engine.mix(W + j, group.layout)
+        mev[j][1].record(stream)
+    torch.cuda.synchronize()
+    mix_ms = np.array([a.elapsed_time(b) for a, b in mev])
+    # secondary figure: a MATCHA C_b = 0.5 schedule on the same workers (random subsets per round)
+    matcha = None
+    if args.budget >= 1.0:
+        np.random.seed(1234)
+        GPm = pkg.MatchaProcessor(pkg.select_graph(args.graph), 0.5, rank, n, W + K, True)
+        gm = pkg.VirtualWorkerGroup(GPm, numel=P, rank=rank, nranks=world, comm=group.engine.comm)
+        for r in range(gm.n_local):
+            pkg._lib.check(pkg.lib.mx_synth_fill(gm.rows[r].data_ptr(), P, 1234 + gm.row_base + r, None))
+        for it in range(W):
+            gm.step(it)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t1 = time.perf_counter()
+        for j in range(K):
+            gm.step(W + j)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t1
+        if world > 1:
+            tt = torch.tensor([el], device="cuda")
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        fl = np.asarray(GPm.active_flags[W:W + K])
+        matcha = {"budget": 0.5, "rounds_per_s": K / el, "probabilities": [round(float(x), 6) for x in GPm.probabilities],
+                  "alpha": GPm.neighbor_weight, "mean_active_matchings": float(fl.sum(1).mean()),
+                  "skipped_rounds": int((fl.sum(1) == 0).sum())}
+        del gm
 
     partner = np.asarray(GP.neighbors_info, np.int32)
     flags = np.asarray(GP.active_flags[W:W + K], np.uint8)
@@ -139,8 +197,10 @@ def main():
         hbm_bytes.append(2 * act * P * 4 + remote * P * 4)
         link_bytes.append(max(links.values()) if links else 0)
     avg_ms = float(step_ms.mean())
+    mix_avg_ms = float(mix_ms.mean())
     mix_bytes = float(np.mean(hbm_bytes))
-    achieved = mix_bytes / (avg_ms * 1e-3)
+    achieved = mix_bytes / (mix_avg_ms * 1e-3)
+    traffic, traffic_src = pmc_traffic()
 
     if rank == 0:
         out = {
@@ -162,16 +222,22 @@ def main():
                        "parallelism": f"{n} workers over {world} GPU(s), contiguous blocks"},
             "roofline": {"bound": "hbm", "kernel": "mix_kernel (mx_gossip_mix)",
                          "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK, "traffic": None,
-                         "bytes_per_launch": mix_bytes, "avg_launch_ms": avg_ms if world == 1 else None,
-                         "note": ("per-launch HIP events on the launch stream" if world == 1 else
-                                  "N>1: events bracket exchange+mix; see xgmi")},
+                         "frac": achieved / HBM_PEAK, "traffic": traffic,
+                         "traffic_source": traffic_src, "bytes_per_launch": mix_bytes,
+                         "avg_launch_ms": mix_avg_ms,
+                         "tuning": pkg.engine.mix_tuning(),
+                         "note": "achieved = algorithmic bytes (2 x active rows x P x 4 [+ slab rows]) / "
+                                 "mean per-launch duration, HIP events on the launch stream"},
+            "matcha_schedule": matcha,
         }
         if world > 1:
             lb = float(np.mean(link_bytes))
             out["xgmi"] = {"max_link_bytes_per_round": lb, "achieved": lb / (avg_ms * 1e-3) / 1e9,
                            "peak": XGMI_LINK_PEAK / 1e9, "unit": "GB/s",
-                           "frac": lb / (avg_ms * 1e-3) / XGMI_LINK_PEAK}
+                           "frac": lb / (avg_ms * 1e-3) / XGMI_LINK_PEAK,
+                           "round_ms_events": avg_ms,
+                           "note": "busiest GPU-pair direction: bytes per round / mean round time "
+                                   "(exchange + mix, HIP events, rank 0)"}
         if world == 1 and args.cpu_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(pkg, partner, GP.neighbor_weight, n, P, args.cpu_seconds)
         else:
