@@ -282,3 +282,49 @@ def test_mix_every_tuning_variant(pkg, O, bpc, u, nt, pf, rg, ch):
             assert np.array_equal(got.view(np.uint32), X.view(np.uint32)), f"graph {gid} lens {lens}"
     finally:
         pkg.engine.set_mix_tuning(**saved)
+
+
+@pytest.mark.parametrize("n,p,seed,P", [(32, 0.2, 7, 70_001), (64, 0.1, 1234, 50_003), (24, 0.3, 3, 9_999)])
+def test_mix_er_graphs_wide_configs(pkg, O, n, p, seed, P):
+    """Random ER topologies decomposed by the host path: 24 / 32 / 64 slots exercise the
+    (VEC 4, NS 16 / 32 / 64) LDS kernels; MATCHA-like random flags, 4 rounds, bit-exact."""
+    import random as pyrandom
+    pyrandom.seed(0)
+    gp = pkg.GraphProcessor(pkg.erdos_renyi(n, p, seed), 1.0, 0, n, 4, False)
+    M = len(gp.neighbors_info)
+    assert M <= 32
+    rng = np.random.RandomState(seed)
+    flags = (rng.uniform(size=(4, M)) < 0.5).astype(np.uint8)
+    flags[0] = 1
+    topo = Topo(gp.neighbors_info, 0.05, flags)
+    grp = pkg.VirtualWorkerGroup(topo, numel=P)
+    X = np.stack([O.synth(11 * seed + i, P) for i in range(n)])
+    grp.rows.copy_(torch.from_numpy(X))
+    for f in flags:
+        grp.communicate()
+        X = O.decen_round(X, topo.neighbors_info, f, 0.05)
+    got = grp.rows.cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), X.view(np.uint32))
+
+
+@pytest.mark.parametrize("P,ratio", [(14_774_436 // 16, 0.99), (545_930, 0.9)])
+def test_choco_vs_oracle_larger(pkg, O, P, ratio):
+    """Choco on 8 workers at VGG-16 / ResNet-50(10) scale slices, 3 rounds, bit-exact vs oracle."""
+    n = 8
+    gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, n, 4, True)
+    flags = np.array([[1, 1, 1, 1, 1], [1, 0, 1, 0, 1], [0, 1, 1, 1, 0]], np.uint8)
+    topo = Topo(gp.neighbors_info, 2 / 7, flags)
+    grp = pkg.ChocoWorkerGroup(topo, numel=P, ratio=ratio, consensus_lr=0.1)
+    X = np.stack([O.synth(500 + i, P) for i in range(n)])
+    XH, S = np.zeros_like(X), np.zeros_like(X)
+    grp.rows.copy_(torch.from_numpy(X))
+    k = O.topk_k(P, ratio)
+    for t, f in enumerate(flags):
+        if t:
+            D = np.stack([np.float32(0.01) * O.synth(9000 + 31 * t + i, P) for i in range(n)])
+            X += D
+            grp.rows.add_(torch.from_numpy(D).cuda())
+        grp.communicate()
+        O.choco_round(X, XH, S, topo.neighbors_info, f, 2 / 7, k, 0.1)
+        got = grp.rows.cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), X.view(np.uint32)), f"round {t}"
