@@ -174,6 +174,8 @@ class GossipEngine:
         self.n_local = self.n if n_local is None else int(n_local)
         self.comm = comm
         self.rank = comm.rank if comm is not None else 0
+        if comm is not None and owner is not None and int(owner[self.row_base]) != self.rank:
+            raise ValueError("worker block does not belong to this rank")
         self.owner = (np.zeros(self.n, np.int32) if owner is None
                       else np.ascontiguousarray(owner, dtype=np.int32))
         self.max_remote = max_incoming_remote(self.partner, self.row_base, self.n_local)
@@ -194,10 +196,29 @@ class GossipEngine:
         self.any_active = self.flags_host.any(axis=1)
 
     # ------------------------------------------------------------------ per round
+    def exchange_plan(self, it):
+        """The ordered point-to-point operations of round `it` for this block (native
+        mx_exchange_plan): int32 [n_ops][4] = (0 send / 1 recv, peer, local row / slab slot,
+        worker whose row travels)."""
+        fr = np.ascontiguousarray(self.flags_host[it])
+        cnt = ctypes.c_int(0)
+        check(lib.mx_exchange_plan(fr.ctypes.data, self.M, self.partner.ctypes.data, self.n,
+                                   self.owner.ctypes.data, self.rank, self.row_base, self.n_local,
+                                   None, 0, ctypes.byref(cnt)), "mx_exchange_plan")
+        ops = np.zeros((max(1, cnt.value), 4), np.int32)
+        check(lib.mx_exchange_plan(fr.ctypes.data, self.M, self.partner.ctypes.data, self.n,
+                                   self.owner.ctypes.data, self.rank, self.row_base, self.n_local,
+                                   ops.ctypes.data, cnt.value, ctypes.byref(cnt)), "mx_exchange_plan")
+        return ops[:cnt.value]
+
     def exchange(self, it, row_ptrs, slab_ptr, slab_ld_bytes, row_bytes, stream=None):
-        """RCCL sends/receives of iteration `it` (no-op with one process)."""
+        """Sends/receives of iteration `it` (no-op with one process).  The transport is the RCCL
+        communicator (mx_exchange_round); an object with an ``exchange_round`` method may stand
+        in for it (tests use an in-process loopback to drive N ranks on one GPU)."""
         if self.comm is None:
             return 0
+        if hasattr(self.comm, "exchange_round"):
+            return self.comm.exchange_round(self, it, row_ptrs, slab_ptr, slab_ld_bytes, row_bytes)
         row_arr = (ctypes.c_void_p * self.n_local)(*row_ptrs)
         nrem = ctypes.c_int(0)
         fr = np.ascontiguousarray(self.flags_host[it])

@@ -328,3 +328,42 @@ def test_choco_vs_oracle_larger(pkg, O, P, ratio):
         O.choco_round(X, XH, S, topo.neighbors_info, f, 2 / 7, k, 0.1)
         got = grp.rows.cpu().numpy()
         assert np.array_equal(got.view(np.uint32), X.view(np.uint32)), f"round {t}"
+
+
+@pytest.mark.parametrize("gid,nranks", [(0, 2), (0, 4), (0, 8), (2, 4), (3, 3)])
+def test_multirank_pipeline_loopback(pkg, O, gid, nranks):
+    """N ranks' engines on one GPU with the loopback transport: owner tables, receive-slab slot
+    numbering, native exchange order and the mixing kernel over local + slab rows, end to end,
+    bit-exact vs the single-process oracle (the RCCL call itself is the only piece not run)."""
+    from conftest import LoopbackHub
+    n = pkg.GRAPH_SIZES[gid]
+    P = 20_011
+    gp = pkg.GraphProcessor(pkg.select_graph(gid), 1.0, 0, n, 4, True)
+    M = len(gp.neighbors_info)
+    rng = np.random.RandomState(gid + nranks)
+    flags = (rng.uniform(size=(6, M)) < 0.6).astype(np.uint8)
+    flags[0] = 1
+    flags[3] = 0
+    topo = Topo(gp.neighbors_info, 0.17, flags)
+    hub = LoopbackHub(nranks)
+    groups = [pkg.VirtualWorkerGroup(topo, numel=P, rank=r, nranks=nranks, comm=hub.comm(r))
+              for r in range(nranks)]
+    X = np.stack([O.synth(700 + i, P) for i in range(n)])
+    for g in groups:
+        g.rows.copy_(torch.from_numpy(X[g.row_base:g.row_base + g.n_local]))
+    for it, f in enumerate(flags):
+        if not f.any():
+            continue
+        for g in groups:                       # phase 1: every rank's receives (pre-round rows)
+            hub.rows[g.engine.rank] = list(g._row_ptrs)
+            hub.row_base[g.engine.rank] = g.row_base
+        for g in groups:
+            g.engine.exchange(it, g._row_ptrs, g.slab.data_ptr() if g.slab is not None else None,
+                              g.ld * 4, g.numel * 4)
+        torch.cuda.synchronize()
+        for g in groups:                       # phase 2: every rank's mix
+            g.engine.mix(it, g.layout)
+        torch.cuda.synchronize()
+        X = O.decen_round(X, topo.neighbors_info, f, 0.17)
+    got = np.concatenate([g.rows.cpu().numpy() for g in groups])
+    assert np.array_equal(got.view(np.uint32), X.view(np.uint32))
