@@ -4,245 +4,319 @@
 //                     send = x - x_hat (ChocoCommunicator.prepare_comm_buffer, communicator.py:188-190)
 // mx_choco_apply    = ChocoCommunicator.averaging (communicator.py:200-230)
 //
-// Top-k is a 3-digit MSB radix select on the 31-bit magnitude key bits(|x - x_hat|) (non-negative
-// floats order like their bit patterns): digits of 11/11/10 bits, one streaming histogram pass
-// per digit (LDS histograms, non-zero bins flushed with global atomics), a one-block select
-// kernel that walks the histogram from the top to find the digit holding the k-th largest key,
-// then a two-pass stable compaction (per-chunk counts -> one-block scan -> per-chunk write) that
-// emits every key above the threshold plus the lowest-index keys equal to it, in index order.
-// Everything stays on the device; no host round trip between passes.
+// Top-k (k largest |x - x_hat|, ties at the threshold resolved towards the lowest indices,
+// output in index order) in THREE streaming passes over x / x_hat:
+//   A  hist_kernel     12-bit histogram of the magnitude key's top digit (bits 19..30: the
+//                      exponent + 4 mantissa bits) in LDS, non-zero bins flushed with atomics;
+//      select_top      one block finds the digit b0 holding the k-th largest key;
+//   B  split_kernel    per 4096-element chunk: count keys whose digit is above b0 (certainly
+//                      selected) and append the keys in digit b0 (candidates) to a side buffer
+//                      with wave-ballot compaction;
+//      cand_hist/select_cand (x2, 10 + 9 bits) finish the radix select on the candidates only,
+//      giving the exact threshold key T and how many of its ties are needed;
+//      cand_mark       per-chunk counts of candidates > T and == T (order-free atomics);
+//      scan_kernel     one block: per-chunk output offsets and tie ranks;
+//   C  write_kernel    per chunk, wave-ballot stable compaction of every key > T plus the
+//                      lowest-index ties, values = x - x_hat, indices int64.
+// Everything stays on the device; no host round trip.
 #include "mx_common.h"
 
 namespace {
 constexpr int kTPB = 256;
-constexpr int kBins = 2048;
-constexpr int kChunk = 4096;                 // elements per compaction chunk (16 per lane)
-constexpr int kPerLane = kChunk / kTPB;
+constexpr int kWaves = kTPB / 64;
+constexpr int kChunk = 4096;                 // elements per chunk (16 per lane)
+constexpr int kSub = kChunk / kTPB;
+constexpr int kTopBits = 12, kTopShift = 19;
+constexpr int kTopBins = 1 << kTopBits;
+constexpr int kMidBits = 10, kMidShift = 9;  // bits 9..18
+constexpr int kLowBits = 9;                  // bits 0..8
+constexpr int kScanTPB = 1024;
 
 struct SelState {
-    uint32_t prefix;    // key bits fixed so far
-    uint32_t mask;      // which bits of the key are fixed
-    int64_t k_rem;      // elements still to take at/below the current prefix
-    int64_t n_gt;       // elements strictly above the current prefix's bucket range
+    uint32_t b0;          // top digit of the threshold bin
+    uint32_t T;           // exact threshold key (after the candidate passes)
+    uint32_t prefix;      // candidate-pass prefix (bits fixed so far, shifted to full key)
+    uint32_t mask;
+    int64_t need;         // keys still to take at/below the current bin / prefix
+    int64_t cand_n;       // candidates appended in pass B
 };
 
-__device__ __forceinline__ uint32_t key_at(const float* x, const float* xh, int64_t i) {
-    const float d = xh ? __fsub_rn(x[i], xh[i]) : x[i];
-    return __float_as_uint(d) & 0x7fffffffu;
+__device__ __forceinline__ uint32_t key_of(float d) { return __float_as_uint(d) & 0x7fffffffu; }
+
+__device__ __forceinline__ float diff_at(const float* x, const float* xh, int64_t i) {
+    return xh ? __fsub_rn(x[i], xh[i]) : x[i];
 }
 
-// digit geometry: pass 0 -> bits [21,32), pass 1 -> [10,21), pass 2 -> [0,10)
-__device__ __forceinline__ int dshift(int pass) { return pass == 0 ? 21 : (pass == 1 ? 10 : 0); }
+__device__ __forceinline__ uint32_t lane_prefix(uint64_t m) {     // set bits below this lane
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 
-__global__ __launch_bounds__(kTPB) void hist_kernel(const float* __restrict__ x,
-                                                    const float* __restrict__ xh, int64_t P,
-                                                    const SelState* __restrict__ st, int pass,
-                                                    uint32_t* __restrict__ ghist) {
-    __shared__ uint32_t h[kBins];
-    for (int i = threadIdx.x; i < kBins; i += kTPB) h[i] = 0;
+// ---- A: top-digit histogram
+__global__ __launch_bounds__(kTPB) void hist_kernel(const float* __restrict__ x, const float* __restrict__ xh,
+                                                    int64_t P, uint32_t* __restrict__ ghist) {
+    __shared__ uint32_t h[kTopBins];
+    for (int i = threadIdx.x; i < kTopBins; i += kTPB) h[i] = 0;
     __syncthreads();
-    const uint32_t prefix = st->prefix, mask = st->mask;
-    const int sh = dshift(pass);
-    for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < P; i += (int64_t)gridDim.x * kTPB) {
-        const uint32_t key = key_at(x, xh, i);
-        if ((key & mask) == prefix) atomicAdd(&h[(key >> sh) & (kBins - 1)], 1u);
-    }
+    for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < P; i += (int64_t)gridDim.x * kTPB)
+        atomicAdd(&h[key_of(diff_at(x, xh, i)) >> kTopShift], 1u);
     __syncthreads();
-    for (int i = threadIdx.x; i < kBins; i += kTPB)
+    for (int i = threadIdx.x; i < kTopBins; i += kTPB)
         if (h[i]) atomicAdd(&ghist[i], h[i]);
 }
 
-// one block: find the digit value holding the k_rem-th largest key among the candidates
-__global__ __launch_bounds__(kTPB) void select_kernel(uint32_t* __restrict__ ghist,
-                                                      SelState* __restrict__ st, int pass) {
-    constexpr int kPer = kBins / kTPB;         // 8 bins per lane, lane 0 holds the TOP bins
+// one block: the bin holding the need-th largest count, scanning bins from the top.
+// bins/bin_shift describe the histogram; on exit st->need is the rank inside the chosen bin.
+template <int NBINS>
+__device__ void select_bin(uint32_t* __restrict__ hist, int64_t need, int* bin_out, int64_t* need_out) {
+    constexpr int kPer = NBINS / kTPB;
     __shared__ int64_t part[kTPB];
     const int t = threadIdx.x;
     int64_t mine = 0;
-    for (int j = 0; j < kPer; ++j) mine += ghist[kBins - 1 - (t * kPer + j)];
+    for (int j = 0; j < kPer; ++j) mine += hist[NBINS - 1 - (t * kPer + j)];
     part[t] = mine;
     __syncthreads();
-    // inclusive scan over lanes (counts from the top)
-    for (int off = 1; off < kTPB; off <<= 1) {
-        int64_t v = (t >= off) ? part[t - off] : 0;
+    for (int off = 1; off < kTPB; off <<= 1) {          // inclusive scan from the top bins down
+        const int64_t v = t >= off ? part[t - off] : 0;
         __syncthreads();
         part[t] += v;
         __syncthreads();
     }
-    const int64_t k_rem = st->k_rem;
-    const int64_t before = part[t] - mine;     // candidates in higher bins than this lane's
-    __syncthreads();
-    if (before < k_rem && part[t] >= k_rem) {
+    const int64_t before = part[t] - mine;
+    if (before < need && part[t] >= need) {
         int64_t acc = before;
         for (int j = 0; j < kPer; ++j) {
-            const int bin = kBins - 1 - (t * kPer + j);
-            const int64_t c = ghist[bin];
-            if (acc + c >= k_rem) {
-                const int sh = dshift(pass);
-                const uint32_t width_mask = (pass == 2) ? 0x3ffu : 0x7ffu;
-                st->prefix |= ((uint32_t)bin & width_mask) << sh;
-                st->mask |= width_mask << sh;
-                st->n_gt += acc;
-                st->k_rem = k_rem - acc;
+            const int bin = NBINS - 1 - (t * kPer + j);
+            const int64_t c = hist[bin];
+            if (acc + c >= need) {
+                *bin_out = bin;
+                *need_out = need - acc;
                 break;
             }
             acc += c;
         }
     }
     __syncthreads();
-    for (int i = t; i < kBins; i += kTPB) ghist[i] = 0;   // ready for the next pass
+    for (int i = t; i < NBINS; i += kTPB) hist[i] = 0;     // ready for the next use
 }
 
-// per-chunk counts of keys > threshold and == threshold
-__global__ __launch_bounds__(kTPB) void count_kernel(const float* __restrict__ x,
-                                                     const float* __restrict__ xh, int64_t P,
-                                                     const SelState* __restrict__ st,
-                                                     int64_t* __restrict__ cnt) {
-    __shared__ int64_t red[2][kTPB];
-    const uint32_t T = st->prefix;
-    const int64_t base = (int64_t)blockIdx.x * kChunk;
-    int64_t gt = 0, eq = 0;
-    for (int j = 0; j < kPerLane; ++j) {
-        const int64_t i = base + (int64_t)j * kTPB + threadIdx.x;
-        if (i < P) {
-            const uint32_t key = key_at(x, xh, i);
-            gt += key > T;
-            eq += key == T;
-        }
+__global__ __launch_bounds__(kTPB) void select_top(uint32_t* __restrict__ hist, SelState* __restrict__ st,
+                                                   int64_t k) {
+    __shared__ int bin;
+    __shared__ int64_t need;
+    select_bin<kTopBins>(hist, k, &bin, &need);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        st->b0 = (uint32_t)bin;
+        st->prefix = (uint32_t)bin << kTopShift;
+        st->mask = 0xffffffffu << kTopShift;
+        st->need = need;
+        st->cand_n = 0;
+        st->T = 0;
     }
-    red[0][threadIdx.x] = gt;
-    red[1][threadIdx.x] = eq;
+}
+
+// ---- B: per-chunk "certainly selected" counts + candidate compaction
+__global__ __launch_bounds__(kTPB) void split_kernel(const float* __restrict__ x, const float* __restrict__ xh,
+                                                     int64_t P, SelState* __restrict__ st,
+                                                     int64_t* __restrict__ cnt, int64_t* __restrict__ cand_idx,
+                                                     uint32_t* __restrict__ cand_key) {
+    __shared__ uint32_t wc[kWaves];
+    __shared__ unsigned long long base_s;
+    const uint32_t b0 = st->b0;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t chunk0 = (int64_t)blockIdx.x * kChunk;
+    uint32_t above = 0;
+    for (int j = 0; j < kSub; ++j) {
+        const int64_t i = chunk0 + (int64_t)j * kTPB + threadIdx.x;
+        uint32_t key = 0;
+        bool in = i < P;
+        if (in) key = key_of(diff_at(x, xh, i));
+        const uint32_t d = key >> kTopShift;
+        above += (in && d > b0);
+        const bool cand = in && d == b0;
+        const uint64_t m = __ballot(cand);
+        if (lane == 0) wc[wave] = (uint32_t)__popcll(m);
+        __syncthreads();
+        uint32_t wpre = 0, tot = 0;
+        for (int w = 0; w < kWaves; ++w) {
+            wpre += (w < wave) ? wc[w] : 0;
+            tot += wc[w];
+        }
+        if (threadIdx.x == 0 && tot) base_s = atomicAdd((unsigned long long*)&st->cand_n, (unsigned long long)tot);
+        __syncthreads();
+        if (cand) {
+            const int64_t pos = (int64_t)base_s + wpre + lane_prefix(m);
+            cand_idx[pos] = i;
+            cand_key[pos] = key;
+        }
+        __syncthreads();
+    }
+    // block sum of `above`
+    __shared__ uint32_t red[kTPB];
+    red[threadIdx.x] = above;
     __syncthreads();
     for (int off = kTPB / 2; off > 0; off >>= 1) {
-        if (threadIdx.x < off) {
-            red[0][threadIdx.x] += red[0][threadIdx.x + off];
-            red[1][threadIdx.x] += red[1][threadIdx.x + off];
-        }
+        if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
         __syncthreads();
     }
     if (threadIdx.x == 0) {
-        cnt[2 * blockIdx.x] = red[0][0];
-        cnt[2 * blockIdx.x + 1] = red[1][0];
+        cnt[3 * blockIdx.x + 0] = red[0];
+        cnt[3 * blockIdx.x + 1] = 0;
+        cnt[3 * blockIdx.x + 2] = 0;
     }
 }
 
-// one block: exclusive scan of chunk counts -> (output offset, equal-rank offset) per chunk
-__global__ __launch_bounds__(kTPB) void scan_kernel(const int64_t* __restrict__ cnt, int64_t nchunks,
-                                                    const SelState* __restrict__ st,
-                                                    int64_t* __restrict__ off) {
-    __shared__ int64_t s_gt[kTPB], s_eq[kTPB];
-    __shared__ int64_t carry_gt, carry_eq;
-    const int64_t need_eq = st->k_rem;
-    if (threadIdx.x == 0) { carry_gt = 0; carry_eq = 0; }
+// candidate histogram of `bits` bits at `shift`, restricted to keys matching st->prefix/mask
+template <int BITS>
+__global__ __launch_bounds__(kTPB) void cand_hist(const uint32_t* __restrict__ cand_key,
+                                                  const SelState* __restrict__ st, int shift,
+                                                  uint32_t* __restrict__ ghist) {
+    constexpr int NB = 1 << BITS;
+    __shared__ uint32_t h[NB];
+    for (int i = threadIdx.x; i < NB; i += kTPB) h[i] = 0;
     __syncthreads();
-    for (int64_t b0 = 0; b0 < nchunks; b0 += kTPB) {
+    const int64_t n = st->cand_n;
+    const uint32_t prefix = st->prefix, mask = st->mask;
+    for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kTPB) {
+        const uint32_t key = cand_key[i];
+        if ((key & mask) == prefix) atomicAdd(&h[(key >> shift) & (NB - 1)], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < NB; i += kTPB)
+        if (h[i]) atomicAdd(&ghist[i], h[i]);
+}
+
+template <int BITS>
+__global__ __launch_bounds__(kTPB) void select_cand(uint32_t* __restrict__ hist, SelState* __restrict__ st,
+                                                    int shift) {
+    constexpr int NB = 1 << BITS;
+    __shared__ int bin;
+    __shared__ int64_t need;
+    select_bin<NB>(hist, st->need, &bin, &need);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        st->prefix |= (uint32_t)bin << shift;
+        st->mask |= (uint32_t)(NB - 1) << shift;
+        st->need = need;
+        if (shift == 0) st->T = st->prefix;
+    }
+}
+
+// per-chunk counts of candidates strictly above T and equal to T
+__global__ __launch_bounds__(kTPB) void cand_mark(const int64_t* __restrict__ cand_idx,
+                                                  const uint32_t* __restrict__ cand_key,
+                                                  const SelState* __restrict__ st,
+                                                  int64_t* __restrict__ cnt) {
+    const int64_t n = st->cand_n;
+    const uint32_t T = st->T;
+    for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kTPB) {
+        const uint32_t key = cand_key[i];
+        const int64_t c = cand_idx[i] / kChunk;
+        if (key > T) atomicAdd((unsigned long long*)&cnt[3 * c + 1], 1ull);
+        else if (key == T) atomicAdd((unsigned long long*)&cnt[3 * c + 2], 1ull);
+    }
+}
+
+// one block: per chunk the output offset and the global tie rank of its first tie
+__global__ __launch_bounds__(kScanTPB) void scan_kernel(const int64_t* __restrict__ cnt, int64_t nchunks,
+                                                        const SelState* __restrict__ st,
+                                                        int64_t* __restrict__ off) {
+    __shared__ int64_t wsum_g[kScanTPB / 64], wsum_e[kScanTPB / 64];
+    __shared__ int64_t carry_g, carry_e;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t need_eq = st->need;
+    if (threadIdx.x == 0) carry_g = carry_e = 0;
+    __syncthreads();
+    for (int64_t b0 = 0; b0 < nchunks; b0 += kScanTPB) {
         const int64_t b = b0 + threadIdx.x;
-        const int64_t g = b < nchunks ? cnt[2 * b] : 0;
-        const int64_t e = b < nchunks ? cnt[2 * b + 1] : 0;
-        s_gt[threadIdx.x] = g;
-        s_eq[threadIdx.x] = e;
-        __syncthreads();
-        for (int o = 1; o < kTPB; o <<= 1) {
-            int64_t vg = threadIdx.x >= o ? s_gt[threadIdx.x - o] : 0;
-            int64_t ve = threadIdx.x >= o ? s_eq[threadIdx.x - o] : 0;
-            __syncthreads();
-            s_gt[threadIdx.x] += vg;
-            s_eq[threadIdx.x] += ve;
-            __syncthreads();
+        const int64_t g = b < nchunks ? cnt[3 * b] + cnt[3 * b + 1] : 0;   // keys > T
+        const int64_t e = b < nchunks ? cnt[3 * b + 2] : 0;                // keys == T
+        int64_t sg = g, se = e;                                            // wave inclusive scan
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t tg = __shfl_up(sg, o, 64), te = __shfl_up(se, o, 64);
+            if (lane >= o) { sg += tg; se += te; }
         }
+        if (lane == 63) { wsum_g[wave] = sg; wsum_e[wave] = se; }
+        __syncthreads();
+        int64_t pg = carry_g, pe = carry_e;
+        for (int w = 0; w < wave; ++w) { pg += wsum_g[w]; pe += wsum_e[w]; }
         if (b < nchunks) {
-            const int64_t eq_before = carry_eq + s_eq[threadIdx.x] - e;
-            const int64_t gt_before = carry_gt + s_gt[threadIdx.x] - g;
-            int64_t eq_taken_before = eq_before < need_eq ? eq_before : need_eq;
-            off[2 * b] = gt_before + eq_taken_before;   // output offset of this chunk
-            off[2 * b + 1] = eq_before;                 // global equal-rank of its first tie
+            const int64_t gt_before = pg + sg - g, eq_before = pe + se - e;
+            off[2 * b] = gt_before + (eq_before < need_eq ? eq_before : need_eq);
+            off[2 * b + 1] = eq_before;
         }
         __syncthreads();
-        if (threadIdx.x == kTPB - 1) {
-            carry_gt += s_gt[kTPB - 1];
-            carry_eq += s_eq[kTPB - 1];
+        if (threadIdx.x == 0) {
+            for (int w = 0; w < kScanTPB / 64; ++w) { carry_g += wsum_g[w]; carry_e += wsum_e[w]; }
         }
         __syncthreads();
     }
 }
 
-// per chunk: stable write of the selected (index, value) pairs in index order
-__global__ __launch_bounds__(kTPB) void write_kernel(const float* __restrict__ x,
-                                                     const float* __restrict__ xh, int64_t P,
-                                                     const SelState* __restrict__ st,
+// ---- C: stable per-chunk compaction in index order
+__global__ __launch_bounds__(kTPB) void write_kernel(const float* __restrict__ x, const float* __restrict__ xh,
+                                                     int64_t P, const SelState* __restrict__ st,
                                                      const int64_t* __restrict__ off,
                                                      float* __restrict__ vals, int64_t* __restrict__ idx) {
-    __shared__ int s_sel[kTPB], s_eq[kTPB];
-    __shared__ int64_t run_out, run_eq;
-    const uint32_t T = st->prefix;
-    const int64_t need_eq = st->k_rem;
-    const int64_t base = (int64_t)blockIdx.x * kChunk;
-    if (threadIdx.x == 0) {
-        run_out = off[2 * blockIdx.x];
-        run_eq = off[2 * blockIdx.x + 1];
-    }
-    __syncthreads();
-    for (int j = 0; j < kPerLane; ++j) {                  // sub-tiles in index order
-        const int64_t i = base + (int64_t)j * kTPB + threadIdx.x;
-        uint32_t key = 0;
+    __shared__ uint32_t weq[2][kWaves], wsel[2][kWaves];
+    const uint32_t T = st->T;
+    const int64_t need_eq = st->need;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t chunk0 = (int64_t)blockIdx.x * kChunk;
+    int64_t run_out = off[2 * blockIdx.x], run_eq = off[2 * blockIdx.x + 1];
+    for (int j = 0; j < kSub; ++j) {
+        const int par = j & 1;
+        const int64_t i = chunk0 + (int64_t)j * kTPB + threadIdx.x;
         float d = 0.0f;
-        bool in = i < P;
+        uint32_t key = 0;
+        const bool in = i < P;
         if (in) {
-            d = xh ? __fsub_rn(x[i], xh[i]) : x[i];
-            key = __float_as_uint(d) & 0x7fffffffu;
+            d = diff_at(x, xh, i);
+            key = key_of(d);
         }
-        const int is_eq = in && key == T;
-        s_eq[threadIdx.x] = is_eq;
+        const bool eq = in && key == T;
+        const uint64_t me = __ballot(eq);
+        if (lane == 0) weq[par][wave] = (uint32_t)__popcll(me);
         __syncthreads();
-        for (int o = 1; o < kTPB; o <<= 1) {              // inclusive scan of ties
-            int v = threadIdx.x >= o ? s_eq[threadIdx.x - o] : 0;
-            __syncthreads();
-            s_eq[threadIdx.x] += v;
-            __syncthreads();
+        uint32_t epre = 0, etot = 0;
+        for (int w = 0; w < kWaves; ++w) {
+            epre += (w < wave) ? weq[par][w] : 0;
+            etot += weq[par][w];
         }
-        const int64_t eq_rank = run_eq + s_eq[threadIdx.x] - is_eq;
-        const int sel = in && (key > T || (is_eq && eq_rank < need_eq));
-        s_sel[threadIdx.x] = sel;
+        const int64_t eq_rank = run_eq + epre + lane_prefix(me);
+        const bool sel = in && (key > T || (eq && eq_rank < need_eq));
+        const uint64_t ms = __ballot(sel);
+        if (lane == 0) wsel[par][wave] = (uint32_t)__popcll(ms);
         __syncthreads();
-        for (int o = 1; o < kTPB; o <<= 1) {
-            int v = threadIdx.x >= o ? s_sel[threadIdx.x - o] : 0;
-            __syncthreads();
-            s_sel[threadIdx.x] += v;
-            __syncthreads();
+        uint32_t spre = 0, stot = 0;
+        for (int w = 0; w < kWaves; ++w) {
+            spre += (w < wave) ? wsel[par][w] : 0;
+            stot += wsel[par][w];
         }
         if (sel) {
-            const int64_t pos = run_out + s_sel[threadIdx.x] - 1;
+            const int64_t pos = run_out + spre + lane_prefix(ms);
             vals[pos] = d;
             idx[pos] = i;
         }
-        __syncthreads();
-        if (threadIdx.x == kTPB - 1) {
-            run_out += s_sel[kTPB - 1];
-            run_eq += s_eq[kTPB - 1];
-        }
-        __syncthreads();
+        run_out += stot;
+        run_eq += etot;
     }
 }
 
-__global__ void init_state_kernel(SelState* st, int64_t k) {
-    st->prefix = 0;
-    st->mask = 0x80000000u;   // sign bit is always 0 in the key
-    st->k_rem = k;
-    st->n_gt = 0;
-}
-
 struct WorkLayout {
-    size_t hist, state, cnt, off, total;
+    size_t hist, state, cnt, off, cidx, ckey, total;
 };
 
 WorkLayout layout(int64_t P) {
     const int64_t nchunks = (P + kChunk - 1) / kChunk;
     WorkLayout w;
     w.hist = 0;
-    w.state = w.hist + sizeof(uint32_t) * kBins;
+    w.state = w.hist + sizeof(uint32_t) * kTopBins;
     w.cnt = w.state + 64;
-    w.off = w.cnt + sizeof(int64_t) * 2 * (size_t)nchunks;
-    w.total = w.off + sizeof(int64_t) * 2 * (size_t)nchunks;
+    w.off = w.cnt + sizeof(int64_t) * 3 * (size_t)nchunks;
+    w.cidx = (w.off + sizeof(int64_t) * 2 * (size_t)nchunks + 255) / 256 * 256;
+    w.ckey = w.cidx + sizeof(int64_t) * (size_t)P;
+    w.total = w.ckey + sizeof(uint32_t) * (size_t)P;
     return w;
 }
 
@@ -332,22 +406,32 @@ extern "C" int mx_topk_abs_diff(const float* x, const float* x_hat, int64_t P, i
     SelState* sst = reinterpret_cast<SelState*>(base + w.state);
     int64_t* cnt = reinterpret_cast<int64_t*>(base + w.cnt);
     int64_t* off = reinterpret_cast<int64_t*>(base + w.off);
+    int64_t* cidx = reinterpret_cast<int64_t*>(base + w.cidx);
+    uint32_t* ckey = reinterpret_cast<uint32_t*>(base + w.ckey);
     const int64_t nchunks = (P + kChunk - 1) / kChunk;
-    MX_HIP(hipMemsetAsync(hist, 0, sizeof(uint32_t) * kBins, st));
-    hipLaunchKernelGGL(init_state_kernel, dim3(1), dim3(1), 0, st, sst, k);
-    MX_LAUNCH_CHECK();
+    MX_HIP(hipMemsetAsync(hist, 0, sizeof(uint32_t) * kTopBins, st));
     const unsigned hgrid = clamp_grid(P, kTPB * 16, 2048);
-    for (int pass = 0; pass < 3; ++pass) {
-        hipLaunchKernelGGL(hist_kernel, dim3(hgrid), dim3(kTPB), 0, st, x, x_hat, P,
-                           (const SelState*)sst, pass, hist);
-        MX_LAUNCH_CHECK();
-        hipLaunchKernelGGL(select_kernel, dim3(1), dim3(kTPB), 0, st, hist, sst, pass);
-        MX_LAUNCH_CHECK();
-    }
-    hipLaunchKernelGGL(count_kernel, dim3((unsigned)nchunks), dim3(kTPB), 0, st, x, x_hat, P,
+    hipLaunchKernelGGL(hist_kernel, dim3(hgrid), dim3(kTPB), 0, st, x, x_hat, P, hist);
+    MX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(select_top, dim3(1), dim3(kTPB), 0, st, hist, sst, k);
+    MX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(split_kernel, dim3((unsigned)nchunks), dim3(kTPB), 0, st, x, x_hat, P, sst, cnt, cidx, ckey);
+    MX_LAUNCH_CHECK();
+    const unsigned cgrid = clamp_grid(P, kTPB * 64, 512);
+    hipLaunchKernelGGL(cand_hist<kMidBits>, dim3(cgrid), dim3(kTPB), 0, st, (const uint32_t*)ckey,
+                       (const SelState*)sst, kMidShift, hist);
+    MX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(select_cand<kMidBits>, dim3(1), dim3(kTPB), 0, st, hist, sst, kMidShift);
+    MX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(cand_hist<kLowBits>, dim3(cgrid), dim3(kTPB), 0, st, (const uint32_t*)ckey,
+                       (const SelState*)sst, 0, hist);
+    MX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(select_cand<kLowBits>, dim3(1), dim3(kTPB), 0, st, hist, sst, 0);
+    MX_LAUNCH_CHECK();
+    hipLaunchKernelGGL(cand_mark, dim3(cgrid), dim3(kTPB), 0, st, (const int64_t*)cidx, (const uint32_t*)ckey,
                        (const SelState*)sst, cnt);
     MX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(kTPB), 0, st, (const int64_t*)cnt, nchunks,
+    hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(kScanTPB), 0, st, (const int64_t*)cnt, nchunks,
                        (const SelState*)sst, off);
     MX_LAUNCH_CHECK();
     hipLaunchKernelGGL(write_kernel, dim3((unsigned)nchunks), dim3(kTPB), 0, st, x, x_hat, P,

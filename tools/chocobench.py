@@ -40,7 +40,7 @@ k = grp.k
 deg = np.zeros(n, int)
 for g in range(5):
     deg += np.asarray(gp.neighbors_info[g]) >= 0
-alg = n * (8 * P + 16 * P) + sum((d + 1) * k * (12 + 8) + k * 8 for d in deg)
+alg = int(n * (8 * P + 16 * P) + sum(int(d + 1) * k * (12 + 8) + k * 8 for d in deg))
 print(json.dumps({"P": P, "ratio": ratio, "k": k, "round_ms_median": float(np.median(ms)),
                   "round_ms_min": float(ms.min()), "rounds_per_s": 1e3 / float(np.median(ms)),
                   "alg_bytes_min": alg, "eff_TBps": alg / (np.median(ms) * 1e-3) / 1e12}))
