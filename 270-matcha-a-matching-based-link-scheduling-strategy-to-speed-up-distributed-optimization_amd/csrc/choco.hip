@@ -52,16 +52,22 @@ __device__ __forceinline__ uint32_t lane_prefix(uint64_t m) {     // set bits be
 }
 
 // ---- A: top-digit histogram
+// one LDS histogram per wave: the keys of real parameter vectors crowd a few exponent bins, so
+// private copies cut same-address atomic serialisation
 __global__ __launch_bounds__(kTPB) void hist_kernel(const float* __restrict__ x, const float* __restrict__ xh,
                                                     int64_t P, uint32_t* __restrict__ ghist) {
-    __shared__ uint32_t h[kTopBins];
-    for (int i = threadIdx.x; i < kTopBins; i += kTPB) h[i] = 0;
+    __shared__ uint32_t h[kWaves][kTopBins];
+    for (int i = threadIdx.x; i < kWaves * kTopBins; i += kTPB) (&h[0][0])[i] = 0;
     __syncthreads();
+    uint32_t* mine = h[threadIdx.x >> 6];
     for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < P; i += (int64_t)gridDim.x * kTPB)
-        atomicAdd(&h[key_of(diff_at(x, xh, i)) >> kTopShift], 1u);
+        atomicAdd(&mine[key_of(diff_at(x, xh, i)) >> kTopShift], 1u);
     __syncthreads();
-    for (int i = threadIdx.x; i < kTopBins; i += kTPB)
-        if (h[i]) atomicAdd(&ghist[i], h[i]);
+    for (int i = threadIdx.x; i < kTopBins; i += kTPB) {
+        uint32_t v = 0;
+        for (int w = 0; w < kWaves; ++w) v += h[w][i];
+        if (v) atomicAdd(&ghist[i], v);
+    }
 }
 
 // one block: the bin holding the need-th largest count, scanning bins from the top.
@@ -115,54 +121,61 @@ __global__ __launch_bounds__(kTPB) void select_top(uint32_t* __restrict__ hist, 
     }
 }
 
-// ---- B: per-chunk "certainly selected" counts + candidate compaction
+// ---- B: per-chunk "certainly selected" counts + candidate compaction.  The chunk's 16 keys per
+// lane stay in registers; one wave ballot per sub-tile gives every candidate its rank, and ONE
+// global atomic per block reserves the block's candidate range.
 __global__ __launch_bounds__(kTPB) void split_kernel(const float* __restrict__ x, const float* __restrict__ xh,
                                                      int64_t P, SelState* __restrict__ st,
                                                      int64_t* __restrict__ cnt, int64_t* __restrict__ cand_idx,
                                                      uint32_t* __restrict__ cand_key) {
-    __shared__ uint32_t wc[kWaves];
+    __shared__ uint32_t wc[kSub][kWaves];
+    __shared__ uint32_t wabove[kWaves];
     __shared__ unsigned long long base_s;
     const uint32_t b0 = st->b0;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t chunk0 = (int64_t)blockIdx.x * kChunk;
+    uint32_t keys[kSub];
+    uint64_t masks[kSub];
     uint32_t above = 0;
+#pragma unroll
     for (int j = 0; j < kSub; ++j) {
         const int64_t i = chunk0 + (int64_t)j * kTPB + threadIdx.x;
-        uint32_t key = 0;
-        bool in = i < P;
-        if (in) key = key_of(diff_at(x, xh, i));
-        const uint32_t d = key >> kTopShift;
+        const bool in = i < P;
+        keys[j] = in ? key_of(diff_at(x, xh, i)) : 0u;
+        const uint32_t d = keys[j] >> kTopShift;
         above += (in && d > b0);
-        const bool cand = in && d == b0;
-        const uint64_t m = __ballot(cand);
-        if (lane == 0) wc[wave] = (uint32_t)__popcll(m);
-        __syncthreads();
-        uint32_t wpre = 0, tot = 0;
-        for (int w = 0; w < kWaves; ++w) {
-            wpre += (w < wave) ? wc[w] : 0;
-            tot += wc[w];
-        }
-        if (threadIdx.x == 0 && tot) base_s = atomicAdd((unsigned long long*)&st->cand_n, (unsigned long long)tot);
-        __syncthreads();
-        if (cand) {
-            const int64_t pos = (int64_t)base_s + wpre + lane_prefix(m);
-            cand_idx[pos] = i;
-            cand_key[pos] = key;
-        }
-        __syncthreads();
+        masks[j] = __ballot(in && d == b0);
+        if (lane == 0) wc[j][wave] = (uint32_t)__popcll(masks[j]);
     }
-    // block sum of `above`
-    __shared__ uint32_t red[kTPB];
-    red[threadIdx.x] = above;
+    // wave total of `above` via a butterfly, then per-wave slots
+    for (int o = 32; o > 0; o >>= 1) above += __shfl_xor(above, o, 64);
+    if (lane == 0) wabove[wave] = above;
     __syncthreads();
-    for (int off = kTPB / 2; off > 0; off >>= 1) {
-        if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
-        __syncthreads();
-    }
     if (threadIdx.x == 0) {
-        cnt[3 * blockIdx.x + 0] = red[0];
+        uint64_t tot = 0, ab = 0;
+        for (int j = 0; j < kSub; ++j)
+            for (int w = 0; w < kWaves; ++w) tot += wc[j][w];
+        for (int w = 0; w < kWaves; ++w) ab += wabove[w];
+        base_s = tot ? atomicAdd((unsigned long long*)&st->cand_n, (unsigned long long)tot) : 0ull;
+        cnt[3 * blockIdx.x + 0] = (int64_t)ab;
         cnt[3 * blockIdx.x + 1] = 0;
         cnt[3 * blockIdx.x + 2] = 0;
+    }
+    __syncthreads();
+    uint64_t run = base_s;
+#pragma unroll
+    for (int j = 0; j < kSub; ++j) {
+        uint32_t wpre = 0, tot = 0;
+        for (int w = 0; w < kWaves; ++w) {
+            wpre += (w < wave) ? wc[j][w] : 0;
+            tot += wc[j][w];
+        }
+        if ((masks[j] >> lane) & 1ull) {
+            const int64_t pos = (int64_t)run + wpre + lane_prefix(masks[j]);
+            cand_idx[pos] = chunk0 + (int64_t)j * kTPB + threadIdx.x;
+            cand_key[pos] = keys[j];
+        }
+        run += tot;
     }
 }
 
@@ -369,15 +382,14 @@ __global__ __launch_bounds__(kTPB) void dense_kernel(float* __restrict__ x, cons
     const float* hr = xh + (int64_t)r * ld;
     const bool vec = (((uintptr_t)xr | (uintptr_t)sr | (uintptr_t)hr) & 15) == 0;
     const int64_t nv = vec ? P / 4 : 0;
+    typedef float f4 __attribute__((ext_vector_type(4)));
     for (int64_t q = (int64_t)blockIdx.x * kTPB + threadIdx.x; q < nv; q += (int64_t)gridDim.x * kTPB) {
-        float4 a = reinterpret_cast<float4*>(xr)[q];
-        const float4 b = reinterpret_cast<const float4*>(sr)[q];
-        const float4 c = reinterpret_cast<const float4*>(hr)[q];
-        a.x = __builtin_fmaf(-g, c.x, __builtin_fmaf(g, b.x, a.x));
-        a.y = __builtin_fmaf(-g, c.y, __builtin_fmaf(g, b.y, a.y));
-        a.z = __builtin_fmaf(-g, c.z, __builtin_fmaf(g, b.z, a.z));
-        a.w = __builtin_fmaf(-g, c.w, __builtin_fmaf(g, b.w, a.w));
-        reinterpret_cast<float4*>(xr)[q] = a;
+        f4 a = __builtin_nontemporal_load(reinterpret_cast<const f4*>(xr) + q);
+        const f4 b = __builtin_nontemporal_load(reinterpret_cast<const f4*>(sr) + q);
+        const f4 c = __builtin_nontemporal_load(reinterpret_cast<const f4*>(hr) + q);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] = __builtin_fmaf(-g, c[j], __builtin_fmaf(g, b[j], a[j]));
+        __builtin_nontemporal_store(a, reinterpret_cast<f4*>(xr) + q);
     }
     for (int64_t i = nv * 4 + (int64_t)blockIdx.x * kTPB + threadIdx.x; i < P; i += (int64_t)gridDim.x * kTPB)
         xr[i] = __builtin_fmaf(-g, hr[i], __builtin_fmaf(g, sr[i], xr[i]));
