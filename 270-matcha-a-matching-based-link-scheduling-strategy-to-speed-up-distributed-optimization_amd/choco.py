@@ -62,7 +62,8 @@ class ChocoWorkerGroup:
         self.msg_bytes = int(lib.mx_choco_msg_bytes(self.k))
         self.msg_ld = (self.msg_bytes + 255) // 256 * 256
         self.msgs = torch.empty(self.engine.n_slots * self.msg_ld, dtype=torch.uint8, device="cuda")
-        self.work = torch.empty(int(lib.mx_topk_work_bytes(P)), dtype=torch.uint8, device="cuda")
+        self.work_ld = int(lib.mx_topk_work_bytes(P))
+        self.work = torch.empty(self.n_local * self.work_ld, dtype=torch.uint8, device="cuda")
         self.gamma32 = float(np.float32(consensus_lr))
 
     @property
@@ -82,10 +83,9 @@ class ChocoWorkerGroup:
         P = self.numel
         st = stream_ptr(stream)
         mbase = self.msgs.data_ptr()
-        for r in range(self.n_local):
-            check(lib.mx_topk_abs_diff(self.x[r].data_ptr(), self.x_hat[r].data_ptr(), P, self.k,
-                                       mbase + r * self.msg_ld, mbase + r * self.msg_ld + 4 * self.kpad,
-                                       self.work.data_ptr(), st), "mx_topk_abs_diff")
+        check(lib.mx_topk_abs_diff_rows(self.x.data_ptr(), self.x_hat.data_ptr(), self.ld, self.n_local, P,
+                                        self.k, mbase, self.msg_ld, 4 * self.kpad, self.work.data_ptr(),
+                                        self.work_ld, st), "mx_topk_abs_diff_rows")
         if self.engine.comm is not None:
             self.engine.exchange(it, [mbase + r * self.msg_ld for r in range(self.n_local)],
                                  mbase + self.n_local * self.msg_ld, self.msg_ld, self.msg_bytes, stream)

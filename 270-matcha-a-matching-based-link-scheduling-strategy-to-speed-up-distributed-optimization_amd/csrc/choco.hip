@@ -18,7 +18,8 @@
 //      scan_kernel     one block: per-chunk output offsets and tie ranks;
 //   C  write_kernel    per chunk, wave-ballot stable compaction of every key > T plus the
 //                      lowest-index ties, values = x - x_hat, indices int64.
-// Everything stays on the device; no host round trip.
+// Everything stays on the device; no host round trip.  All local workers' rows are processed by
+// the same launches (blockIdx.y = row), so a round costs ~11 launches, not ~11 per worker.
 #include "mx_common.h"
 
 namespace {
@@ -41,6 +42,67 @@ struct SelState {
     int64_t cand_n;       // candidates appended in pass B
 };
 
+struct WorkLayout {
+    size_t hist, state, cnt, off, cidx, ckey, total;
+};
+
+__host__ __device__ inline WorkLayout layout(int64_t P) {
+    const int64_t nchunks = (P + kChunk - 1) / kChunk;
+    WorkLayout w;
+    w.hist = 0;
+    w.state = w.hist + sizeof(uint32_t) * kTopBins;
+    w.cnt = w.state + 64;
+    w.off = w.cnt + sizeof(int64_t) * 3 * (size_t)nchunks;
+    w.cidx = (w.off + sizeof(int64_t) * 2 * (size_t)nchunks + 255) / 256 * 256;
+    w.ckey = w.cidx + sizeof(int64_t) * (size_t)P;
+    w.total = (w.ckey + sizeof(uint32_t) * (size_t)P + 255) / 256 * 256;
+    return w;
+}
+
+// A batch of rows: input row r at x + r*ld (x_hat likewise, may be null); its output message at
+// out + r*out_ld (values) and + idx_off (int64 indices); its scratch at work + r*work_ld.
+struct Rows {
+    const float* x;
+    const float* xh;
+    int64_t ld;
+    char* out;
+    int64_t out_ld, idx_off;
+    char* work;
+    int64_t work_ld;
+    int64_t P, k;
+};
+
+struct RowView {
+    const float* x;
+    const float* xh;
+    uint32_t* hist;
+    SelState* st;
+    int64_t* cnt;
+    int64_t* off;
+    int64_t* cidx;
+    uint32_t* ckey;
+    float* vals;
+    int64_t* idx;
+};
+
+__device__ __forceinline__ RowView row_view(const Rows& R) {
+    const int r = blockIdx.y;
+    const WorkLayout w = layout(R.P);
+    char* wb = R.work + (int64_t)r * R.work_ld;
+    RowView v;
+    v.x = R.x + (int64_t)r * R.ld;
+    v.xh = R.xh ? R.xh + (int64_t)r * R.ld : nullptr;
+    v.hist = reinterpret_cast<uint32_t*>(wb + w.hist);
+    v.st = reinterpret_cast<SelState*>(wb + w.state);
+    v.cnt = reinterpret_cast<int64_t*>(wb + w.cnt);
+    v.off = reinterpret_cast<int64_t*>(wb + w.off);
+    v.cidx = reinterpret_cast<int64_t*>(wb + w.cidx);
+    v.ckey = reinterpret_cast<uint32_t*>(wb + w.ckey);
+    v.vals = reinterpret_cast<float*>(R.out + (int64_t)r * R.out_ld);
+    v.idx = reinterpret_cast<int64_t*>(R.out + (int64_t)r * R.out_ld + R.idx_off);
+    return v;
+}
+
 __device__ __forceinline__ uint32_t key_of(float d) { return __float_as_uint(d) & 0x7fffffffu; }
 
 __device__ __forceinline__ float diff_at(const float* x, const float* xh, int64_t i) {
@@ -52,22 +114,16 @@ __device__ __forceinline__ uint32_t lane_prefix(uint64_t m) {     // set bits be
 }
 
 // ---- A: top-digit histogram
-// one LDS histogram per wave: the keys of real parameter vectors crowd a few exponent bins, so
-// private copies cut same-address atomic serialisation
-__global__ __launch_bounds__(kTPB) void hist_kernel(const float* __restrict__ x, const float* __restrict__ xh,
-                                                    int64_t P, uint32_t* __restrict__ ghist) {
-    __shared__ uint32_t h[kWaves][kTopBins];
-    for (int i = threadIdx.x; i < kWaves * kTopBins; i += kTPB) (&h[0][0])[i] = 0;
+__global__ __launch_bounds__(kTPB) void hist_kernel(Rows R) {
+    const RowView v = row_view(R);
+    __shared__ uint32_t h[kTopBins];
+    for (int i = threadIdx.x; i < kTopBins; i += kTPB) h[i] = 0;
     __syncthreads();
-    uint32_t* mine = h[threadIdx.x >> 6];
-    for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < P; i += (int64_t)gridDim.x * kTPB)
-        atomicAdd(&mine[key_of(diff_at(x, xh, i)) >> kTopShift], 1u);
+    for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < R.P; i += (int64_t)gridDim.x * kTPB)
+        atomicAdd(&h[key_of(diff_at(v.x, v.xh, i)) >> kTopShift], 1u);
     __syncthreads();
-    for (int i = threadIdx.x; i < kTopBins; i += kTPB) {
-        uint32_t v = 0;
-        for (int w = 0; w < kWaves; ++w) v += h[w][i];
-        if (v) atomicAdd(&ghist[i], v);
-    }
+    for (int i = threadIdx.x; i < kTopBins; i += kTPB)
+        if (h[i]) atomicAdd(&v.hist[i], h[i]);
 }
 
 // one block: the bin holding the need-th largest count, scanning bins from the top.
@@ -105,11 +161,12 @@ __device__ void select_bin(uint32_t* __restrict__ hist, int64_t need, int* bin_o
     for (int i = t; i < NBINS; i += kTPB) hist[i] = 0;     // ready for the next use
 }
 
-__global__ __launch_bounds__(kTPB) void select_top(uint32_t* __restrict__ hist, SelState* __restrict__ st,
-                                                   int64_t k) {
+__global__ __launch_bounds__(kTPB) void select_top(Rows R) {
+    const RowView v = row_view(R);
+    SelState* st = v.st;
     __shared__ int bin;
     __shared__ int64_t need;
-    select_bin<kTopBins>(hist, k, &bin, &need);
+    select_bin<kTopBins>(v.hist, R.k, &bin, &need);
     __syncthreads();
     if (threadIdx.x == 0) {
         st->b0 = (uint32_t)bin;
@@ -124,10 +181,15 @@ __global__ __launch_bounds__(kTPB) void select_top(uint32_t* __restrict__ hist, 
 // ---- B: per-chunk "certainly selected" counts + candidate compaction.  The chunk's 16 keys per
 // lane stay in registers; one wave ballot per sub-tile gives every candidate its rank, and ONE
 // global atomic per block reserves the block's candidate range.
-__global__ __launch_bounds__(kTPB) void split_kernel(const float* __restrict__ x, const float* __restrict__ xh,
-                                                     int64_t P, SelState* __restrict__ st,
-                                                     int64_t* __restrict__ cnt, int64_t* __restrict__ cand_idx,
-                                                     uint32_t* __restrict__ cand_key) {
+__global__ __launch_bounds__(kTPB) void split_kernel(Rows R) {
+    const RowView v = row_view(R);
+    const float* x = v.x;
+    const float* xh = v.xh;
+    const int64_t P = R.P;
+    SelState* st = v.st;
+    int64_t* cnt = v.cnt;
+    int64_t* cand_idx = v.cidx;
+    uint32_t* cand_key = v.ckey;
     __shared__ uint32_t wc[kSub][kWaves];
     __shared__ uint32_t wabove[kWaves];
     __shared__ unsigned long long base_s;
@@ -181,9 +243,11 @@ __global__ __launch_bounds__(kTPB) void split_kernel(const float* __restrict__ x
 
 // candidate histogram of `bits` bits at `shift`, restricted to keys matching st->prefix/mask
 template <int BITS>
-__global__ __launch_bounds__(kTPB) void cand_hist(const uint32_t* __restrict__ cand_key,
-                                                  const SelState* __restrict__ st, int shift,
-                                                  uint32_t* __restrict__ ghist) {
+__global__ __launch_bounds__(kTPB) void cand_hist(Rows R, int shift) {
+    const RowView v = row_view(R);
+    const uint32_t* cand_key = v.ckey;
+    const SelState* st = v.st;
+    uint32_t* ghist = v.hist;
     constexpr int NB = 1 << BITS;
     __shared__ uint32_t h[NB];
     for (int i = threadIdx.x; i < NB; i += kTPB) h[i] = 0;
@@ -200,8 +264,10 @@ __global__ __launch_bounds__(kTPB) void cand_hist(const uint32_t* __restrict__ c
 }
 
 template <int BITS>
-__global__ __launch_bounds__(kTPB) void select_cand(uint32_t* __restrict__ hist, SelState* __restrict__ st,
-                                                    int shift) {
+__global__ __launch_bounds__(kTPB) void select_cand(Rows R, int shift) {
+    const RowView v = row_view(R);
+    uint32_t* hist = v.hist;
+    SelState* st = v.st;
     constexpr int NB = 1 << BITS;
     __shared__ int bin;
     __shared__ int64_t need;
@@ -216,10 +282,12 @@ __global__ __launch_bounds__(kTPB) void select_cand(uint32_t* __restrict__ hist,
 }
 
 // per-chunk counts of candidates strictly above T and equal to T
-__global__ __launch_bounds__(kTPB) void cand_mark(const int64_t* __restrict__ cand_idx,
-                                                  const uint32_t* __restrict__ cand_key,
-                                                  const SelState* __restrict__ st,
-                                                  int64_t* __restrict__ cnt) {
+__global__ __launch_bounds__(kTPB) void cand_mark(Rows R) {
+    const RowView v = row_view(R);
+    const int64_t* cand_idx = v.cidx;
+    const uint32_t* cand_key = v.ckey;
+    const SelState* st = v.st;
+    int64_t* cnt = v.cnt;
     const int64_t n = st->cand_n;
     const uint32_t T = st->T;
     for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kTPB) {
@@ -231,9 +299,12 @@ __global__ __launch_bounds__(kTPB) void cand_mark(const int64_t* __restrict__ ca
 }
 
 // one block: per chunk the output offset and the global tie rank of its first tie
-__global__ __launch_bounds__(kScanTPB) void scan_kernel(const int64_t* __restrict__ cnt, int64_t nchunks,
-                                                        const SelState* __restrict__ st,
-                                                        int64_t* __restrict__ off) {
+__global__ __launch_bounds__(kScanTPB) void scan_kernel(Rows R) {
+    const RowView v = row_view(R);
+    const int64_t* cnt = v.cnt;
+    const int64_t nchunks = (R.P + kChunk - 1) / kChunk;
+    const SelState* st = v.st;
+    int64_t* off = v.off;
     __shared__ int64_t wsum_g[kScanTPB / 64], wsum_e[kScanTPB / 64];
     __shared__ int64_t carry_g, carry_e;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -267,10 +338,15 @@ __global__ __launch_bounds__(kScanTPB) void scan_kernel(const int64_t* __restric
 }
 
 // ---- C: stable per-chunk compaction in index order
-__global__ __launch_bounds__(kTPB) void write_kernel(const float* __restrict__ x, const float* __restrict__ xh,
-                                                     int64_t P, const SelState* __restrict__ st,
-                                                     const int64_t* __restrict__ off,
-                                                     float* __restrict__ vals, int64_t* __restrict__ idx) {
+__global__ __launch_bounds__(kTPB) void write_kernel(Rows R) {
+    const RowView v = row_view(R);
+    const float* x = v.x;
+    const float* xh = v.xh;
+    const int64_t P = R.P;
+    const SelState* st = v.st;
+    const int64_t* off = v.off;
+    float* vals = v.vals;
+    int64_t* idx = v.idx;
     __shared__ uint32_t weq[2][kWaves], wsel[2][kWaves];
     const uint32_t T = st->T;
     const int64_t need_eq = st->need;
@@ -314,23 +390,6 @@ __global__ __launch_bounds__(kTPB) void write_kernel(const float* __restrict__ x
         run_out += stot;
         run_eq += etot;
     }
-}
-
-struct WorkLayout {
-    size_t hist, state, cnt, off, cidx, ckey, total;
-};
-
-WorkLayout layout(int64_t P) {
-    const int64_t nchunks = (P + kChunk - 1) / kChunk;
-    WorkLayout w;
-    w.hist = 0;
-    w.state = w.hist + sizeof(uint32_t) * kTopBins;
-    w.cnt = w.state + 64;
-    w.off = w.cnt + sizeof(int64_t) * 3 * (size_t)nchunks;
-    w.cidx = (w.off + sizeof(int64_t) * 2 * (size_t)nchunks + 255) / 256 * 256;
-    w.ckey = w.cidx + sizeof(int64_t) * (size_t)P;
-    w.total = w.ckey + sizeof(uint32_t) * (size_t)P;
-    return w;
 }
 
 // ------------------------------------------------------------------------------- apply
@@ -407,49 +466,54 @@ extern "C" size_t mx_topk_work_bytes(int64_t P) { return layout(P < 1 ? 1 : P).t
 
 extern "C" int64_t mx_choco_msg_bytes(int64_t k) { return 4 * ((k + 1) / 2 * 2) + 8 * k; }
 
-extern "C" int mx_topk_abs_diff(const float* x, const float* x_hat, int64_t P, int64_t k, float* vals,
-                                int64_t* idx, void* work, void* stream) {
-    MX_CHECK(x && vals && idx && work, "mx_topk_abs_diff: null pointer");
-    MX_CHECK(P >= 1 && k >= 1 && k <= P, "mx_topk_abs_diff: P=%lld k=%lld", (long long)P, (long long)k);
+extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t ld, int nrows, int64_t P,
+                                     int64_t k, void* out, int64_t out_ld_bytes, int64_t idx_off_bytes,
+                                     void* work, int64_t work_ld_bytes, void* stream) {
+    MX_CHECK(x && out && work, "mx_topk_abs_diff_rows: null pointer");
+    MX_CHECK(P >= 1 && k >= 1 && k <= P && nrows >= 1 && nrows <= 65535 && (nrows == 1 || ld >= P),
+             "mx_topk_abs_diff_rows: P=%lld k=%lld nrows=%d ld=%lld", (long long)P, (long long)k, nrows, (long long)ld);
+    MX_CHECK(((uintptr_t)(static_cast<char*>(out) + idx_off_bytes)) % 8 == 0 && (nrows == 1 || out_ld_bytes % 8 == 0),
+             "mx_topk_abs_diff_rows: int64 index output must be 8-byte aligned");
+    MX_CHECK(work_ld_bytes >= (int64_t)layout(P).total || nrows == 1, "mx_topk_abs_diff_rows: work_ld too small");
     hipStream_t st = mx::as_stream(stream);
+    Rows R{x, x_hat, ld, static_cast<char*>(out), out_ld_bytes, idx_off_bytes, static_cast<char*>(work),
+           work_ld_bytes, P, k};
     const WorkLayout w = layout(P);
-    char* base = static_cast<char*>(work);
-    uint32_t* hist = reinterpret_cast<uint32_t*>(base + w.hist);
-    SelState* sst = reinterpret_cast<SelState*>(base + w.state);
-    int64_t* cnt = reinterpret_cast<int64_t*>(base + w.cnt);
-    int64_t* off = reinterpret_cast<int64_t*>(base + w.off);
-    int64_t* cidx = reinterpret_cast<int64_t*>(base + w.cidx);
-    uint32_t* ckey = reinterpret_cast<uint32_t*>(base + w.ckey);
-    const int64_t nchunks = (P + kChunk - 1) / kChunk;
-    MX_HIP(hipMemsetAsync(hist, 0, sizeof(uint32_t) * kTopBins, st));
-    const unsigned hgrid = clamp_grid(P, kTPB * 16, 2048);
-    hipLaunchKernelGGL(hist_kernel, dim3(hgrid), dim3(kTPB), 0, st, x, x_hat, P, hist);
+    for (int r = 0; r < nrows; ++r)
+        MX_HIP(hipMemsetAsync(static_cast<char*>(work) + (int64_t)r * work_ld_bytes + w.hist, 0,
+                              sizeof(uint32_t) * kTopBins, st));
+    const unsigned nchunks = (unsigned)((P + kChunk - 1) / kChunk);
+    const unsigned hgrid = clamp_grid(P, (int64_t)kTPB * 64, (512 + nrows - 1) / nrows);
+    const unsigned cgrid = clamp_grid(P, (int64_t)kTPB * 64, (512 + nrows - 1) / nrows);
+    const dim3 one(1, nrows);
+    hipLaunchKernelGGL(hist_kernel, dim3(hgrid, nrows), dim3(kTPB), 0, st, R);
     MX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(select_top, dim3(1), dim3(kTPB), 0, st, hist, sst, k);
+    hipLaunchKernelGGL(select_top, one, dim3(kTPB), 0, st, R);
     MX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(split_kernel, dim3((unsigned)nchunks), dim3(kTPB), 0, st, x, x_hat, P, sst, cnt, cidx, ckey);
+    hipLaunchKernelGGL(split_kernel, dim3(nchunks, nrows), dim3(kTPB), 0, st, R);
     MX_LAUNCH_CHECK();
-    const unsigned cgrid = clamp_grid(P, kTPB * 64, 512);
-    hipLaunchKernelGGL(cand_hist<kMidBits>, dim3(cgrid), dim3(kTPB), 0, st, (const uint32_t*)ckey,
-                       (const SelState*)sst, kMidShift, hist);
+    hipLaunchKernelGGL(cand_hist<kMidBits>, dim3(cgrid, nrows), dim3(kTPB), 0, st, R, kMidShift);
     MX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(select_cand<kMidBits>, dim3(1), dim3(kTPB), 0, st, hist, sst, kMidShift);
+    hipLaunchKernelGGL(select_cand<kMidBits>, one, dim3(kTPB), 0, st, R, kMidShift);
     MX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(cand_hist<kLowBits>, dim3(cgrid), dim3(kTPB), 0, st, (const uint32_t*)ckey,
-                       (const SelState*)sst, 0, hist);
+    hipLaunchKernelGGL(cand_hist<kLowBits>, dim3(cgrid, nrows), dim3(kTPB), 0, st, R, 0);
     MX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(select_cand<kLowBits>, dim3(1), dim3(kTPB), 0, st, hist, sst, 0);
+    hipLaunchKernelGGL(select_cand<kLowBits>, one, dim3(kTPB), 0, st, R, 0);
     MX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(cand_mark, dim3(cgrid), dim3(kTPB), 0, st, (const int64_t*)cidx, (const uint32_t*)ckey,
-                       (const SelState*)sst, cnt);
+    hipLaunchKernelGGL(cand_mark, dim3(cgrid, nrows), dim3(kTPB), 0, st, R);
     MX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(kScanTPB), 0, st, (const int64_t*)cnt, nchunks,
-                       (const SelState*)sst, off);
+    hipLaunchKernelGGL(scan_kernel, one, dim3(kScanTPB), 0, st, R);
     MX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(write_kernel, dim3((unsigned)nchunks), dim3(kTPB), 0, st, x, x_hat, P,
-                       (const SelState*)sst, (const int64_t*)off, vals, idx);
+    hipLaunchKernelGGL(write_kernel, dim3(nchunks, nrows), dim3(kTPB), 0, st, R);
     MX_LAUNCH_CHECK();
     return MX_OK;
+}
+
+extern "C" int mx_topk_abs_diff(const float* x, const float* x_hat, int64_t P, int64_t k, float* vals,
+                                int64_t* idx, void* work, void* stream) {
+    MX_CHECK(vals && idx, "mx_topk_abs_diff: null pointer");
+    const int64_t idx_off = reinterpret_cast<char*>(idx) - reinterpret_cast<char*>(vals);
+    return mx_topk_abs_diff_rows(x, x_hat, P, 1, P, k, vals, 0, idx_off, work, 0, stream);
 }
 
 extern "C" int mx_choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t k,

@@ -130,6 +130,13 @@ int mx_scatter(float* const* ptrs_dev, const int64_t* off_dev, int nseg, int64_t
 size_t mx_topk_work_bytes(int64_t P);
 int mx_topk_abs_diff(const float* x, const float* x_hat, int64_t P, int64_t k, float* vals,
                      int64_t* idx, void* work, void* stream);
+/* Batched form (one set of launches for every local worker): row r reads x + r*ld (and
+ * x_hat + r*ld), writes its values at out + r*out_ld_bytes and its int64 indices at
+ * out + r*out_ld_bytes + idx_off_bytes, and uses work + r*work_ld_bytes
+ * (work_ld_bytes >= mx_topk_work_bytes(P)). */
+int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t ld, int nrows, int64_t P,
+                          int64_t k, void* out, int64_t out_ld_bytes, int64_t idx_off_bytes,
+                          void* work, int64_t work_ld_bytes, void* stream);
 
 /* ChocoCommunicator.averaging (communicator.py:200-230) for one round of n_local workers,
  * in place on the state rows (a round whose flags are all zero must not be applied):
