@@ -25,8 +25,7 @@
 namespace {
 constexpr int kTPB = 256;
 constexpr int kWaves = kTPB / 64;
-constexpr int kChunk = 4096;                 // elements per chunk (16 per lane)
-constexpr int kSub = kChunk / kTPB;
+constexpr int kChunk = 4096;                 // elements per chunk (4 quads of 4 per lane)
 constexpr int kTopBits = 12, kTopShift = 19;
 constexpr int kTopBins = 1 << kTopBits;
 constexpr int kMidBits = 10, kMidShift = 9;  // bits 9..18
@@ -109,8 +108,47 @@ __device__ __forceinline__ float diff_at(const float* x, const float* xh, int64_
     return xh ? __fsub_rn(x[i], xh[i]) : x[i];
 }
 
-__device__ __forceinline__ uint32_t lane_prefix(uint64_t m) {     // set bits below this lane
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// elements 4q .. 4q+3 of x - x_hat (16-byte non-temporal loads when the rows are aligned);
+// returns how many of them are < P
+__device__ __forceinline__ int load_quad(const float* x, const float* xh, int64_t q, int64_t P, bool vec,
+                                         float (&d)[4]) {
+    const int64_t i0 = 4 * q;
+    if (vec && i0 + 4 <= P) {
+        const f4 a = __builtin_nontemporal_load(reinterpret_cast<const f4*>(x) + q);
+        if (xh) {
+            const f4 b = __builtin_nontemporal_load(reinterpret_cast<const f4*>(xh) + q);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) d[c] = __fsub_rn(a[c], b[c]);
+        } else {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) d[c] = a[c];
+        }
+        return 4;
+    }
+    int n = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int64_t i = i0 + c;
+        d[c] = 0.0f;
+        if (i < P) {
+            d[c] = diff_at(x, xh, i);
+            ++n;
+        }
+    }
+    return n;
+}
+
+// inclusive scan of a per-lane count over the wave
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
 }
 
 // ---- A: top-digit histogram
@@ -119,8 +157,24 @@ __global__ __launch_bounds__(kTPB) void hist_kernel(Rows R) {
     __shared__ uint32_t h[kTopBins];
     for (int i = threadIdx.x; i < kTopBins; i += kTPB) h[i] = 0;
     __syncthreads();
-    for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < R.P; i += (int64_t)gridDim.x * kTPB)
-        atomicAdd(&h[key_of(diff_at(v.x, v.xh, i)) >> kTopShift], 1u);
+    const bool vec = (((uintptr_t)v.x | (uintptr_t)v.xh) & 15) == 0;
+    const int64_t nq = (R.P + 3) / 4;
+    constexpr int U = 4;                       // quads in flight per lane
+    const int64_t stride = (int64_t)gridDim.x * kTPB;
+    for (int64_t q0 = (int64_t)blockIdx.x * kTPB + threadIdx.x; q0 < nq; q0 += U * stride) {
+        float d[U][4];
+        int n[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t q = q0 + u * stride;
+            n[u] = q < nq ? load_quad(v.x, v.xh, q, R.P, vec, d[u]) : 0;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (c < n[u]) atomicAdd(&h[key_of(d[u][c]) >> kTopShift], 1u);
+    }
     __syncthreads();
     for (int i = threadIdx.x; i < kTopBins; i += kTPB)
         if (h[i]) atomicAdd(&v.hist[i], h[i]);
@@ -178,66 +232,67 @@ __global__ __launch_bounds__(kTPB) void select_top(Rows R) {
     }
 }
 
-// ---- B: per-chunk "certainly selected" counts + candidate compaction.  The chunk's 16 keys per
-// lane stay in registers; one wave ballot per sub-tile gives every candidate its rank, and ONE
-// global atomic per block reserves the block's candidate range.
+// ---- B: per-chunk "certainly selected" counts + candidate compaction.  A chunk is 4 sub-tiles of
+// 256 lanes x one 16-byte quad; the 16 keys per lane stay in registers, a wave scan of the
+// per-lane candidate counts ranks them and ONE global atomic per block reserves the block's range
+// (candidate order is irrelevant: only order-free statistics are taken from the list).
+constexpr int kQuads = kChunk / (4 * kTPB);   // quads per lane per chunk
+
 __global__ __launch_bounds__(kTPB) void split_kernel(Rows R) {
     const RowView v = row_view(R);
-    const float* x = v.x;
-    const float* xh = v.xh;
     const int64_t P = R.P;
     SelState* st = v.st;
-    int64_t* cnt = v.cnt;
-    int64_t* cand_idx = v.cidx;
-    uint32_t* cand_key = v.ckey;
-    __shared__ uint32_t wc[kSub][kWaves];
-    __shared__ uint32_t wabove[kWaves];
+    __shared__ uint32_t wcand[kWaves], wabove[kWaves];
     __shared__ unsigned long long base_s;
     const uint32_t b0 = st->b0;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t chunk0 = (int64_t)blockIdx.x * kChunk;
-    uint32_t keys[kSub];
-    uint64_t masks[kSub];
-    uint32_t above = 0;
+    const bool vec = (((uintptr_t)v.x | (uintptr_t)v.xh) & 15) == 0;
+    const int64_t q0 = (int64_t)blockIdx.x * (kChunk / 4);
+    uint32_t keys[kQuads][4];
+    uint32_t ccount = 0, above = 0;
 #pragma unroll
-    for (int j = 0; j < kSub; ++j) {
-        const int64_t i = chunk0 + (int64_t)j * kTPB + threadIdx.x;
-        const bool in = i < P;
-        keys[j] = in ? key_of(diff_at(x, xh, i)) : 0u;
-        const uint32_t d = keys[j] >> kTopShift;
-        above += (in && d > b0);
-        masks[j] = __ballot(in && d == b0);
-        if (lane == 0) wc[j][wave] = (uint32_t)__popcll(masks[j]);
+    for (int j = 0; j < kQuads; ++j) {
+        float d[4];
+        const int n = load_quad(v.x, v.xh, q0 + (int64_t)j * kTPB + threadIdx.x, P, vec, d);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const bool in = c < n;
+            keys[j][c] = in ? key_of(d[c]) : 0xffffffffu;    // sentinel: never a candidate / above
+            const uint32_t dg = keys[j][c] >> kTopShift;
+            above += in && dg > b0;
+            ccount += in && dg == b0;
+        }
     }
-    // wave total of `above` via a butterfly, then per-wave slots
-    for (int o = 32; o > 0; o >>= 1) above += __shfl_xor(above, o, 64);
-    if (lane == 0) wabove[wave] = above;
+    const uint32_t incl = wave_incl_scan(ccount);
+    uint32_t ab = above;
+    for (int o = 32; o > 0; o >>= 1) ab += __shfl_xor(ab, o, 64);
+    if (lane == 63) wcand[wave] = incl;
+    if (lane == 0) wabove[wave] = ab;
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint64_t tot = 0, ab = 0;
-        for (int j = 0; j < kSub; ++j)
-            for (int w = 0; w < kWaves; ++w) tot += wc[j][w];
-        for (int w = 0; w < kWaves; ++w) ab += wabove[w];
+        uint64_t tot = 0, a = 0;
+        for (int w = 0; w < kWaves; ++w) {
+            tot += wcand[w];
+            a += wabove[w];
+        }
         base_s = tot ? atomicAdd((unsigned long long*)&st->cand_n, (unsigned long long)tot) : 0ull;
-        cnt[3 * blockIdx.x + 0] = (int64_t)ab;
-        cnt[3 * blockIdx.x + 1] = 0;
-        cnt[3 * blockIdx.x + 2] = 0;
+        v.cnt[3 * blockIdx.x + 0] = (int64_t)a;
+        v.cnt[3 * blockIdx.x + 1] = 0;
+        v.cnt[3 * blockIdx.x + 2] = 0;
     }
     __syncthreads();
-    uint64_t run = base_s;
+    uint64_t pos = base_s + (incl - ccount);
+    for (int w = 0; w < wave; ++w) pos += wcand[w];
 #pragma unroll
-    for (int j = 0; j < kSub; ++j) {
-        uint32_t wpre = 0, tot = 0;
-        for (int w = 0; w < kWaves; ++w) {
-            wpre += (w < wave) ? wc[j][w] : 0;
-            tot += wc[j][w];
+    for (int j = 0; j < kQuads; ++j) {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if ((keys[j][c] >> kTopShift) == b0 && keys[j][c] != 0xffffffffu) {
+                v.cidx[pos] = 4 * (q0 + (int64_t)j * kTPB + threadIdx.x) + c;
+                v.ckey[pos] = keys[j][c];
+                ++pos;
+            }
         }
-        if ((masks[j] >> lane) & 1ull) {
-            const int64_t pos = (int64_t)run + wpre + lane_prefix(masks[j]);
-            cand_idx[pos] = chunk0 + (int64_t)j * kTPB + threadIdx.x;
-            cand_key[pos] = keys[j];
-        }
-        run += tot;
     }
 }
 
@@ -337,55 +392,66 @@ __global__ __launch_bounds__(kScanTPB) void scan_kernel(Rows R) {
     }
 }
 
-// ---- C: stable per-chunk compaction in index order
+// ---- C: stable per-chunk compaction in index order.  In sub-tile j lane l holds elements
+// 4(q0 + j*256 + l) .. +3, so index order is lane-major: a wave scan of per-lane counts (0..4)
+// plus the per-wave totals in LDS rank every tie and every selected element.
 __global__ __launch_bounds__(kTPB) void write_kernel(Rows R) {
     const RowView v = row_view(R);
-    const float* x = v.x;
-    const float* xh = v.xh;
     const int64_t P = R.P;
-    const SelState* st = v.st;
-    const int64_t* off = v.off;
-    float* vals = v.vals;
-    int64_t* idx = v.idx;
     __shared__ uint32_t weq[2][kWaves], wsel[2][kWaves];
-    const uint32_t T = st->T;
-    const int64_t need_eq = st->need;
+    const uint32_t T = v.st->T;
+    const int64_t need_eq = v.st->need;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t chunk0 = (int64_t)blockIdx.x * kChunk;
-    int64_t run_out = off[2 * blockIdx.x], run_eq = off[2 * blockIdx.x + 1];
-    for (int j = 0; j < kSub; ++j) {
+    const bool vec = (((uintptr_t)v.x | (uintptr_t)v.xh) & 15) == 0;
+    const int64_t q0 = (int64_t)blockIdx.x * (kChunk / 4);
+    int64_t run_out = v.off[2 * blockIdx.x], run_eq = v.off[2 * blockIdx.x + 1];
+    for (int j = 0; j < kQuads; ++j) {
         const int par = j & 1;
-        const int64_t i = chunk0 + (int64_t)j * kTPB + threadIdx.x;
-        float d = 0.0f;
-        uint32_t key = 0;
-        const bool in = i < P;
-        if (in) {
-            d = diff_at(x, xh, i);
-            key = key_of(d);
+        const int64_t q = q0 + (int64_t)j * kTPB + threadIdx.x;
+        float d[4];
+        const int n = load_quad(v.x, v.xh, q, P, vec, d);
+        uint32_t key[4];
+        uint32_t ne = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            key[c] = key_of(d[c]);
+            ne += (c < n) && key[c] == T;
         }
-        const bool eq = in && key == T;
-        const uint64_t me = __ballot(eq);
-        if (lane == 0) weq[par][wave] = (uint32_t)__popcll(me);
+        const uint32_t einc = wave_incl_scan(ne);
+        if (lane == 63) weq[par][wave] = einc;
         __syncthreads();
         uint32_t epre = 0, etot = 0;
         for (int w = 0; w < kWaves; ++w) {
             epre += (w < wave) ? weq[par][w] : 0;
             etot += weq[par][w];
         }
-        const int64_t eq_rank = run_eq + epre + lane_prefix(me);
-        const bool sel = in && (key > T || (eq && eq_rank < need_eq));
-        const uint64_t ms = __ballot(sel);
-        if (lane == 0) wsel[par][wave] = (uint32_t)__popcll(ms);
+        int64_t er = run_eq + epre + (einc - ne);
+        bool sel[4];
+        uint32_t ns = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const bool in = c < n;
+            const bool eq = in && key[c] == T;
+            sel[c] = in && (key[c] > T || (eq && er < need_eq));
+            er += eq;
+            ns += sel[c];
+        }
+        const uint32_t sinc = wave_incl_scan(ns);
+        if (lane == 63) wsel[par][wave] = sinc;
         __syncthreads();
         uint32_t spre = 0, stot = 0;
         for (int w = 0; w < kWaves; ++w) {
             spre += (w < wave) ? wsel[par][w] : 0;
             stot += wsel[par][w];
         }
-        if (sel) {
-            const int64_t pos = run_out + spre + lane_prefix(ms);
-            vals[pos] = d;
-            idx[pos] = i;
+        int64_t pos = run_out + spre + (sinc - ns);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (sel[c]) {
+                v.vals[pos] = d[c];
+                v.idx[pos] = 4 * q + c;
+                ++pos;
+            }
         }
         run_out += stot;
         run_eq += etot;
