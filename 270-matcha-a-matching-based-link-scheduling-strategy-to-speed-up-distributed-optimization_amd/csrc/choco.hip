@@ -38,7 +38,7 @@ struct SelState {
     uint32_t prefix;      // candidate-pass prefix (bits fixed so far, shifted to full key)
     uint32_t mask;
     int64_t need;         // keys still to take at/below the current bin / prefix
-    int64_t cand_n;       // candidates appended in pass B
+    int64_t cand_n;       // unused (candidates live in per-chunk regions)
 };
 
 struct WorkLayout {
@@ -51,7 +51,7 @@ __host__ __device__ inline WorkLayout layout(int64_t P) {
     w.hist = 0;
     w.state = w.hist + sizeof(uint32_t) * kTopBins;
     w.cnt = w.state + 64;
-    w.off = w.cnt + sizeof(int64_t) * 3 * (size_t)nchunks;
+    w.off = w.cnt + sizeof(int64_t) * 4 * (size_t)nchunks;
     w.cidx = (w.off + sizeof(int64_t) * 2 * (size_t)nchunks + 255) / 256 * 256;
     w.ckey = w.cidx + sizeof(int64_t) * (size_t)P;
     w.total = (w.ckey + sizeof(uint32_t) * (size_t)P + 255) / 256 * 256;
@@ -233,18 +233,17 @@ __global__ __launch_bounds__(kTPB) void select_top(Rows R) {
 }
 
 // ---- B: per-chunk "certainly selected" counts + candidate compaction.  A chunk is 4 sub-tiles of
-// 256 lanes x one 16-byte quad; the 16 keys per lane stay in registers, a wave scan of the
-// per-lane candidate counts ranks them and ONE global atomic per block reserves the block's range
-// (candidate order is irrelevant: only order-free statistics are taken from the list).
+// 256 lanes x one 16-byte quad; the 16 keys per lane stay in registers and a wave scan of the
+// per-lane candidate counts ranks them inside the chunk's OWN region of the candidate buffer
+// (chunk c owns slots [c*4096, c*4096 + ncand)), so no global atomics are needed.
+// cnt[4c + 0..3] = {keys above digit b0, candidates > T, candidates == T, candidates}.
 constexpr int kQuads = kChunk / (4 * kTPB);   // quads per lane per chunk
 
 __global__ __launch_bounds__(kTPB) void split_kernel(Rows R) {
     const RowView v = row_view(R);
     const int64_t P = R.P;
-    SelState* st = v.st;
     __shared__ uint32_t wcand[kWaves], wabove[kWaves];
-    __shared__ unsigned long long base_s;
-    const uint32_t b0 = st->b0;
+    const uint32_t b0 = v.st->b0;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const bool vec = (((uintptr_t)v.x | (uintptr_t)v.xh) & 15) == 0;
     const int64_t q0 = (int64_t)blockIdx.x * (kChunk / 4);
@@ -269,27 +268,25 @@ __global__ __launch_bounds__(kTPB) void split_kernel(Rows R) {
     if (lane == 63) wcand[wave] = incl;
     if (lane == 0) wabove[wave] = ab;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t tot = 0, a = 0;
-        for (int w = 0; w < kWaves; ++w) {
-            tot += wcand[w];
-            a += wabove[w];
-        }
-        base_s = tot ? atomicAdd((unsigned long long*)&st->cand_n, (unsigned long long)tot) : 0ull;
-        v.cnt[3 * blockIdx.x + 0] = (int64_t)a;
-        v.cnt[3 * blockIdx.x + 1] = 0;
-        v.cnt[3 * blockIdx.x + 2] = 0;
+    uint32_t pos = incl - ccount;
+    uint32_t tot = 0, a = 0;
+    for (int w = 0; w < kWaves; ++w) {
+        pos += (w < wave) ? wcand[w] : 0;
+        tot += wcand[w];
+        a += wabove[w];
     }
-    __syncthreads();
-    uint64_t pos = base_s + (incl - ccount);
-    for (int w = 0; w < wave; ++w) pos += wcand[w];
+    if (threadIdx.x == 0) {
+        v.cnt[4 * blockIdx.x + 0] = a;
+        v.cnt[4 * blockIdx.x + 3] = tot;
+    }
+    const int64_t region = (int64_t)blockIdx.x * kChunk;
 #pragma unroll
     for (int j = 0; j < kQuads; ++j) {
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             if ((keys[j][c] >> kTopShift) == b0 && keys[j][c] != 0xffffffffu) {
-                v.cidx[pos] = 4 * (q0 + (int64_t)j * kTPB + threadIdx.x) + c;
-                v.ckey[pos] = keys[j][c];
+                v.cidx[region + pos] = 4 * (q0 + (int64_t)j * kTPB + threadIdx.x) + c;
+                v.ckey[region + pos] = keys[j][c];
                 ++pos;
             }
         }
@@ -297,25 +294,27 @@ __global__ __launch_bounds__(kTPB) void split_kernel(Rows R) {
 }
 
 // candidate histogram of `bits` bits at `shift`, restricted to keys matching st->prefix/mask
+// one wave per chunk region; the block's LDS histogram is flushed once (few global atomics)
 template <int BITS>
 __global__ __launch_bounds__(kTPB) void cand_hist(Rows R, int shift) {
     const RowView v = row_view(R);
-    const uint32_t* cand_key = v.ckey;
-    const SelState* st = v.st;
-    uint32_t* ghist = v.hist;
     constexpr int NB = 1 << BITS;
     __shared__ uint32_t h[NB];
     for (int i = threadIdx.x; i < NB; i += kTPB) h[i] = 0;
     __syncthreads();
-    const int64_t n = st->cand_n;
-    const uint32_t prefix = st->prefix, mask = st->mask;
-    for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kTPB) {
-        const uint32_t key = cand_key[i];
-        if ((key & mask) == prefix) atomicAdd(&h[(key >> shift) & (NB - 1)], 1u);
+    const uint32_t prefix = v.st->prefix, mask = v.st->mask;
+    const int64_t nchunks = (R.P + kChunk - 1) / kChunk;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int64_t c = (int64_t)blockIdx.x * kWaves + wave; c < nchunks; c += (int64_t)gridDim.x * kWaves) {
+        const int64_t nc = v.cnt[4 * c + 3];
+        for (int64_t i = lane; i < nc; i += 64) {
+            const uint32_t key = v.ckey[c * kChunk + i];
+            if ((key & mask) == prefix) atomicAdd(&h[(key >> shift) & (NB - 1)], 1u);
+        }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < NB; i += kTPB)
-        if (h[i]) atomicAdd(&ghist[i], h[i]);
+        if (h[i]) atomicAdd(&v.hist[i], h[i]);
 }
 
 template <int BITS>
@@ -337,19 +336,28 @@ __global__ __launch_bounds__(kTPB) void select_cand(Rows R, int shift) {
 }
 
 // per-chunk counts of candidates strictly above T and equal to T
+// one wave per chunk region: counts of candidates > T and == T, written without atomics
 __global__ __launch_bounds__(kTPB) void cand_mark(Rows R) {
     const RowView v = row_view(R);
-    const int64_t* cand_idx = v.cidx;
-    const uint32_t* cand_key = v.ckey;
-    const SelState* st = v.st;
-    int64_t* cnt = v.cnt;
-    const int64_t n = st->cand_n;
-    const uint32_t T = st->T;
-    for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < n; i += (int64_t)gridDim.x * kTPB) {
-        const uint32_t key = cand_key[i];
-        const int64_t c = cand_idx[i] / kChunk;
-        if (key > T) atomicAdd((unsigned long long*)&cnt[3 * c + 1], 1ull);
-        else if (key == T) atomicAdd((unsigned long long*)&cnt[3 * c + 2], 1ull);
+    const uint32_t T = v.st->T;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t nchunks = (R.P + kChunk - 1) / kChunk;
+    for (int64_t c = (int64_t)blockIdx.x * kWaves + wave; c < nchunks; c += (int64_t)gridDim.x * kWaves) {
+        const int64_t nc = v.cnt[4 * c + 3];
+        uint32_t g = 0, e = 0;
+        for (int64_t i = lane; i < nc; i += 64) {
+            const uint32_t key = v.ckey[c * kChunk + i];
+            g += key > T;
+            e += key == T;
+        }
+        for (int o = 32; o > 0; o >>= 1) {
+            g += __shfl_xor(g, o, 64);
+            e += __shfl_xor(e, o, 64);
+        }
+        if (lane == 0) {
+            v.cnt[4 * c + 1] = g;
+            v.cnt[4 * c + 2] = e;
+        }
     }
 }
 
@@ -368,8 +376,8 @@ __global__ __launch_bounds__(kScanTPB) void scan_kernel(Rows R) {
     __syncthreads();
     for (int64_t b0 = 0; b0 < nchunks; b0 += kScanTPB) {
         const int64_t b = b0 + threadIdx.x;
-        const int64_t g = b < nchunks ? cnt[3 * b] + cnt[3 * b + 1] : 0;   // keys > T
-        const int64_t e = b < nchunks ? cnt[3 * b + 2] : 0;                // keys == T
+        const int64_t g = b < nchunks ? cnt[4 * b] + cnt[4 * b + 1] : 0;   // keys > T
+        const int64_t e = b < nchunks ? cnt[4 * b + 2] : 0;                // keys == T
         int64_t sg = g, se = e;                                            // wave inclusive scan
         for (int o = 1; o < 64; o <<= 1) {
             const int64_t tg = __shfl_up(sg, o, 64), te = __shfl_up(se, o, 64);
@@ -550,7 +558,7 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
                               sizeof(uint32_t) * kTopBins, st));
     const unsigned nchunks = (unsigned)((P + kChunk - 1) / kChunk);
     const unsigned hgrid = clamp_grid(P, (int64_t)kTPB * 64, (512 + nrows - 1) / nrows);
-    const unsigned cgrid = clamp_grid(P, (int64_t)kTPB * 64, (512 + nrows - 1) / nrows);
+    const unsigned cgrid = clamp_grid((P + kChunk - 1) / kChunk, kWaves, (1024 + nrows - 1) / nrows);
     const dim3 one(1, nrows);
     hipLaunchKernelGGL(hist_kernel, dim3(hgrid, nrows), dim3(kTPB), 0, st, R);
     MX_LAUNCH_CHECK();
