@@ -73,13 +73,25 @@ class _Staging:
 
 
 class Communicator(object):
-    """communicator.py:10-43 -- communicate(model) -> seconds spent averaging."""
+    """communicator.py:10-43 -- communicate(model) -> seconds spent averaging.
 
-    def __init__(self, rank, size):
+    `transport` (keyword-only extension, default None = the process-wide RCCL communicator
+    bootstrapped over torch.distributed) may be any object GossipEngine accepts as its comm."""
+
+    def __init__(self, rank, size, *, transport=None):
         self.comm = None
         self.rank = rank
         self.size = size
-        _ensure_process_group(rank, size)
+        self._transport = transport
+        if transport is None:
+            _ensure_process_group(rank, size)
+        else:
+            require_device()
+
+    def _comm(self):
+        if self.size <= 1:
+            return None
+        return self._transport if self._transport is not None else default_comm()
 
     def communicate(self, model):
         raise NotImplementedError
@@ -88,8 +100,8 @@ class Communicator(object):
 class decenCommunicator(Communicator):
     """communicator.py:79-158 -- decentralized averaging according to the topology's schedule."""
 
-    def __init__(self, rank, size, topology):
-        super(decenCommunicator, self).__init__(rank, size)
+    def __init__(self, rank, size, topology, *, transport=None):
+        super(decenCommunicator, self).__init__(rank, size, transport=transport)
         self.topology = topology
         self.neighbor_weight = topology.neighbor_weight
         self.iter = 0
@@ -100,7 +112,7 @@ class decenCommunicator(Communicator):
     def _bind(self, model):
         params = [p for p in model.parameters()]
         on_gpu = all(p.device.type == "cuda" for p in params)
-        comm = default_comm() if self.size > 1 else None
+        comm = self._comm()
         if on_gpu:
             self._group = VirtualWorkerGroup(self.topology, [model], rank=self.rank, nranks=self.size,
                                              comm=comm)
@@ -135,8 +147,8 @@ class decenCommunicator(Communicator):
 class ChocoCommunicator(Communicator):
     """communicator.py:161-268 -- top-k compressed gossip with persistent x_hat / s."""
 
-    def __init__(self, rank, size, topology, ratio, consensus_lr):
-        super(ChocoCommunicator, self).__init__(rank, size)
+    def __init__(self, rank, size, topology, ratio, consensus_lr, *, transport=None):
+        super(ChocoCommunicator, self).__init__(rank, size, transport=transport)
         self.topology = topology
         self.neighbor_weight = topology.neighbor_weight
         self.iter = 0
@@ -157,7 +169,7 @@ class ChocoCommunicator(Communicator):
     def _bind(self, model):
         params = [p for p in model.parameters()]
         on_gpu = all(p.device.type == "cuda" for p in params)
-        comm = default_comm() if self.size > 1 else None
+        comm = self._comm()
         if on_gpu:
             self._group = ChocoWorkerGroup(self.topology, [model], ratio=self.ratio,
                                            consensus_lr=self.consensus_lr, rank=self.rank,
@@ -194,8 +206,8 @@ class ChocoCommunicator(Communicator):
 class centralizedCommunicator(Communicator):
     """communicator.py:46-76 -- all-reduce averaging: x = allreduce_sum(x) / size (RCCL)."""
 
-    def __init__(self, rank, size):
-        super(centralizedCommunicator, self).__init__(rank, size)
+    def __init__(self, rank, size, *, transport=None):
+        super(centralizedCommunicator, self).__init__(rank, size, transport=transport)
 
     def communicate(self, model):
         tensors = [p.data for p in model.parameters()]
@@ -204,8 +216,12 @@ class centralizedCommunicator(Communicator):
         torch.cuda.synchronize()
         tic = time.time()
         if self.size > 1:
-            check(lib.mx_allreduce_mean(default_comm().handle, flat.data_ptr(), flat.numel(), self.size,
-                                        stream_ptr()), "mx_allreduce_mean")
+            comm = self._comm()
+            if hasattr(comm, "allreduce_mean"):
+                comm.allreduce_mean(flat, self.size)
+            else:
+                check(lib.mx_allreduce_mean(comm.handle, flat.data_ptr(), flat.numel(), self.size,
+                                            stream_ptr()), "mx_allreduce_mean")
         torch.cuda.synchronize()
         toc = time.time()
         with torch.no_grad():

@@ -52,17 +52,30 @@ class Topo:
 class LoopbackHub:
     """Test double for the RCCL transport: N simulated ranks on ONE GPU in one process.
 
-    Each rank's GossipEngine gets a LoopbackComm; a round runs in two phases driven by the test:
-    every rank's exchange (the ops of the native mx_exchange_plan, executed as device copies from
-    the peer rank's rows into this rank's slab, in posting order), then every rank's mix."""
+    Ranks register their rows (``register``).  At a rank's exchange for iteration `it` the hub
+    first snapshots that rank's own pre-round rows, then fills each receive-slab slot named by the
+    native mx_exchange_plan with the sender's row for iteration `it`: its snapshot if the sender
+    already took part in `it` (and has since mixed in place), else its live row (it has not
+    started `it` yet).  That is exactly what concurrent ncclSend/ncclRecv pairs deliver, so ranks
+    may be stepped one after another in one thread."""
 
     def __init__(self, nranks):
+        import ctypes
         self.nranks = nranks
-        self.rows = {}          # rank -> {local row index: device pointer}
-        self.row_base = {}
+        self.live = {}          # worker id -> device pointer of its current row
+        self.snap = {}          # (it, worker id) -> torch tensor copy of the pre-round row
+        self.hip = ctypes.CDLL("libamdhip64.so")
+        self.hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+
+    def register(self, row_base, row_ptrs):
+        for r, p in enumerate(row_ptrs):
+            self.live[row_base + r] = int(p)
 
     def comm(self, rank):
         return LoopbackComm(self, rank)
+
+    def copy(self, dst, src, nbytes):
+        assert self.hip.hipMemcpy(int(dst), int(src), int(nbytes), 3) == 0   # device to device
 
 
 class LoopbackComm:
@@ -71,16 +84,25 @@ class LoopbackComm:
         self.handle = None
 
     def exchange_round(self, engine, it, row_ptrs, slab_ptr, slab_ld_bytes, row_bytes):
-        import ctypes
         import torch
-        hip = ctypes.CDLL("libamdhip64.so")
-        hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
         torch.cuda.synchronize()
+        hub = self.hub
+        hub.register(engine.row_base, row_ptrs)
+        for r, p in enumerate(row_ptrs):
+            w = engine.row_base + r
+            if (it, w) not in hub.snap:
+                t = torch.empty(row_bytes // 4, dtype=torch.float32, device="cuda")
+                hub.copy(t.data_ptr(), p, row_bytes)
+                hub.snap[(it, w)] = t
         nrem = 0
         for kind, peer, idx, who in engine.exchange_plan(it):
-            if kind == 1:   # what ncclRecv delivers: the partner's pre-round row into slab slot idx
-                src = self.hub.rows[int(peer)][int(who) - self.hub.row_base[int(peer)]]
-                dst = slab_ptr + int(idx) * slab_ld_bytes
-                assert hip.hipMemcpy(dst, src, int(row_bytes), 3) == 0   # device to device
+            if kind == 1:
+                who = int(who)
+                src = hub.snap[(it, who)].data_ptr() if (it, who) in hub.snap else hub.live[who]
+                hub.copy(slab_ptr + int(idx) * slab_ld_bytes, src, row_bytes)
                 nrem += 1
+        torch.cuda.synchronize()
         return nrem
+
+    def allreduce_mean(self, flat, size):
+        raise NotImplementedError("loopback transport: all-reduce is not emulated")

@@ -351,19 +351,49 @@ def test_multirank_pipeline_loopback(pkg, O, gid, nranks):
     X = np.stack([O.synth(700 + i, P) for i in range(n)])
     for g in groups:
         g.rows.copy_(torch.from_numpy(X[g.row_base:g.row_base + g.n_local]))
+        hub.register(g.row_base, g._row_ptrs)
     for it, f in enumerate(flags):
-        if not f.any():
-            continue
-        for g in groups:                       # phase 1: every rank's receives (pre-round rows)
-            hub.rows[g.engine.rank] = list(g._row_ptrs)
-            hub.row_base[g.engine.rank] = g.row_base
-        for g in groups:
-            g.engine.exchange(it, g._row_ptrs, g.slab.data_ptr() if g.slab is not None else None,
-                              g.ld * 4, g.numel * 4)
-        torch.cuda.synchronize()
-        for g in groups:                       # phase 2: every rank's mix
-            g.engine.mix(it, g.layout)
+        for g in groups:                       # ranks one after another: exchange + mix each
+            g.step(it)
         torch.cuda.synchronize()
         X = O.decen_round(X, topo.neighbors_info, f, 0.17)
     got = np.concatenate([g.rows.cpu().numpy() for g in groups])
     assert np.array_equal(got.view(np.uint32), X.view(np.uint32))
+
+
+@pytest.mark.parametrize("on_gpu", [True, False])
+def test_dropin_decen_communicators_per_rank(pkg, O, on_gpu):
+    """The reference API one process per worker -- here 8 decenCommunicator(rank, 8, GP) objects
+    in one process on one GPU over the loopback transport -- with nn.Module workers on the GPU
+    (adopted into arenas) or on the CPU (staged, as the reference's train_mpi.py keeps them).
+    communicate() return values, skipped rounds and parameter identity as in the reference."""
+    from conftest import LoopbackHub
+    n = 8
+    np.random.seed(1234)
+    GP = pkg.MatchaProcessor(pkg.select_graph(0), 0.5, 0, n, 12, True)
+    dev = "cuda" if on_gpu else "cpu"
+    torch.manual_seed(3)
+    models = [torch.nn.Sequential(torch.nn.Linear(20, 31), torch.nn.Tanh(), torch.nn.Linear(31, 3)).to(dev)
+              for _ in range(n)]
+    ids = [[id(p) for p in m.parameters()] for m in models]
+    X = np.stack([torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy() for m in models])
+    hub = LoopbackHub(n)
+    comms = [pkg.decenCommunicator(r, n, GP, transport=hub.comm(r)) for r in range(n)]
+    for r in range(n):                         # bind + stage every rank before round 0
+        comms[r]._bind(models[r])
+        comms[r]._stage.load()
+        hub.register(r, [comms[r]._group.rows[0].data_ptr()])
+    partner = np.asarray(GP.neighbors_info, np.int32)
+    for it in range(12):
+        f = np.asarray(GP.active_flags[it], np.uint8)
+        times = [comms[r].communicate(models[r]) for r in range(n)]
+        if not f.any():
+            assert times == [0] * n
+        else:
+            assert all(t > 0 for t in times)
+            X = O.decen_round(X, partner, f, GP.neighbor_weight)
+        got = np.stack([torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy() for m in models])
+        assert np.array_equal(got.view(np.uint32), X.view(np.uint32)), f"iteration {it}"
+    assert all(c.iter == 12 for c in comms)
+    assert ids == [[id(p) for p in m.parameters()] for m in models]
+    assert all(p.device.type == dev for m in models for p in m.parameters())
