@@ -77,22 +77,33 @@ class ChocoWorkerGroup:
         idx = self.msgs[base + 4 * self.kpad:base + 4 * self.kpad + 8 * self.k].view(torch.int64)
         return vals, idx
 
-    def step(self, it, stream=None):
-        if not self.engine.any_active[it]:
-            return False
-        P = self.numel
-        st = stream_ptr(stream)
+    def compress(self, it, stream=None):
+        """prepare_comm_buffer (communicator.py:175-196): every local row's top-k message of
+        x - x_hat into its message slot."""
+        check(lib.mx_topk_abs_diff_rows(self.x.data_ptr(), self.x_hat.data_ptr(), self.ld, self.n_local,
+                                        self.numel, self.k, self.msgs.data_ptr(), self.msg_ld, 4 * self.kpad,
+                                        self.work.data_ptr(), self.work_ld, stream_ptr(stream)),
+              "mx_topk_abs_diff_rows")
+
+    def average(self, it, stream=None):
+        """averaging (communicator.py:200-230): receive partner messages ([N > 1] over the
+        transport into the message slots after the local ones), then the s / x_hat scatters and
+        the dense x update."""
         mbase = self.msgs.data_ptr()
-        check(lib.mx_topk_abs_diff_rows(self.x.data_ptr(), self.x_hat.data_ptr(), self.ld, self.n_local, P,
-                                        self.k, mbase, self.msg_ld, 4 * self.kpad, self.work.data_ptr(),
-                                        self.work_ld, st), "mx_topk_abs_diff_rows")
         if self.engine.comm is not None:
             self.engine.exchange(it, [mbase + r * self.msg_ld for r in range(self.n_local)],
                                  mbase + self.n_local * self.msg_ld, self.msg_ld, self.msg_bytes, stream)
-        check(lib.mx_choco_apply(self.x.data_ptr(), self.x_hat.data_ptr(), self.s.data_ptr(), self.ld, P,
-                                 self.k, mbase, self.msg_ld, self.engine.plan.data_ptr(), int(it),
-                                 self.n_local, self.engine.M, self.engine.alpha32, self.gamma32, st),
-              "mx_choco_apply")
+        check(lib.mx_choco_apply(self.x.data_ptr(), self.x_hat.data_ptr(), self.s.data_ptr(), self.ld,
+                                 self.numel, self.k, mbase, self.msg_ld, self.engine.plan.data_ptr(), int(it),
+                                 self.n_local, self.engine.M, self.engine.alpha32, self.gamma32,
+                                 stream_ptr(stream)), "mx_choco_apply")
+
+    def step(self, it, stream=None):
+        """One round at iteration `it`; False (nothing done) for an all-zero flags row."""
+        if not self.engine.any_active[it]:
+            return False
+        self.compress(it, stream)
+        self.average(it, stream)
         return True
 
     def communicate(self):

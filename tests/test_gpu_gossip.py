@@ -397,3 +397,38 @@ def test_dropin_decen_communicators_per_rank(pkg, O, on_gpu):
     assert all(c.iter == 12 for c in comms)
     assert ids == [[id(p) for p in m.parameters()] for m in models]
     assert all(p.device.type == dev for m in models for p in m.parameters())
+
+
+@pytest.mark.parametrize("nranks", [2, 4, 8])
+def test_choco_multirank_loopback(pkg, O, nranks):
+    """ChocoWorkerGroups of N ranks on one GPU: every rank compresses, then each receives its
+    partners' messages (loopback transport, native exchange order) and averages; bit-exact vs the
+    single-process oracle over 4 rounds with parameter drift between rounds."""
+    from conftest import LoopbackHub
+    n, P, ratio = 8, 30_011, 0.95
+    gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, n, 4, True)
+    flags = np.array([[1, 1, 1, 1, 1], [1, 0, 1, 0, 1], [0, 0, 0, 0, 0], [0, 1, 1, 1, 0]], np.uint8)
+    topo = Topo(gp.neighbors_info, 2 / 7, flags)
+    hub = LoopbackHub(nranks)
+    groups = [pkg.ChocoWorkerGroup(topo, numel=P, ratio=ratio, consensus_lr=0.3, rank=r, nranks=nranks,
+                                   comm=hub.comm(r)) for r in range(nranks)]
+    X = np.stack([O.synth(40 + i, P) for i in range(n)])
+    XH, S = np.zeros_like(X), np.zeros_like(X)
+    k = O.topk_k(P, ratio)
+    for g in groups:
+        g.rows.copy_(torch.from_numpy(X[g.row_base:g.row_base + g.n_local]))
+    for t, f in enumerate(flags):
+        if t:
+            D = np.stack([np.float32(0.02) * O.synth(77 * t + i, P) for i in range(n)])
+            X += D
+            for g in groups:
+                g.rows.add_(torch.from_numpy(D[g.row_base:g.row_base + g.n_local]).cuda())
+        if f.any():
+            for g in groups:
+                g.compress(t)
+            for g in groups:
+                g.average(t)
+            torch.cuda.synchronize()
+        O.choco_round(X, XH, S, topo.neighbors_info, f, 2 / 7, k, 0.3)
+        got = np.concatenate([g.rows.cpu().numpy() for g in groups])
+        assert np.array_equal(got.view(np.uint32), X.view(np.uint32)), f"round {t}"
