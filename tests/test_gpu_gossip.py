@@ -426,6 +426,7 @@ def test_choco_multirank_loopback(pkg, O, nranks):
         if f.any():
             for g in groups:
                 g.compress(t)
+                hub.register(g.row_base, [g.msgs.data_ptr() + r * g.msg_ld for r in range(g.n_local)])
             for g in groups:
                 g.average(t)
             torch.cuda.synchronize()
