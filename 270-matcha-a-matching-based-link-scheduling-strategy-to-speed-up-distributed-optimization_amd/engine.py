@@ -253,7 +253,8 @@ class VirtualWorkerGroup:
     numel   -- arena width when no models are given (synthetic workloads / benchmarks).
     """
 
-    def __init__(self, topology, models=None, numel=None, *, rank=0, nranks=1, comm=None, adopt=True):
+    def __init__(self, topology, models=None, numel=None, *, rank=0, nranks=1, comm=None, adopt=True,
+                 chunk_cols=None):
         require_device()
         n = int(topology.size)
         blocks = partition(n, nranks)
@@ -278,8 +279,18 @@ class VirtualWorkerGroup:
             self.numel = int(numel)
         self.ld = (self.numel + ROW_ALIGN - 1) // ROW_ALIGN * ROW_ALIGN
         self.arena = torch.zeros((self.n_local, self.ld), dtype=torch.float32, device="cuda")
-        self.slab = (torch.empty((self.engine.max_remote, self.ld), dtype=torch.float32, device="cuda")
-                     if self.engine.max_remote else None)
+        # column pipelining of the cross-GPU exchange (N > 1): chunk c+1 travels over RCCL on a side
+        # stream while chunk c is mixed; the receive slab is two chunk-wide buffers
+        self.chunked = bool(self.engine.max_remote and chunk_cols and int(chunk_cols) < self.numel)
+        if self.chunked:
+            W = (int(chunk_cols) + ROW_ALIGN - 1) // ROW_ALIGN * ROW_ALIGN
+            self.chunk_w = W
+            self.chunks = [(c0, min(self.numel, c0 + W)) for c0 in range(0, self.numel, W)]
+            self.slab = torch.empty((2, self.engine.max_remote, W), dtype=torch.float32, device="cuda")
+            self.comm_stream = torch.cuda.Stream()
+        else:
+            self.slab = (torch.empty((self.engine.max_remote, self.ld), dtype=torch.float32, device="cuda")
+                         if self.engine.max_remote else None)
         if models is not None:
             for r, m in enumerate(models):
                 off = 0
@@ -292,11 +303,21 @@ class VirtualWorkerGroup:
                     if adopt:
                         p.data = view
                     off += k
-        slot_ptrs = [[self.arena[r].data_ptr()] for r in range(self.n_local)]
-        if self.slab is not None:
-            slot_ptrs += [[self.slab[k].data_ptr()] for k in range(self.engine.max_remote)]
-        self.layout = Layout([self.numel], slot_ptrs, self.engine.n_slots)
         self._row_ptrs = [self.arena[r].data_ptr() for r in range(self.n_local)]
+        if self.chunked:
+            self.chunk_layouts = []
+            for ci, (c0, c1) in enumerate(self.chunks):
+                buf = self.slab[ci % 2]
+                ptrs = [[p + 4 * c0] for p in self._row_ptrs]
+                ptrs += [[buf[k].data_ptr()] for k in range(self.engine.max_remote)]
+                self.chunk_layouts.append(Layout([c1 - c0], ptrs, self.engine.n_slots))
+            self.layout = Layout([self.numel], [[p] for p in self._row_ptrs] +
+                                 [[self.slab[0, 0].data_ptr()]] * self.engine.max_remote, self.engine.n_slots)
+        else:
+            slot_ptrs = [[p] for p in self._row_ptrs]
+            if self.slab is not None:
+                slot_ptrs += [[self.slab[k].data_ptr()] for k in range(self.engine.max_remote)]
+            self.layout = Layout([self.numel], slot_ptrs, self.engine.n_slots)
 
     @property
     def rows(self):
@@ -307,11 +328,34 @@ class VirtualWorkerGroup:
         """Enqueue round `it` (exchange + mix) on `stream`; returns False for an all-zero round."""
         if not self.engine.any_active[it]:
             return False
+        if self.chunked:
+            return self._step_chunked(it, stream)
         if self.engine.comm is not None:
             self.engine.exchange(it, self._row_ptrs,
                                  self.slab.data_ptr() if self.slab is not None else None,
                                  self.ld * 4, self.numel * 4, stream)
         self.engine.mix(it, self.layout, stream)
+        return True
+
+    def _step_chunked(self, it, stream=None):
+        cur = stream if stream is not None else torch.cuda.current_stream()
+        cs = self.comm_stream
+        start = torch.cuda.Event()
+        start.record(cur)
+        cs.wait_event(start)                 # rows are final (previous round, optimizer) before sending
+        mixed = [None, None]
+        for ci, (c0, c1) in enumerate(self.chunks):
+            b = ci % 2
+            if mixed[b] is not None:
+                cs.wait_event(mixed[b])      # slab buffer b is free once chunk ci-2 has been mixed
+            self.engine.exchange(it, [p + 4 * c0 for p in self._row_ptrs], self.slab[b].data_ptr(),
+                                 self.chunk_w * 4, (c1 - c0) * 4, cs)
+            arrived = torch.cuda.Event()
+            arrived.record(cs)
+            cur.wait_event(arrived)
+            self.engine.mix(it, self.chunk_layouts[ci], cur)
+            mixed[b] = torch.cuda.Event()
+            mixed[b].record(cur)
         return True
 
     def communicate(self):

@@ -84,21 +84,25 @@ class LoopbackComm:
         self.handle = None
 
     def exchange_round(self, engine, it, row_ptrs, slab_ptr, slab_ld_bytes, row_bytes):
+        """row_ptrs may point into the registered rows (column-chunked exchanges): the byte offset
+        from this rank's registered row 0 selects the same columns of every sender."""
         import torch
         torch.cuda.synchronize()
         hub = self.hub
-        hub.register(engine.row_base, row_ptrs)
+        if engine.row_base not in hub.live:
+            hub.register(engine.row_base, row_ptrs)
+        off = int(row_ptrs[0]) - hub.live[engine.row_base]
         for r, p in enumerate(row_ptrs):
-            w = engine.row_base + r
-            if (it, w) not in hub.snap:
+            key = (it, engine.row_base + r, off)
+            if key not in hub.snap:
                 t = torch.empty(row_bytes // 4, dtype=torch.float32, device="cuda")
                 hub.copy(t.data_ptr(), p, row_bytes)
-                hub.snap[(it, w)] = t
+                hub.snap[key] = t
         nrem = 0
         for kind, peer, idx, who in engine.exchange_plan(it):
             if kind == 1:
-                who = int(who)
-                src = hub.snap[(it, who)].data_ptr() if (it, who) in hub.snap else hub.live[who]
+                key = (it, int(who), off)
+                src = hub.snap[key].data_ptr() if key in hub.snap else hub.live[int(who)] + off
                 hub.copy(slab_ptr + int(idx) * slab_ld_bytes, src, row_bytes)
                 nrem += 1
         torch.cuda.synchronize()

@@ -330,8 +330,9 @@ def test_choco_vs_oracle_larger(pkg, O, P, ratio):
         assert np.array_equal(got.view(np.uint32), X.view(np.uint32)), f"round {t}"
 
 
-@pytest.mark.parametrize("gid,nranks", [(0, 2), (0, 4), (0, 8), (2, 4), (3, 3)])
-def test_multirank_pipeline_loopback(pkg, O, gid, nranks):
+@pytest.mark.parametrize("gid,nranks,chunk", [(0, 2, None), (0, 4, None), (0, 8, None), (2, 4, None),
+                                               (3, 3, None), (0, 8, 4096), (2, 4, 7000), (0, 2, 20_000)])
+def test_multirank_pipeline_loopback(pkg, O, gid, nranks, chunk):
     """N ranks' engines on one GPU with the loopback transport: owner tables, receive-slab slot
     numbering, native exchange order and the mixing kernel over local + slab rows, end to end,
     bit-exact vs the single-process oracle (the RCCL call itself is the only piece not run)."""
@@ -346,8 +347,9 @@ def test_multirank_pipeline_loopback(pkg, O, gid, nranks):
     flags[3] = 0
     topo = Topo(gp.neighbors_info, 0.17, flags)
     hub = LoopbackHub(nranks)
-    groups = [pkg.VirtualWorkerGroup(topo, numel=P, rank=r, nranks=nranks, comm=hub.comm(r))
+    groups = [pkg.VirtualWorkerGroup(topo, numel=P, rank=r, nranks=nranks, comm=hub.comm(r), chunk_cols=chunk)
               for r in range(nranks)]
+    assert all(g.chunked == bool(chunk and chunk < P and g.engine.max_remote) for g in groups)
     X = np.stack([O.synth(700 + i, P) for i in range(n)])
     for g in groups:
         g.rows.copy_(torch.from_numpy(X[g.row_base:g.row_base + g.n_local]))
