@@ -1,0 +1,177 @@
+// hbm_probe.hip -- HBM ceilings for the mixing kernel's access pattern on this box (tool, not product).
+//
+// Every variant moves the same bytes as one headline gossip round (8 rows x 25.6M fp32 read and
+// written = 1.6384 GB) so its time is directly comparable with mix_kernel:
+//   copy     dst = src, one 819 MB stream in, another out
+//   rmw1     x = a*x in place over one 819 MB buffer
+//   rmw8     8 rows of 102 MB updated in place, each lane loading the same column of all 8 rows
+//            before storing them (the mixing kernel's pattern, without the partner walk)
+//   read / write   half the bytes, one direction only (reported as GB/s of their own bytes)
+// Knobs per run: blocks per CU, non-temporal on/off, 16-byte accesses per lane per iteration (U).
+//   hipcc --offload-arch=gfx950 -O3 -o tools/hbm_probe tools/hbm_probe.hip && tools/hbm_probe
+#include <hip/hip_runtime.h>
+
+#include <stdio.h>
+#include <stdlib.h>
+#include <algorithm>
+#include <vector>
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+#define CK(x)                                                                          \
+    do {                                                                               \
+        hipError_t e = (x);                                                            \
+        if (e != hipSuccess) {                                                         \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+            exit(1);                                                                   \
+        }                                                                              \
+    } while (0)
+
+template <bool NT>
+__device__ __forceinline__ f4 ld(const f4* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st(f4* p, f4 v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+// n4 = number of float4; every lane handles U float4 per iteration, 256-lane tiles strided
+template <bool NT, int U>
+__global__ __launch_bounds__(256) void k_copy(const f4* __restrict__ s, f4* __restrict__ d, int64_t n4) {
+    const int64_t tile = 256 * U;
+    for (int64_t b = (int64_t)blockIdx.x * tile; b < n4; b += (int64_t)gridDim.x * tile) {
+        f4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = ld<NT>(s + b + u * 256 + threadIdx.x);
+#pragma unroll
+        for (int u = 0; u < U; ++u) st<NT>(d + b + u * 256 + threadIdx.x, v[u]);
+    }
+}
+
+template <bool NT, int U>
+__global__ __launch_bounds__(256) void k_rmw1(f4* __restrict__ x, int64_t n4, float a) {
+    const int64_t tile = 256 * U;
+    for (int64_t b = (int64_t)blockIdx.x * tile; b < n4; b += (int64_t)gridDim.x * tile) {
+        f4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = ld<NT>(x + b + u * 256 + threadIdx.x);
+#pragma unroll
+        for (int u = 0; u < U; ++u) st<NT>(x + b + u * 256 + threadIdx.x, v[u] * a);
+    }
+}
+
+// 8 rows of ld4 float4 each; lane loads its column of every row, then stores every row
+template <bool NT>
+__global__ __launch_bounds__(256) void k_rmw8(f4* __restrict__ x, int64_t ld4, float a) {
+    for (int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x; c < ld4; c += (int64_t)gridDim.x * 256) {
+        f4 v[8];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) v[r] = ld<NT>(x + r * ld4 + c);
+        f4 sum = v[0];
+#pragma unroll
+        for (int r = 1; r < 8; ++r) sum += v[r];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) st<NT>(x + r * ld4 + c, v[r] * a + sum * 1e-30f);
+    }
+}
+
+template <bool NT, int U>
+__global__ __launch_bounds__(256) void k_read(const f4* __restrict__ s, float* out, int64_t n4) {
+    const int64_t tile = 256 * U;
+    f4 acc = {0, 0, 0, 0};
+    for (int64_t b = (int64_t)blockIdx.x * tile; b < n4; b += (int64_t)gridDim.x * tile) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) acc += ld<NT>(s + b + u * 256 + threadIdx.x);
+    }
+    if (acc.x + acc.y + acc.z + acc.w == 1.2345f) out[0] = 1.0f;
+}
+
+template <bool NT, int U>
+__global__ __launch_bounds__(256) void k_write(f4* __restrict__ d, int64_t n4) {
+    const int64_t tile = 256 * U;
+    const f4 v = {1, 2, 3, 4};
+    for (int64_t b = (int64_t)blockIdx.x * tile; b < n4; b += (int64_t)gridDim.x * tile) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) st<NT>(d + b + u * 256 + threadIdx.x, v);
+    }
+}
+
+template <typename F>
+static float time_ms(F launch, int reps = 30) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int i = 0; i < 5; ++i) launch();
+    CK(hipDeviceSynchronize());
+    std::vector<float> t;
+    for (int i = 0; i < reps; ++i) {
+        CK(hipEventRecord(a, 0));
+        launch();
+        CK(hipEventRecord(b, 0));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        t.push_back(ms);
+    }
+    std::sort(t.begin(), t.end());
+    return t[t.size() / 2];
+}
+
+int main() {
+    int cus = 0;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    const int64_t P = 25600000, rows = 8;
+    const int64_t n4 = rows * P / 4;            // one 819.2 MB buffer in float4
+    const double round_bytes = 2.0 * rows * P * 4;
+    f4 *A, *B;
+    float* out;
+    CK(hipMalloc(&A, n4 * 16 + (int64_t)8 * 65536 * 16 * 2));
+    CK(hipMalloc(&B, n4 * 16));
+    CK(hipMalloc(&out, 64));
+    CK(hipMemset(A, 0, n4 * 16 + (int64_t)8 * 65536 * 16 * 2));
+    CK(hipMemset(B, 0, n4 * 16));
+    auto report = [&](const char* name, int bpc, int nt, int u, double bytes, float ms) {
+        printf("{\"kernel\": \"%s\", \"bpc\": %d, \"nt\": %d, \"U\": %d, \"us\": %.1f, \"TBps\": %.3f}\n",
+               name, bpc, nt, u, ms * 1e3, bytes / (ms * 1e-3) / 1e12);
+        fflush(stdout);
+    };
+    for (int bpc : {2, 4, 8}) {
+        if (getenv("PROBE_QUICK")) break;
+        const int grid = cus * bpc;
+#define RUN(NAME, NT, U, BYTES, ...) \
+    report(NAME, bpc, NT, U, BYTES, time_ms([&] { hipLaunchKernelGGL(__VA_ARGS__); }))
+        RUN("copy", 0, 1, round_bytes, (k_copy<false, 1>), dim3(grid), dim3(256), 0, 0, A, B, n4);
+        RUN("copy", 1, 1, round_bytes, (k_copy<true, 1>), dim3(grid), dim3(256), 0, 0, A, B, n4);
+        RUN("copy", 1, 4, round_bytes, (k_copy<true, 4>), dim3(grid), dim3(256), 0, 0, A, B, n4);
+        RUN("copy", 0, 4, round_bytes, (k_copy<false, 4>), dim3(grid), dim3(256), 0, 0, A, B, n4);
+        RUN("rmw1", 1, 1, round_bytes, (k_rmw1<true, 1>), dim3(grid), dim3(256), 0, 0, A, n4, 1.0f);
+        RUN("rmw1", 1, 4, round_bytes, (k_rmw1<true, 4>), dim3(grid), dim3(256), 0, 0, A, n4, 1.0f);
+        RUN("rmw1", 0, 4, round_bytes, (k_rmw1<false, 4>), dim3(grid), dim3(256), 0, 0, A, n4, 1.0f);
+        RUN("rmw8", 1, 8, round_bytes, (k_rmw8<true>), dim3(grid), dim3(256), 0, 0, A, P / 4, 1.0f);
+        RUN("rmw8", 0, 8, round_bytes, (k_rmw8<false>), dim3(grid), dim3(256), 0, 0, A, P / 4, 1.0f);
+        RUN("read", 1, 4, round_bytes / 2, (k_read<true, 4>), dim3(grid), dim3(256), 0, 0, A, out, n4);
+        RUN("read", 0, 4, round_bytes / 2, (k_read<false, 4>), dim3(grid), dim3(256), 0, 0, A, out, n4);
+        RUN("write", 1, 4, round_bytes / 2, (k_write<true, 4>), dim3(grid), dim3(256), 0, 0, B, n4);
+        RUN("write", 0, 4, round_bytes / 2, (k_write<false, 4>), dim3(grid), dim3(256), 0, 0, B, n4);
+#undef RUN
+    }
+    // rmw8 with padded row strides: does the distance between the 8 rows matter (channel mapping)?
+    for (int bpc : {3, 4, 5, 6}) {
+        const int grid = cus * bpc;
+        for (int64_t pad4 : {0, 16, 64, 192, 256, 1024, 4096 + 64, 65536 + 256}) {
+            const int64_t ld4 = P / 4 + pad4;
+            char name[64];
+            snprintf(name, sizeof(name), "rmw8_pad%lldB", (long long)(pad4 * 16));
+            report(name, bpc, 1, 8, round_bytes,
+                   time_ms([&] { hipLaunchKernelGGL((k_rmw8<true>), dim3(grid), dim3(256), 0, 0, A, ld4, 1.0f); }));
+        }
+        report("rmw1", bpc, 1, 1, round_bytes,
+               time_ms([&] { hipLaunchKernelGGL((k_rmw1<true, 1>), dim3(grid), dim3(256), 0, 0, A, n4, 1.0f); }));
+    }
+    report("hipMemcpyDtoD", 0, 0, 0, round_bytes,
+           time_ms([&] { CK(hipMemcpyAsync(B, A, n4 * 16, hipMemcpyDeviceToDevice, 0)); }));
+    return 0;
+}
