@@ -4,7 +4,7 @@ ChocoWorkerGroup keeps, for a block of workers on this GPU, the parameter arena 
 persistent Choco state x_hat and s (all [n_local, P] in HBM).  Per round:
     q_r = top-k(|x_r - x_hat_r|)            mx_topk_abs_diff   (prepare_comm_buffer, 175-196)
     [N > 1] RCCL exchange of the messages   mx_exchange_round  (12 k bytes per edge direction)
-    s / x_hat scatters + dense x update     mx_choco_apply     (averaging, 200-230)
+    s / x_hat updates + dense x update      mx_choco_apply     (averaging, 200-230; one fused pass)
 """
 import time
 
@@ -64,6 +64,8 @@ class ChocoWorkerGroup:
         self.msgs = torch.empty(self.engine.n_slots * self.msg_ld, dtype=torch.uint8, device="cuda")
         self.work_ld = int(lib.mx_topk_work_bytes(P))
         self.work = torch.empty(self.n_local * self.work_ld, dtype=torch.uint8, device="cuda")
+        self.apply_work = torch.empty(int(lib.mx_choco_apply_work_bytes(P, self.engine.n_slots)),
+                                      dtype=torch.uint8, device="cuda")
         self.gamma32 = float(np.float32(consensus_lr))
 
     @property
@@ -94,8 +96,9 @@ class ChocoWorkerGroup:
             self.engine.exchange(it, [mbase + r * self.msg_ld for r in range(self.n_local)],
                                  mbase + self.n_local * self.msg_ld, self.msg_ld, self.msg_bytes, stream)
         check(lib.mx_choco_apply(self.x.data_ptr(), self.x_hat.data_ptr(), self.s.data_ptr(), self.ld,
-                                 self.numel, self.k, mbase, self.msg_ld, self.engine.plan.data_ptr(), int(it),
-                                 self.n_local, self.engine.M, self.engine.alpha32, self.gamma32,
+                                 self.numel, self.k, mbase, self.msg_ld, self.engine.n_slots,
+                                 self.engine.plan.data_ptr(), int(it), self.n_local, self.engine.M,
+                                 self.engine.alpha32, self.gamma32, self.apply_work.data_ptr(),
                                  stream_ptr(stream)), "mx_choco_apply")
 
     def step(self, it, stream=None):

@@ -5,56 +5,65 @@
 // mx_choco_apply    = ChocoCommunicator.averaging (communicator.py:200-230)
 //
 // Top-k (k largest |x - x_hat|, ties at the threshold resolved towards the lowest indices,
-// output in index order) in THREE streaming passes over x / x_hat:
-//   A  hist_kernel     12-bit histogram of the magnitude key's top digit (bits 19..30: the
-//                      exponent + 4 mantissa bits) in LDS, non-zero bins flushed with atomics;
-//      select_top      one block finds the digit b0 holding the k-th largest key;
-//   B  split_kernel    per 4096-element chunk: count keys whose digit is above b0 (certainly
-//                      selected) and append the keys in digit b0 (candidates) to a side buffer
-//                      with wave-ballot compaction;
-//      cand_hist/select_cand (x2, 10 + 9 bits) finish the radix select on the candidates only,
-//      giving the exact threshold key T and how many of its ties are needed;
-//      cand_mark       per-chunk counts of candidates > T and == T (order-free atomics);
-//      scan_kernel     one block: per-chunk output offsets and tie ranks;
-//   C  write_kernel    per chunk, wave-ballot stable compaction of every key > T plus the
-//                      lowest-index ties, values = x - x_hat, indices int64.
+// output in index order) with ONE full streaming pass over x / x_hat:
+//   S  sample_kernel   12-bit histogram of the magnitude key's top digit (bits 19..30: exponent +
+//                      4 mantissa bits) over every S-th 1024-element piece (S = 1: all of them);
+//      select_lo       one block per row: the digit b_lo such that the sampled keys at or above it
+//                      cover k (S = 1: exactly the digit of the k-th largest key; S > 1: k scaled to
+//                      the sample, with a 25 % + 4 sigma margin);
+//   B  compact_kernel  THE full pass: one block per 4096-element chunk stores every key whose
+//                      digit is >= b_lo as (value, chunk-local index) into the chunk's own region,
+//                      in index order (wave scans + one barrier; no atomics);
+//      count_kernel    candidates per row; compact_kernel(fallback) re-runs with b_lo = 0 in the
+//                      (sample-dependent, rare) case that fewer than k were kept -- the result is
+//                      exact either way;
+//   C  cand_hist/select_cand (12 + 10 + 9 bits) radix-select the exact threshold key T and the
+//      number of its ties to take, over the candidates only; cand_mark counts > T / == T per
+//      chunk; scan_kernel turns them into output offsets; write_cand emits the selected
+//      candidates in index order (values = x - x_hat, int64 indices).
 // Everything stays on the device; no host round trip.  All local workers' rows are processed by
-// the same launches (blockIdx.y = row), so a round costs ~11 launches, not ~11 per worker.
+// the same launches (blockIdx.y = row).
 #include "mx_common.h"
 
 namespace {
 constexpr int kTPB = 256;
 constexpr int kWaves = kTPB / 64;
-constexpr int kChunk = 4096;                 // elements per chunk (4 quads of 4 per lane)
+constexpr int kSub = 1024;                   // elements per wave step = 4 quads x 64 lanes
+constexpr int kSubQuads = kSub / 4;
+constexpr int kChunk = kWaves * kSub;        // elements per chunk = one block (candidate region)
 constexpr int kTopBits = 12, kTopShift = 19;
 constexpr int kTopBins = 1 << kTopBits;
 constexpr int kMidBits = 10, kMidShift = 9;  // bits 9..18
 constexpr int kLowBits = 9;                  // bits 0..8
 constexpr int kScanTPB = 1024;
+constexpr int64_t kSampleTarget = 1 << 18;   // sampled elements per row (auto stride)
 
 struct SelState {
-    uint32_t b0;          // top digit of the threshold bin
+    uint32_t b0;          // lowest top digit kept as a candidate (b_lo)
     uint32_t T;           // exact threshold key (after the candidate passes)
     uint32_t prefix;      // candidate-pass prefix (bits fixed so far, shifted to full key)
     uint32_t mask;
     int64_t need;         // keys still to take at/below the current bin / prefix
-    int64_t cand_n;       // unused (candidates live in per-chunk regions)
+    int64_t cand_n;       // candidates kept by compact_kernel
 };
 
 struct WorkLayout {
-    size_t hist, state, cnt, off, cidx, ckey, total;
+    size_t hist, state, cnt, off, cval, cloc, total;
 };
 
+__host__ __device__ inline int64_t n_chunks(int64_t P) { return (P + kChunk - 1) / kChunk; }
+__host__ __device__ inline int64_t n_subs(int64_t P) { return (P + kSub - 1) / kSub; }
+
 __host__ __device__ inline WorkLayout layout(int64_t P) {
-    const int64_t nchunks = (P + kChunk - 1) / kChunk;
+    const int64_t nc = n_chunks(P);
     WorkLayout w;
     w.hist = 0;
     w.state = w.hist + sizeof(uint32_t) * kTopBins;
     w.cnt = w.state + 64;
-    w.off = w.cnt + sizeof(int64_t) * 4 * (size_t)nchunks;
-    w.cidx = (w.off + sizeof(int64_t) * 2 * (size_t)nchunks + 255) / 256 * 256;
-    w.ckey = w.cidx + sizeof(int64_t) * (size_t)P;
-    w.total = (w.ckey + sizeof(uint32_t) * (size_t)P + 255) / 256 * 256;
+    w.off = w.cnt + sizeof(int64_t) * 4 * (size_t)nc;
+    w.cval = (w.off + sizeof(int64_t) * 2 * (size_t)nc + 255) / 256 * 256;
+    w.cloc = w.cval + sizeof(float) * (size_t)nc * kChunk;
+    w.total = (w.cloc + sizeof(uint16_t) * (size_t)nc * kChunk + 255) / 256 * 256;
     return w;
 }
 
@@ -78,8 +87,8 @@ struct RowView {
     SelState* st;
     int64_t* cnt;
     int64_t* off;
-    int64_t* cidx;
-    uint32_t* ckey;
+    float* cval;
+    uint16_t* cloc;
     float* vals;
     int64_t* idx;
 };
@@ -95,8 +104,8 @@ __device__ __forceinline__ RowView row_view(const Rows& R) {
     v.st = reinterpret_cast<SelState*>(wb + w.state);
     v.cnt = reinterpret_cast<int64_t*>(wb + w.cnt);
     v.off = reinterpret_cast<int64_t*>(wb + w.off);
-    v.cidx = reinterpret_cast<int64_t*>(wb + w.cidx);
-    v.ckey = reinterpret_cast<uint32_t*>(wb + w.ckey);
+    v.cval = reinterpret_cast<float*>(wb + w.cval);
+    v.cloc = reinterpret_cast<uint16_t*>(wb + w.cloc);
     v.vals = reinterpret_cast<float*>(R.out + (int64_t)r * R.out_ld);
     v.idx = reinterpret_cast<int64_t*>(R.out + (int64_t)r * R.out_ld + R.idx_off);
     return v;
@@ -151,45 +160,59 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
-// ---- A: top-digit histogram
-__global__ __launch_bounds__(kTPB) void hist_kernel(Rows R) {
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// zero every row's top-digit histogram (one launch for the batch)
+__global__ __launch_bounds__(kTPB) void zero_hist(Rows R) {
+    const RowView v = row_view(R);
+    for (int i = threadIdx.x; i < kTopBins; i += kTPB) v.hist[i] = 0;
+}
+
+// ---- S: top-digit histogram over every S-th chunk, one wave per sampled chunk
+__global__ __launch_bounds__(kTPB) void sample_kernel(Rows R, int64_t S) {
     const RowView v = row_view(R);
     __shared__ uint32_t h[kTopBins];
     for (int i = threadIdx.x; i < kTopBins; i += kTPB) h[i] = 0;
     __syncthreads();
     const bool vec = (((uintptr_t)v.x | (uintptr_t)v.xh) & 15) == 0;
-    const int64_t nq = (R.P + 3) / 4;
-    constexpr int U = 4;                       // quads in flight per lane
-    const int64_t stride = (int64_t)gridDim.x * kTPB;
-    for (int64_t q0 = (int64_t)blockIdx.x * kTPB + threadIdx.x; q0 < nq; q0 += U * stride) {
-        float d[U][4];
-        int n[U];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t nsamp = (n_subs(R.P) + S - 1) / S;
+    for (int64_t u = (int64_t)blockIdx.x * kWaves + wave; u < nsamp; u += (int64_t)gridDim.x * kWaves) {
+        const int64_t q0 = u * S * kSubQuads;
+        float d[4][4];
+        int n[4];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t q = q0 + u * stride;
-            n[u] = q < nq ? load_quad(v.x, v.xh, q, R.P, vec, d[u]) : 0;
-        }
+        for (int j = 0; j < 4; ++j) n[j] = load_quad(v.x, v.xh, q0 + j * 64 + lane, R.P, vec, d[j]);
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
             for (int c = 0; c < 4; ++c)
-                if (c < n[u]) atomicAdd(&h[key_of(d[u][c]) >> kTopShift], 1u);
+                if (c < n[j]) atomicAdd(&h[key_of(d[j][c]) >> kTopShift], 1u);
     }
     __syncthreads();
     for (int i = threadIdx.x; i < kTopBins; i += kTPB)
         if (h[i]) atomicAdd(&v.hist[i], h[i]);
 }
 
-// one block: the bin holding the need-th largest count, scanning bins from the top.
-// bins/bin_shift describe the histogram; on exit st->need is the rank inside the chosen bin.
+// one block: the bin holding the need-th largest count, scanning bins from the top; bin 0 with
+// rank `need - total` when the histogram holds fewer than `need` keys.  Re-zeroes the histogram.
 template <int NBINS>
-__device__ void select_bin(uint32_t* __restrict__ hist, int64_t need, int* bin_out, int64_t* need_out) {
+__device__ void select_bin(uint32_t* __restrict__ hist, int64_t need, int* bin_out, int64_t* need_out,
+                           int64_t* total_out) {
     constexpr int kPer = NBINS / kTPB;
     __shared__ int64_t part[kTPB];
     const int t = threadIdx.x;
     int64_t mine = 0;
     for (int j = 0; j < kPer; ++j) mine += hist[NBINS - 1 - (t * kPer + j)];
     part[t] = mine;
+    if (t == 0) {
+        *bin_out = 0;
+        *need_out = need;
+    }
     __syncthreads();
     for (int off = 1; off < kTPB; off <<= 1) {          // inclusive scan from the top bins down
         const int64_t v = t >= off ? part[t - off] : 0;
@@ -198,6 +221,10 @@ __device__ void select_bin(uint32_t* __restrict__ hist, int64_t need, int* bin_o
         __syncthreads();
     }
     const int64_t before = part[t] - mine;
+    if (t == kTPB - 1) {
+        *total_out = part[t];
+        if (part[t] < need) *need_out = need - part[t];
+    }
     if (before < need && part[t] >= need) {
         int64_t acc = before;
         for (int j = 0; j < kPer; ++j) {
@@ -215,85 +242,108 @@ __device__ void select_bin(uint32_t* __restrict__ hist, int64_t need, int* bin_o
     for (int i = t; i < NBINS; i += kTPB) hist[i] = 0;     // ready for the next use
 }
 
-__global__ __launch_bounds__(kTPB) void select_top(Rows R) {
+// one block per row: b_lo from the (sampled) top-digit histogram
+__global__ __launch_bounds__(kTPB) void select_lo(Rows R, int64_t S, double frac) {
     const RowView v = row_view(R);
     SelState* st = v.st;
     __shared__ int bin;
-    __shared__ int64_t need;
-    select_bin<kTopBins>(v.hist, R.k, &bin, &need);
+    __shared__ int64_t need, total;
+    int64_t want = R.k;
+    if (S > 1) {
+        const double e = (double)R.k * frac;
+        want = (int64_t)ceil(1.25 * e + 4.0 * sqrt(e) + 16.0);
+    }
+    select_bin<kTopBins>(v.hist, want, &bin, &need, &total);
     __syncthreads();
     if (threadIdx.x == 0) {
-        st->b0 = (uint32_t)bin;
-        st->prefix = (uint32_t)bin << kTopShift;
-        st->mask = 0xffffffffu << kTopShift;
-        st->need = need;
+        st->b0 = total < want ? 0u : (uint32_t)bin;     // too few sampled keys: keep everything
+        st->prefix = 0;
+        st->mask = 0;
+        st->need = R.k;
         st->cand_n = 0;
         st->T = 0;
     }
 }
 
-// ---- B: per-chunk "certainly selected" counts + candidate compaction.  A chunk is 4 sub-tiles of
-// 256 lanes x one 16-byte quad; the 16 keys per lane stay in registers and a wave scan of the
-// per-lane candidate counts ranks them inside the chunk's OWN region of the candidate buffer
-// (chunk c owns slots [c*4096, c*4096 + ncand)), so no global atomics are needed.
-// cnt[4c + 0..3] = {keys above digit b0, candidates > T, candidates == T, candidates}.
-constexpr int kQuads = kChunk / (4 * kTPB);   // quads per lane per chunk
-
-__global__ __launch_bounds__(kTPB) void split_kernel(Rows R) {
+// ---- B: one block per chunk; keys with top digit >= b_lo -> (value, local index) in the chunk's
+// region, in index order (wave w, step j, lane l holds elements 4(c*1024 + 256w + 64j + l) .. +3).
+// cnt[4c + 0..3] = {0, candidates > T, candidates == T, candidates}.
+// fallback = 1: runs only if fewer than k candidates were kept, then keeps every key.
+__global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int fallback) {
     const RowView v = row_view(R);
-    const int64_t P = R.P;
-    __shared__ uint32_t wcand[kWaves], wabove[kWaves];
-    const uint32_t b0 = v.st->b0;
+    uint32_t b_lo = v.st->b0;
+    if (fallback) {
+        if (v.st->cand_n >= R.k) return;
+        b_lo = 0;
+    }
+    __shared__ uint32_t wtot[kWaves];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t c = blockIdx.x;
     const bool vec = (((uintptr_t)v.x | (uintptr_t)v.xh) & 15) == 0;
-    const int64_t q0 = (int64_t)blockIdx.x * (kChunk / 4);
-    uint32_t keys[kQuads][4];
-    uint32_t ccount = 0, above = 0;
+    const int64_t q0 = c * (kChunk / 4) + wave * kSubQuads;
+    float d[4][4];
+    uint32_t keep = 0;                           // bit 4j + e: element e of step j is kept
+    uint32_t incl[4], m[4];
+    uint32_t tot = 0;
 #pragma unroll
-    for (int j = 0; j < kQuads; ++j) {
-        float d[4];
-        const int n = load_quad(v.x, v.xh, q0 + (int64_t)j * kTPB + threadIdx.x, P, vec, d);
+    for (int j = 0; j < 4; ++j) {
+        const int n = load_quad(v.x, v.xh, q0 + j * 64 + lane, R.P, vec, d[j]);
+        m[j] = 0;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const bool in = c < n;
-            keys[j][c] = in ? key_of(d[c]) : 0xffffffffu;    // sentinel: never a candidate / above
-            const uint32_t dg = keys[j][c] >> kTopShift;
-            above += in && dg > b0;
-            ccount += in && dg == b0;
+        for (int e = 0; e < 4; ++e) {
+            const bool f = e < n && (key_of(d[j][e]) >> kTopShift) >= b_lo;
+            keep |= (f ? 1u : 0u) << (4 * j + e);
+            m[j] += f;
         }
+        incl[j] = wave_incl_scan(m[j]);
+        tot += __shfl(incl[j], 63, 64);
     }
-    const uint32_t incl = wave_incl_scan(ccount);
-    uint32_t ab = above;
-    for (int o = 32; o > 0; o >>= 1) ab += __shfl_xor(ab, o, 64);
-    if (lane == 63) wcand[wave] = incl;
-    if (lane == 0) wabove[wave] = ab;
+    if (lane == 0) wtot[wave] = tot;
     __syncthreads();
-    uint32_t pos = incl - ccount;
-    uint32_t tot = 0, a = 0;
+    uint32_t pos = 0, all = 0;
     for (int w = 0; w < kWaves; ++w) {
-        pos += (w < wave) ? wcand[w] : 0;
-        tot += wcand[w];
-        a += wabove[w];
+        pos += w < wave ? wtot[w] : 0;
+        all += wtot[w];
     }
-    if (threadIdx.x == 0) {
-        v.cnt[4 * blockIdx.x + 0] = a;
-        v.cnt[4 * blockIdx.x + 3] = tot;
-    }
-    const int64_t region = (int64_t)blockIdx.x * kChunk;
+    float* cv = v.cval + c * kChunk;
+    uint16_t* cl = v.cloc + c * kChunk;
 #pragma unroll
-    for (int j = 0; j < kQuads; ++j) {
+    for (int j = 0; j < 4; ++j) {
+        uint32_t p = pos + incl[j] - m[j];
 #pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            if ((keys[j][c] >> kTopShift) == b0 && keys[j][c] != 0xffffffffu) {
-                v.cidx[region + pos] = 4 * (q0 + (int64_t)j * kTPB + threadIdx.x) + c;
-                v.ckey[region + pos] = keys[j][c];
-                ++pos;
+        for (int e = 0; e < 4; ++e) {
+            if ((keep >> (4 * j + e)) & 1u) {
+                cv[p] = d[j][e];
+                cl[p] = (uint16_t)(kSub * wave + 4 * (64 * j + lane) + e);
+                ++p;
             }
         }
+        pos += __shfl(incl[j], 63, 64);
+    }
+    if (threadIdx.x == 0) {
+        v.cnt[4 * c + 0] = 0;
+        v.cnt[4 * c + 3] = all;
     }
 }
 
-// candidate histogram of `bits` bits at `shift`, restricted to keys matching st->prefix/mask
+// one block per row: total candidates
+__global__ __launch_bounds__(kScanTPB) void count_kernel(Rows R) {
+    const RowView v = row_view(R);
+    const int64_t nc = n_chunks(R.P);
+    __shared__ int64_t ws[kScanTPB / 64];
+    int64_t s = 0;
+    for (int64_t c = threadIdx.x; c < nc; c += kScanTPB) s += v.cnt[4 * c + 3];
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t t = 0;
+        for (int w = 0; w < kScanTPB / 64; ++w) t += ws[w];
+        v.st->cand_n = t;
+    }
+}
+
+// candidate histogram of `bits` bits at `shift`, restricted to keys matching st->prefix/mask;
 // one wave per chunk region; the block's LDS histogram is flushed once (few global atomics)
 template <int BITS>
 __global__ __launch_bounds__(kTPB) void cand_hist(Rows R, int shift) {
@@ -303,12 +353,12 @@ __global__ __launch_bounds__(kTPB) void cand_hist(Rows R, int shift) {
     for (int i = threadIdx.x; i < NB; i += kTPB) h[i] = 0;
     __syncthreads();
     const uint32_t prefix = v.st->prefix, mask = v.st->mask;
-    const int64_t nchunks = (R.P + kChunk - 1) / kChunk;
+    const int64_t nchunks = n_chunks(R.P);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int64_t c = (int64_t)blockIdx.x * kWaves + wave; c < nchunks; c += (int64_t)gridDim.x * kWaves) {
         const int64_t nc = v.cnt[4 * c + 3];
         for (int64_t i = lane; i < nc; i += 64) {
-            const uint32_t key = v.ckey[c * kChunk + i];
+            const uint32_t key = key_of(v.cval[c * kChunk + i]);
             if ((key & mask) == prefix) atomicAdd(&h[(key >> shift) & (NB - 1)], 1u);
         }
     }
@@ -320,12 +370,11 @@ __global__ __launch_bounds__(kTPB) void cand_hist(Rows R, int shift) {
 template <int BITS>
 __global__ __launch_bounds__(kTPB) void select_cand(Rows R, int shift) {
     const RowView v = row_view(R);
-    uint32_t* hist = v.hist;
     SelState* st = v.st;
     constexpr int NB = 1 << BITS;
     __shared__ int bin;
-    __shared__ int64_t need;
-    select_bin<NB>(hist, st->need, &bin, &need);
+    __shared__ int64_t need, total;
+    select_bin<NB>(v.hist, st->need, &bin, &need, &total);
     __syncthreads();
     if (threadIdx.x == 0) {
         st->prefix |= (uint32_t)bin << shift;
@@ -335,25 +384,22 @@ __global__ __launch_bounds__(kTPB) void select_cand(Rows R, int shift) {
     }
 }
 
-// per-chunk counts of candidates strictly above T and equal to T
 // one wave per chunk region: counts of candidates > T and == T, written without atomics
 __global__ __launch_bounds__(kTPB) void cand_mark(Rows R) {
     const RowView v = row_view(R);
     const uint32_t T = v.st->T;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t nchunks = (R.P + kChunk - 1) / kChunk;
+    const int64_t nchunks = n_chunks(R.P);
     for (int64_t c = (int64_t)blockIdx.x * kWaves + wave; c < nchunks; c += (int64_t)gridDim.x * kWaves) {
         const int64_t nc = v.cnt[4 * c + 3];
         uint32_t g = 0, e = 0;
         for (int64_t i = lane; i < nc; i += 64) {
-            const uint32_t key = v.ckey[c * kChunk + i];
+            const uint32_t key = key_of(v.cval[c * kChunk + i]);
             g += key > T;
             e += key == T;
         }
-        for (int o = 32; o > 0; o >>= 1) {
-            g += __shfl_xor(g, o, 64);
-            e += __shfl_xor(e, o, 64);
-        }
+        g = wave_sum(g);
+        e = wave_sum(e);
         if (lane == 0) {
             v.cnt[4 * c + 1] = g;
             v.cnt[4 * c + 2] = e;
@@ -365,7 +411,7 @@ __global__ __launch_bounds__(kTPB) void cand_mark(Rows R) {
 __global__ __launch_bounds__(kScanTPB) void scan_kernel(Rows R) {
     const RowView v = row_view(R);
     const int64_t* cnt = v.cnt;
-    const int64_t nchunks = (R.P + kChunk - 1) / kChunk;
+    const int64_t nchunks = n_chunks(R.P);
     const SelState* st = v.st;
     int64_t* off = v.off;
     __shared__ int64_t wsum_g[kScanTPB / 64], wsum_e[kScanTPB / 64];
@@ -400,132 +446,169 @@ __global__ __launch_bounds__(kScanTPB) void scan_kernel(Rows R) {
     }
 }
 
-// ---- C: stable per-chunk compaction in index order.  In sub-tile j lane l holds elements
-// 4(q0 + j*256 + l) .. +3, so index order is lane-major: a wave scan of per-lane counts (0..4)
-// plus the per-wave totals in LDS rank every tie and every selected element.
-__global__ __launch_bounds__(kTPB) void write_kernel(Rows R) {
+// ---- C: one wave per chunk region: the candidates are already in index order, so a wave scan
+// of the tie flags ranks the ties and a wave scan of the selection flags places the output.
+__global__ __launch_bounds__(kTPB) void write_cand(Rows R) {
     const RowView v = row_view(R);
-    const int64_t P = R.P;
-    __shared__ uint32_t weq[2][kWaves], wsel[2][kWaves];
     const uint32_t T = v.st->T;
     const int64_t need_eq = v.st->need;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const bool vec = (((uintptr_t)v.x | (uintptr_t)v.xh) & 15) == 0;
-    const int64_t q0 = (int64_t)blockIdx.x * (kChunk / 4);
-    int64_t run_out = v.off[2 * blockIdx.x], run_eq = v.off[2 * blockIdx.x + 1];
-    for (int j = 0; j < kQuads; ++j) {
-        const int par = j & 1;
-        const int64_t q = q0 + (int64_t)j * kTPB + threadIdx.x;
-        float d[4];
-        const int n = load_quad(v.x, v.xh, q, P, vec, d);
-        uint32_t key[4];
-        uint32_t ne = 0;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            key[c] = key_of(d[c]);
-            ne += (c < n) && key[c] == T;
+    const int64_t c = (int64_t)blockIdx.x * kWaves + wave;
+    if (c >= n_chunks(R.P)) return;
+    const int64_t nc = v.cnt[4 * c + 3];
+    int64_t run_out = v.off[2 * c], run_eq = v.off[2 * c + 1];
+    for (int64_t i0 = 0; i0 < nc; i0 += 64) {
+        const int64_t i = i0 + lane;
+        const bool in = i < nc;
+        const float d = in ? v.cval[c * kChunk + i] : 0.0f;
+        const uint32_t key = key_of(d);
+        const bool eq = in && key == T;
+        const uint32_t einc = wave_incl_scan(eq ? 1u : 0u);
+        const bool sel = in && (key > T || (eq && run_eq + (int64_t)einc - 1 < need_eq));
+        const uint32_t sinc = wave_incl_scan(sel ? 1u : 0u);
+        if (sel) {
+            const int64_t pos = run_out + sinc - 1;
+            v.vals[pos] = d;
+            v.idx[pos] = c * kChunk + v.cloc[c * kChunk + i];
         }
-        const uint32_t einc = wave_incl_scan(ne);
-        if (lane == 63) weq[par][wave] = einc;
-        __syncthreads();
-        uint32_t epre = 0, etot = 0;
-        for (int w = 0; w < kWaves; ++w) {
-            epre += (w < wave) ? weq[par][w] : 0;
-            etot += weq[par][w];
-        }
-        int64_t er = run_eq + epre + (einc - ne);
-        bool sel[4];
-        uint32_t ns = 0;
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            const bool in = c < n;
-            const bool eq = in && key[c] == T;
-            sel[c] = in && (key[c] > T || (eq && er < need_eq));
-            er += eq;
-            ns += sel[c];
-        }
-        const uint32_t sinc = wave_incl_scan(ns);
-        if (lane == 63) wsel[par][wave] = sinc;
-        __syncthreads();
-        uint32_t spre = 0, stot = 0;
-        for (int w = 0; w < kWaves; ++w) {
-            spre += (w < wave) ? wsel[par][w] : 0;
-            stot += wsel[par][w];
-        }
-        int64_t pos = run_out + spre + (sinc - ns);
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            if (sel[c]) {
-                v.vals[pos] = d[c];
-                v.idx[pos] = 4 * q + c;
-                ++pos;
-            }
-        }
-        run_out += stot;
-        run_eq += etot;
+        run_out += __shfl(sinc, 63, 64);
+        run_eq += __shfl(einc, 63, 64);
     }
 }
 
 // ------------------------------------------------------------------------------- apply
-// partner position e: s_r[idx_j] = s_r[idx_j] + f32(alpha) * v_j for rows with degree > e
-__global__ __launch_bounds__(kTPB) void scatter_partner_kernel(float* __restrict__ s, int64_t ld,
-                                                               const char* __restrict__ msgs,
-                                                               int64_t msg_ld, int64_t kpad, int64_t k,
-                                                               const int32_t* __restrict__ rec,
-                                                               int n_local, int M, int e, float alpha) {
-    const int r = blockIdx.y;
-    const int32_t* deg = rec + mx::kPlanHeader;
-    if (deg[r] <= e) return;
-    const int slot = deg[2 * n_local + r * M + e];
-    const float* v = reinterpret_cast<const float*>(msgs + (int64_t)slot * msg_ld);
-    const int64_t* ix = reinterpret_cast<const int64_t*>(msgs + (int64_t)slot * msg_ld + 4 * kpad);
-    float* sr = s + (int64_t)r * ld;
-    for (int64_t q = (int64_t)blockIdx.x * kTPB + threadIdx.x; q < k; q += (int64_t)gridDim.x * kTPB) {
-        const int64_t c = ix[q];
-        sr[c] = __fadd_rn(sr[c], __fmul_rn(alpha, v[q]));
+// ChocoCommunicator.averaging (communicator.py:200-230) fused into one pass per state tile.
+// Row r's tile [t0, t0 + kTile) of s and x_hat is staged in LDS; every message that touches the
+// tile is applied there in the reference order (partners in matching order, then the own
+// message), then the dense update x = fma(-g, x_hat, fma(g, s, x)) streams x through once and
+// only the 64-byte granules of s / x_hat that a message touched are written back.  Per element
+// the rounding sequence is exactly the reference's; HBM traffic is x read + written, s and
+// x_hat read once, their dirty granules written, and the messages read once.
+//
+// Messages are index-sorted, so the entries of message `slot` inside tile t are the range
+// [bnd[slot][t], bnd[slot][t+1]) (bounds_kernel: a linear pass over the index arrays).
+constexpr int kTile = 4096;                    // elements per apply tile (16 KB of s + 16 KB of x_hat)
+constexpr int kGran = 16;                      // floats per dirty granule (64 B)
+
+__host__ __device__ inline int64_t n_tiles(int64_t P) { return (P + kTile - 1) / kTile; }
+
+struct Msg {
+    const float* v;
+    const int64_t* ix;
+};
+
+__device__ __forceinline__ Msg msg_at(const char* msgs, int64_t msg_ld, int64_t kpad, int slot) {
+    const char* b = msgs + (int64_t)slot * msg_ld;
+    return Msg{reinterpret_cast<const float*>(b), reinterpret_cast<const int64_t*>(b + 4 * kpad)};
+}
+
+// bnd[slot][t] = first entry of message `slot` with index >= t * kTile, for t in [0, ntiles];
+// only the slots this round uses (local rows + its received messages; others may hold stale
+// bytes -- the tile numbers are clamped anyway so nothing is written out of range)
+__device__ __forceinline__ int64_t tile_of(int64_t i, int64_t ntiles) {
+    const int64_t t = i < 0 ? -1 : i / kTile;
+    return t < ntiles ? t : ntiles;
+}
+
+__global__ __launch_bounds__(kTPB) void bounds_kernel(const char* __restrict__ msgs, int64_t msg_ld,
+                                                      int64_t kpad, int64_t k, int64_t ntiles,
+                                                      const int32_t* __restrict__ rec, int n_local,
+                                                      int32_t* __restrict__ bnd) {
+    const int slot = blockIdx.y;
+    if (slot >= n_local + rec[1]) return;
+    const Msg m = msg_at(msgs, msg_ld, kpad, slot);
+    int32_t* b = bnd + (int64_t)slot * (ntiles + 1);
+    for (int64_t q = (int64_t)blockIdx.x * kTPB + threadIdx.x; q <= k; q += (int64_t)gridDim.x * kTPB) {
+        const int64_t prev = q == 0 ? -1 : tile_of(m.ix[q - 1], ntiles);
+        const int64_t cur = q == k ? ntiles : tile_of(m.ix[q], ntiles);
+        for (int64_t t = prev + 1; t <= cur; ++t) b[t] = (int32_t)q;
     }
 }
 
-// own message: s_r[idx_r] += f32(1 - d alpha) v_r ; x_hat_r[idx_r] += v_r
-__global__ __launch_bounds__(kTPB) void scatter_self_kernel(float* __restrict__ s, float* __restrict__ xh,
-                                                            int64_t ld, const char* __restrict__ msgs,
-                                                            int64_t msg_ld, int64_t kpad, int64_t k,
-                                                            const int32_t* __restrict__ rec, int n_local) {
+__global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, float* __restrict__ xh,
+                                                     float* __restrict__ s, int64_t ld, int64_t P,
+                                                     const char* __restrict__ msgs, int64_t msg_ld,
+                                                     int64_t kpad, int64_t ntiles,
+                                                     const int32_t* __restrict__ bnd,
+                                                     const int32_t* __restrict__ rec, int n_local, int M,
+                                                     float alpha, float g) {
+    __shared__ float ls[kTile], lh[kTile];
+    __shared__ uint8_t ds[kTile / kGran], dh[kTile / kGran];
     const int r = blockIdx.y;
-    const float sw = __int_as_float(rec[mx::kPlanHeader + n_local + r]);
-    const float* v = reinterpret_cast<const float*>(msgs + (int64_t)r * msg_ld);
-    const int64_t* ix = reinterpret_cast<const int64_t*>(msgs + (int64_t)r * msg_ld + 4 * kpad);
-    float* sr = s + (int64_t)r * ld;
-    float* hr = xh + (int64_t)r * ld;
-    for (int64_t q = (int64_t)blockIdx.x * kTPB + threadIdx.x; q < k; q += (int64_t)gridDim.x * kTPB) {
-        const int64_t c = ix[q];
-        const float vq = v[q];
-        sr[c] = __fadd_rn(sr[c], __fmul_rn(sw, vq));
-        hr[c] = __fadd_rn(hr[c], vq);
-    }
-}
-
-// x = fma(g, s, x); x = fma(-g, x_hat, x)  (communicator.py:225), 16-byte lanes
-__global__ __launch_bounds__(kTPB) void dense_kernel(float* __restrict__ x, const float* __restrict__ s,
-                                                     const float* __restrict__ xh, int64_t ld, int64_t P,
-                                                     float g) {
-    const int r = blockIdx.y;
-    float* xr = x + (int64_t)r * ld;
-    const float* sr = s + (int64_t)r * ld;
-    const float* hr = xh + (int64_t)r * ld;
-    const bool vec = (((uintptr_t)xr | (uintptr_t)sr | (uintptr_t)hr) & 15) == 0;
-    const int64_t nv = vec ? P / 4 : 0;
-    typedef float f4 __attribute__((ext_vector_type(4)));
-    for (int64_t q = (int64_t)blockIdx.x * kTPB + threadIdx.x; q < nv; q += (int64_t)gridDim.x * kTPB) {
-        f4 a = __builtin_nontemporal_load(reinterpret_cast<const f4*>(xr) + q);
-        const f4 b = __builtin_nontemporal_load(reinterpret_cast<const f4*>(sr) + q);
-        const f4 c = __builtin_nontemporal_load(reinterpret_cast<const f4*>(hr) + q);
+    const int64_t t = blockIdx.x;
+    const int64_t t0 = t * kTile;
+    const int len = (int)(P - t0 < kTile ? P - t0 : kTile);
+    float* xr = x + (int64_t)r * ld + t0;
+    float* sr = s + (int64_t)r * ld + t0;
+    float* hr = xh + (int64_t)r * ld + t0;
+    const int tid = threadIdx.x;
+    const bool vec = len == kTile && (((uintptr_t)xr | (uintptr_t)sr | (uintptr_t)hr) & 15) == 0;
+    constexpr int kQ = kTile / 4 / kTPB;       // quads per lane
+    if (vec) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) a[j] = __builtin_fmaf(-g, c[j], __builtin_fmaf(g, b[j], a[j]));
-        __builtin_nontemporal_store(a, reinterpret_cast<f4*>(xr) + q);
+        for (int j = 0; j < kQ; ++j) {
+            const int q = j * kTPB + tid;
+            reinterpret_cast<f4*>(ls)[q] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(sr) + q);
+            reinterpret_cast<f4*>(lh)[q] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(hr) + q);
+        }
+    } else {
+        for (int i = tid; i < len; i += kTPB) {
+            ls[i] = sr[i];
+            lh[i] = hr[i];
+        }
     }
-    for (int64_t i = nv * 4 + (int64_t)blockIdx.x * kTPB + threadIdx.x; i < P; i += (int64_t)gridDim.x * kTPB)
-        xr[i] = __builtin_fmaf(-g, hr[i], __builtin_fmaf(g, sr[i], xr[i]));
+    for (int i = tid; i < kTile / kGran; i += kTPB) ds[i] = dh[i] = 0;
+    __syncthreads();
+    const int32_t* deg = rec + mx::kPlanHeader;
+    const int d = deg[r];
+    const int32_t* src = deg + 2 * n_local + r * M;
+    for (int e = 0; e < d; ++e) {              // partners, ascending matching order
+        const int slot = src[e];
+        const Msg m = msg_at(msgs, msg_ld, kpad, slot);
+        const int32_t* b = bnd + (int64_t)slot * (ntiles + 1);
+        const int lo = b[t], hi = b[t + 1];
+        for (int q = lo + tid; q < hi; q += kTPB) {
+            const int c = (int)(m.ix[q] - t0);
+            ls[c] = __fadd_rn(ls[c], __fmul_rn(alpha, m.v[q]));
+            ds[c / kGran] = 1;
+        }
+        __syncthreads();                       // a later message may touch the same element
+    }
+    {                                          // own message
+        const float sw = __int_as_float(deg[n_local + r]);
+        const Msg m = msg_at(msgs, msg_ld, kpad, r);
+        const int32_t* b = bnd + (int64_t)r * (ntiles + 1);
+        const int lo = b[t], hi = b[t + 1];
+        for (int q = lo + tid; q < hi; q += kTPB) {
+            const int c = (int)(m.ix[q] - t0);
+            const float vq = m.v[q];
+            ls[c] = __fadd_rn(ls[c], __fmul_rn(sw, vq));
+            lh[c] = __fadd_rn(lh[c], vq);
+            ds[c / kGran] = 1;
+            dh[c / kGran] = 1;
+        }
+    }
+    __syncthreads();
+    if (vec) {
+#pragma unroll
+        for (int j = 0; j < kQ; ++j) {
+            const int q = j * kTPB + tid;
+            f4 a = __builtin_nontemporal_load(reinterpret_cast<const f4*>(xr) + q);
+            const f4 sv = reinterpret_cast<const f4*>(ls)[q];
+            const f4 hv = reinterpret_cast<const f4*>(lh)[q];
+#pragma unroll
+            for (int c = 0; c < 4; ++c) a[c] = __builtin_fmaf(-g, hv[c], __builtin_fmaf(g, sv[c], a[c]));
+            __builtin_nontemporal_store(a, reinterpret_cast<f4*>(xr) + q);
+            if (ds[q / (kGran / 4)]) __builtin_nontemporal_store(sv, reinterpret_cast<f4*>(sr) + q);
+            if (dh[q / (kGran / 4)]) __builtin_nontemporal_store(hv, reinterpret_cast<f4*>(hr) + q);
+        }
+    } else {
+        for (int i = tid; i < len; i += kTPB) {
+            xr[i] = __builtin_fmaf(-g, lh[i], __builtin_fmaf(g, ls[i], xr[i]));
+            if (ds[i / kGran]) sr[i] = ls[i];
+            if (dh[i / kGran]) hr[i] = lh[i];
+        }
+    }
 }
 
 unsigned clamp_grid(int64_t n, int64_t per, int64_t cap) {
@@ -536,9 +619,36 @@ unsigned clamp_grid(int64_t n, int64_t per, int64_t cap) {
 }
 }  // namespace
 
+int g_sample_stride = 0;   // 0 = auto (about kSampleTarget sampled elements per row)
+
+int64_t sample_stride(int64_t P) {
+    const int64_t nc = n_chunks(P);
+    int64_t S = g_sample_stride > 0 ? g_sample_stride : (nc * kChunk) / kSampleTarget;
+    const int64_t ns = n_subs(P);
+    if (S < 1) S = 1;
+    if (S > ns) S = ns;
+    return S;
+}
+
 extern "C" size_t mx_topk_work_bytes(int64_t P) { return layout(P < 1 ? 1 : P).total; }
 
 extern "C" int64_t mx_choco_msg_bytes(int64_t k) { return 4 * ((k + 1) / 2 * 2) + 8 * k; }
+
+extern "C" int mx_topk_set(const char* key, int64_t value) {
+    MX_CHECK(key, "mx_topk_set: null key");
+    if (!strcmp(key, "sample_stride")) {
+        MX_CHECK(value >= 0, "mx_topk_set: sample_stride %lld", (long long)value);
+        g_sample_stride = (int)value;
+        return MX_OK;
+    }
+    MX_CHECK(false, "mx_topk_set: unknown key '%s'", key);
+}
+
+extern "C" int64_t mx_topk_get(const char* key) {
+    if (key && !strcmp(key, "sample_stride")) return g_sample_stride;
+    mx::set_error("mx_topk_get: unknown key '%s'", key ? key : "(null)");
+    return MX_ERR_INVALID;
+}
 
 extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t ld, int nrows, int64_t P,
                                      int64_t k, void* out, int64_t out_ld_bytes, int64_t idx_off_bytes,
@@ -549,37 +659,47 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
     MX_CHECK(((uintptr_t)(static_cast<char*>(out) + idx_off_bytes)) % 8 == 0 && (nrows == 1 || out_ld_bytes % 8 == 0),
              "mx_topk_abs_diff_rows: int64 index output must be 8-byte aligned");
     MX_CHECK(work_ld_bytes >= (int64_t)layout(P).total || nrows == 1, "mx_topk_abs_diff_rows: work_ld too small");
+    MX_CHECK(((uintptr_t)work) % 256 == 0 && (nrows == 1 || work_ld_bytes % 256 == 0),
+             "mx_topk_abs_diff_rows: work must be 256-byte aligned");
     hipStream_t st = mx::as_stream(stream);
     Rows R{x, x_hat, ld, static_cast<char*>(out), out_ld_bytes, idx_off_bytes, static_cast<char*>(work),
            work_ld_bytes, P, k};
-    const WorkLayout w = layout(P);
-    for (int r = 0; r < nrows; ++r)
-        MX_HIP(hipMemsetAsync(static_cast<char*>(work) + (int64_t)r * work_ld_bytes + w.hist, 0,
-                              sizeof(uint32_t) * kTopBins, st));
-    const unsigned nchunks = (unsigned)((P + kChunk - 1) / kChunk);
-    const unsigned hgrid = clamp_grid(P, (int64_t)kTPB * 64, (512 + nrows - 1) / nrows);
-    const unsigned cgrid = clamp_grid((P + kChunk - 1) / kChunk, kWaves, (1024 + nrows - 1) / nrows);
+    const int64_t nc = n_chunks(P);
+    const int64_t S = sample_stride(P);
+    const int64_t nsamp = (n_subs(P) + S - 1) / S;
+    int64_t sampled = 0;                      // elements in the sampled pieces
+    for (int64_t u = 0; u < nsamp; ++u) {
+        const int64_t c0 = u * S * kSub;
+        sampled += (P - c0 < kSub) ? P - c0 : kSub;
+    }
+    const double frac = (double)sampled / (double)P;
+    MX_CHECK(nc <= 0x7fffffff, "mx_topk_abs_diff_rows: P too large");
+    const unsigned bgrid = (unsigned)nc;                                       // one block per chunk
+    const unsigned wgrid = (unsigned)((nc + kWaves - 1) / kWaves);          // one wave per chunk
+    const unsigned sgrid = clamp_grid(nsamp, 4 * kWaves, (1024 + nrows - 1) / nrows);
+    const unsigned cgrid = clamp_grid(wgrid, 2, (2048 + nrows - 1) / nrows);
     const dim3 one(1, nrows);
-    hipLaunchKernelGGL(hist_kernel, dim3(hgrid, nrows), dim3(kTPB), 0, st, R);
-    MX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(select_top, one, dim3(kTPB), 0, st, R);
-    MX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(split_kernel, dim3(nchunks, nrows), dim3(kTPB), 0, st, R);
-    MX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(cand_hist<kMidBits>, dim3(cgrid, nrows), dim3(kTPB), 0, st, R, kMidShift);
-    MX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(select_cand<kMidBits>, one, dim3(kTPB), 0, st, R, kMidShift);
-    MX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(cand_hist<kLowBits>, dim3(cgrid, nrows), dim3(kTPB), 0, st, R, 0);
-    MX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(select_cand<kLowBits>, one, dim3(kTPB), 0, st, R, 0);
-    MX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(cand_mark, dim3(cgrid, nrows), dim3(kTPB), 0, st, R);
-    MX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(scan_kernel, one, dim3(kScanTPB), 0, st, R);
-    MX_LAUNCH_CHECK();
-    hipLaunchKernelGGL(write_kernel, dim3(nchunks, nrows), dim3(kTPB), 0, st, R);
-    MX_LAUNCH_CHECK();
+#define MX_L(kern, grid, tpb, ...)                                                 \
+    hipLaunchKernelGGL(kern, grid, dim3(tpb), 0, st, R, ##__VA_ARGS__);            \
+    MX_LAUNCH_CHECK()
+    MX_L(zero_hist, one, kTPB);
+    MX_L(sample_kernel, dim3(sgrid, nrows), kTPB, S);
+    MX_L(select_lo, one, kTPB, S, frac);
+    MX_L(compact_kernel, dim3(bgrid, nrows), kTPB, 0);
+    if (S > 1) {
+        MX_L(count_kernel, one, kScanTPB);
+        MX_L(compact_kernel, dim3(bgrid, nrows), kTPB, 1);
+    }
+    MX_L(cand_hist<kTopBits>, dim3(cgrid, nrows), kTPB, kTopShift);
+    MX_L(select_cand<kTopBits>, one, kTPB, kTopShift);
+    MX_L(cand_hist<kMidBits>, dim3(cgrid, nrows), kTPB, kMidShift);
+    MX_L(select_cand<kMidBits>, one, kTPB, kMidShift);
+    MX_L(cand_hist<kLowBits>, dim3(cgrid, nrows), kTPB, 0);
+    MX_L(select_cand<kLowBits>, one, kTPB, 0);
+    MX_L(cand_mark, dim3(cgrid, nrows), kTPB);
+    MX_L(scan_kernel, one, kScanTPB);
+    MX_L(write_cand, dim3(wgrid, nrows), kTPB);
+#undef MX_L
     return MX_OK;
 }
 
@@ -590,31 +710,33 @@ extern "C" int mx_topk_abs_diff(const float* x, const float* x_hat, int64_t P, i
     return mx_topk_abs_diff_rows(x, x_hat, P, 1, P, k, vals, 0, idx_off, work, 0, stream);
 }
 
+extern "C" size_t mx_choco_apply_work_bytes(int64_t P, int n_slots) {
+    return sizeof(int32_t) * (size_t)(n_tiles(P < 1 ? 1 : P) + 1) * (size_t)(n_slots < 1 ? 1 : n_slots);
+}
+
 extern "C" int mx_choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t k,
-                              const void* msgs, int64_t msg_ld_bytes, const int32_t* plan_dev,
-                              int64_t iter, int n_local, int M, float alpha, float gamma,
+                              const void* msgs, int64_t msg_ld_bytes, int n_slots, const int32_t* plan_dev,
+                              int64_t iter, int n_local, int M, float alpha, float gamma, void* work,
                               void* stream) {
-    MX_CHECK(x && xhat && s && msgs && plan_dev, "mx_choco_apply: null pointer");
-    MX_CHECK(P >= 1 && k >= 1 && k <= P && ld >= P, "mx_choco_apply: P=%lld k=%lld ld=%lld",
+    MX_CHECK(x && xhat && s && msgs && plan_dev && work, "mx_choco_apply: null pointer");
+    MX_CHECK(P >= 1 && k >= 1 && k <= P && ld >= P && k < (int64_t)1 << 31, "mx_choco_apply: P=%lld k=%lld ld=%lld",
              (long long)P, (long long)k, (long long)ld);
-    MX_CHECK(n_local >= 1 && n_local <= 65535 && M >= 1, "mx_choco_apply: n_local=%d M=%d", n_local, M);
+    MX_CHECK(n_local >= 1 && n_local <= 65535 && n_slots >= n_local && n_slots <= 65535 && M >= 1,
+             "mx_choco_apply: n_local=%d n_slots=%d M=%d", n_local, n_slots, M);
     const int64_t kpad = (k + 1) / 2 * 2;
     MX_CHECK(msg_ld_bytes >= 4 * kpad + 8 * k && msg_ld_bytes % 8 == 0, "mx_choco_apply: msg_ld %lld",
              (long long)msg_ld_bytes);
     hipStream_t st = mx::as_stream(stream);
     const int32_t* rec = plan_dev + iter * mx::plan_words(n_local, M);
-    const unsigned sgrid = clamp_grid(k, kTPB * 4, 1024);
-    for (int e = 0; e < M; ++e) {
-        hipLaunchKernelGGL(scatter_partner_kernel, dim3(sgrid, n_local), dim3(kTPB), 0, st, s, ld,
-                           static_cast<const char*>(msgs), msg_ld_bytes, kpad, k, rec, n_local, M, e, alpha);
-        MX_LAUNCH_CHECK();
-    }
-    hipLaunchKernelGGL(scatter_self_kernel, dim3(sgrid, n_local), dim3(kTPB), 0, st, s, xhat, ld,
-                       static_cast<const char*>(msgs), msg_ld_bytes, kpad, k, rec, n_local);
+    const int64_t nt = n_tiles(P);
+    int32_t* bnd = static_cast<int32_t*>(work);
+    const char* m = static_cast<const char*>(msgs);
+    hipLaunchKernelGGL(bounds_kernel, dim3(clamp_grid(k + 1, kTPB * 4, 1024), n_slots), dim3(kTPB), 0, st, m,
+                       msg_ld_bytes, kpad, k, nt, rec, n_local, bnd);
     MX_LAUNCH_CHECK();
-    const unsigned dgrid = clamp_grid(P, kTPB * 16, 2048);
-    hipLaunchKernelGGL(dense_kernel, dim3(dgrid, n_local), dim3(kTPB), 0, st, x, (const float*)s,
-                       (const float*)xhat, ld, P, gamma);
+    MX_CHECK(nt <= 0x7fffffff, "mx_choco_apply: P too large");
+    hipLaunchKernelGGL(apply_kernel, dim3((unsigned)nt, n_local), dim3(kTPB), 0, st, x, xhat, s, ld, P, m,
+                       msg_ld_bytes, kpad, nt, (const int32_t*)bnd, rec, n_local, M, alpha, gamma);
     MX_LAUNCH_CHECK();
     return MX_OK;
 }

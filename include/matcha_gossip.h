@@ -125,9 +125,17 @@ int mx_scatter(float* const* ptrs_dev, const int64_t* off_dev, int nseg, int64_t
  * Writes vals[k] = (x - x_hat)[idx] and idx[k] (int64) sorted by index.  Among equal
  * magnitudes at the k-th threshold the lowest indices are taken (torch.topk(sorted=False)
  * leaves that unspecified).  x_hat may be NULL (treated as zeros: get_top_k on x itself).
- * `work` is a device scratch of mx_topk_work_bytes(P) bytes.
+ * `work` is a 256-byte aligned device scratch of mx_topk_work_bytes(P) bytes.
+ * One full pass over x / x_hat: a sampled top-digit histogram picks a candidate floor, one
+ * streaming pass keeps the keys above it, and the exact radix select runs on those only (a
+ * too-high floor is detected on the device and the pass re-run keeping every key: the result
+ * is exact in every case).
  */
 size_t mx_topk_work_bytes(int64_t P);
+/* Top-k knobs: "sample_stride" = sample every S-th 1024-element chunk for the candidate floor
+ * (0 = auto, about 2^18 sampled elements per row; 1 = exact full histogram, no sampling). */
+int mx_topk_set(const char* key, int64_t value);
+int64_t mx_topk_get(const char* key);
 int mx_topk_abs_diff(const float* x, const float* x_hat, int64_t P, int64_t k, float* vals,
                      int64_t* idx, void* work, void* stream);
 /* Batched form (one set of launches for every local worker): row r reads x + r*ld (and
@@ -147,11 +155,18 @@ int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t ld, int nr
  *   msgs      compressed messages, one per plan slot, msg_ld_bytes apart: slot k holds
  *             vals float[k] at +0 and idx int64[k] at +4*round_up(k, 2) (mx_choco_msg_bytes);
  *             slots [0, n_local) are the local rows' own messages, the rest received ones
+ *   work      device scratch of mx_choco_apply_work_bytes(P, n_slots) bytes
+ * One fused pass: per 4096-element tile of a row, s and x_hat are staged in LDS, every message
+ * entry in the tile is applied there in the order above, x is updated, and only the touched
+ * 64-byte granules of s / x_hat are written back.
  */
 int64_t mx_choco_msg_bytes(int64_t k);
+/* Scratch of mx_choco_apply (per-tile ranges of every message slot). */
+size_t mx_choco_apply_work_bytes(int64_t P, int n_slots);
 int mx_choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t k,
-                   const void* msgs, int64_t msg_ld_bytes, const int32_t* plan_dev, int64_t iter,
-                   int n_local, int M, float alpha, float gamma, void* stream);
+                   const void* msgs, int64_t msg_ld_bytes, int n_slots, const int32_t* plan_dev,
+                   int64_t iter, int n_local, int M, float alpha, float gamma, void* work,
+                   void* stream);
 
 /* ---------------------------------------------------------------- cross-GPU exchange (RCCL)
  * One process per GPU; workers partitioned by owner[].  mx_exchange_round posts, inside one

@@ -229,6 +229,40 @@ def test_topk_large_and_ties_vs_oracle(pkg, O, P, ratio):
     assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32))
 
 
+def _topk_case(O, P, pattern):
+    x = O.synth(P + 3, P)
+    if pattern == "layers":           # parameter-tensor-like blocks of very different scales
+        edges = np.linspace(0, P, 9).astype(np.int64)
+        for j in range(8):
+            x[edges[j]:edges[j + 1]] *= np.float32(10.0 ** (j % 4 - 2))
+    elif pattern == "sampled_large":  # only the chunks the sampler reads are large: forces the
+        c = np.arange(P) // 1024      # device-side fallback (candidate floor too high)
+        x[(c % 16) == 0] *= np.float32(1000.0)
+    elif pattern == "constant":       # every key ties
+        x[:] = np.float32(-0.25)
+    elif pattern == "ties":
+        x[::7] = np.float32(0.5)
+        x[::11] = np.float32(-0.5)
+    return x
+
+
+@pytest.mark.parametrize("stride", [0, 1, 16])
+@pytest.mark.parametrize("pattern", ["layers", "sampled_large", "constant", "ties"])
+def test_topk_sampled_floor_exact(pkg, O, stride, pattern):
+    """The sampled candidate floor (and its device-side fallback) never changes the result."""
+    P, ratio = 2_000_001, 0.99
+    x = _topk_case(O, P, pattern)
+    k = O.topk_k(P, ratio)
+    ov, oi = O.topk_abs(x, k)
+    pkg._lib.check(pkg.lib.mx_topk_set(b"sample_stride", stride))
+    try:
+        v, i = pkg.get_top_k(torch.from_numpy(x).cuda(), ratio)
+    finally:
+        pkg.lib.mx_topk_set(b"sample_stride", 0)
+    assert np.array_equal(i.cpu().numpy(), oi)
+    assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32))
+
+
 # ------------------------------------------------------------------------------------ helpers
 def test_flatten_unflatten_scatter(pkg):
     ts = [torch.randn(s, device="cuda") for s in ((3, 5), (7,), (0,), (64, 33), (1,))]
