@@ -37,6 +37,7 @@ def parse():
     ap.add_argument("--graph", type=int, default=0)
     ap.add_argument("--budget", type=float, default=1.0, help="1.0 = full rounds (headline)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--choco", type=int, default=1, help="also time ChocoSGD rounds (VGG-16 size, top-1%%)")
     return ap.parse_args()
 
 
@@ -74,6 +75,37 @@ def pmc_traffic(kernel_prefix="mix_kernel"):
     vals = [v.get("hbm_bytes_per_launch") for k, v in d.get("mix_pmc", {}).items() if kernel_prefix in k]
     vals = [v for v in vals if v]
     return (max(vals) if vals else None), os.path.relpath(files[-1], ROOT)
+
+
+def choco_figure(pkg, GP, rank, world, K, W, P=14_774_436, ratio=0.99, gamma=0.1):
+    """Secondary figure: ChocoSGD rounds (BASELINE config: VGG-16 size, top-1 %, graph 0, every
+    matching active) on the same GPUs -- top-k compress + [N > 1] message exchange + fused apply."""
+    import torch.distributed as dist
+    grp = pkg.ChocoWorkerGroup(GP, numel=P, ratio=ratio, consensus_lr=gamma, rank=rank, nranks=world,
+                               comm=None if world == 1 else pkg.engine.default_comm())
+    for r in range(grp.n_local):
+        pkg._lib.check(pkg.lib.mx_synth_fill(grp.rows[r].data_ptr(), P, 1234 + grp.row_base + r, None))
+    for it in range(W):
+        grp.step(it)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t = time.perf_counter()
+    for j in range(K):
+        grp.step(W + j)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t
+    if world > 1:
+        tt = torch.tensor([el], device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        el = float(tt.item())
+    out = {"config": f"VGG-16 size P={P}, ratio {ratio} (k={grp.k}), gamma {gamma}, graph 0 full rounds",
+           "rounds_per_s": K / el, "ms_per_round": 1e3 * el / K}
+    del grp
+    torch.cuda.empty_cache()
+    return out
 
 
 def timed_rounds(group, first, K):
@@ -167,6 +199,8 @@ def main():
                   "skipped_rounds": int((fl.sum(1) == 0).sum())}
         del gm
 
+    choco = choco_figure(pkg, GP, rank, world, max(5, K // 5), 3) if args.choco else None
+
     partner = np.asarray(GP.neighbors_info, np.int32)
     flags = np.asarray(GP.active_flags[W:W + K], np.uint8)
     # algorithmic HBM bytes of the mixing kernel on this GPU: every local row with degree > 0 read
@@ -174,6 +208,7 @@ def main():
     eng = group.engine
     hbm_bytes = []
     link_bytes = []
+    pair_bytes = []
     for f in flags:
         deg = np.zeros(n, int)
         for g in range(len(f)):
@@ -191,11 +226,16 @@ def main():
                     continue
                 a, b = eng.owner[p], eng.owner[q]
                 if a != b:
-                    links[(a, b)] = links.get((a, b), 0) + P * 4
+                    links[(a, b)] = links.get((a, b), 0) + P * 4     # p's row travels a -> b
                     if b == rank:
                         remote += 1
         hbm_bytes.append(2 * act * P * 4 + remote * P * 4)
         link_bytes.append(max(links.values()) if links else 0)
+        pair = {}
+        for (a, b), v in links.items():
+            key = (min(a, b), max(a, b))
+            pair[key] = pair.get(key, 0) + v
+        pair_bytes.append(max(pair.values()) if pair else 0)
     avg_ms = float(step_ms.mean())
     mix_avg_ms = float(mix_ms.mean())
     mix_bytes = float(np.mean(hbm_bytes))
@@ -229,15 +269,22 @@ def main():
                          "note": "achieved = algorithmic bytes (2 x active rows x P x 4 [+ slab rows]) / "
                                  "mean per-launch duration, HIP events on the launch stream"},
             "matcha_schedule": matcha,
+            "choco": choco,
         }
         if world > 1:
             lb = float(np.mean(link_bytes))
-            out["xgmi"] = {"max_link_bytes_per_round": lb, "achieved": lb / (avg_ms * 1e-3) / 1e9,
+            pb = float(np.mean(pair_bytes))
+            round_s = elapsed / K
+            out["xgmi"] = {"max_link_bytes_per_round": lb, "achieved": lb / round_s / 1e9,
                            "peak": XGMI_LINK_PEAK / 1e9, "unit": "GB/s",
-                           "frac": lb / (avg_ms * 1e-3) / XGMI_LINK_PEAK,
-                           "round_ms_events": avg_ms,
-                           "note": "busiest GPU-pair direction: bytes per round / mean round time "
-                                   "(exchange + mix, HIP events, rank 0)"}
+                           "frac": lb / round_s / XGMI_LINK_PEAK,
+                           "max_pair_bytes_both_directions": pb,
+                           "achieved_both_directions": pb / round_s / 1e9,
+                           "frac_both_directions": pb / round_s / XGMI_LINK_PEAK,
+                           "round_ms": 1e3 * round_s, "round_ms_events_rank0": avg_ms,
+                           "note": "busiest GPU pair: bytes that cross it per round (one direction, and "
+                                   "both directions summed) / whole-job round time (exchange + mix), "
+                                   "against the 153 GB/s per-link figure of SURVEY.md §8d"}
         if world == 1 and args.cpu_seconds > 0:
             out["cpu_baseline"] = cpu_baseline(pkg, partner, GP.neighbor_weight, n, P, args.cpu_seconds)
         else:
