@@ -14,11 +14,12 @@ from .comm_helpers import flatten_tensors, unflatten_tensors, scatter_tensors
 from .compressors import get_top_k
 from .topologies import select_graph, erdos_renyi, GRAPH_SIZES
 from . import solver
+from . import harness
 
 __all__ = [
     "MXError", "lib", "GraphProcessor", "FixedProcessor", "MatchaProcessor", "GossipEngine",
     "VirtualWorkerGroup", "RcclComm", "Layout", "partition", "ChocoWorkerGroup", "topk_count",
     "Communicator", "decenCommunicator", "ChocoCommunicator", "centralizedCommunicator",
     "flatten_tensors", "unflatten_tensors", "scatter_tensors", "get_top_k", "select_graph",
-    "erdos_renyi", "GRAPH_SIZES", "solver",
+    "erdos_renyi", "GRAPH_SIZES", "solver", "harness",
 ]

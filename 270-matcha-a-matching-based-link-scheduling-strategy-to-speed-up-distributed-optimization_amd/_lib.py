@@ -56,6 +56,11 @@ def _load():
         raise ImportError(
             f"native gossip library not built: {LIB_PATH} is missing. Build it with "
             f"`make -C {_HERE}` (hipcc --offload-arch=gfx950) or __graft_entry__.build().")
+    # torch first: it brings its own libamdhip64.so.7 / librccl / libhsa-runtime64 (same SONAMEs as
+    # /opt/rocm's), and the loader then binds this library to those already-loaded objects, so the
+    # process has ONE HIP runtime whose device pointers and streams both sides share.  Loading
+    # this library first would pull /opt/rocm's runtime in under torch's feet.
+    import torch  # noqa: F401
     L = ctypes.CDLL(LIB_PATH)
     for name, (res, args) in SIGNATURES.items():
         f = getattr(L, name)

@@ -109,6 +109,25 @@ class ChocoWorkerGroup:
         self.average(it, stream)
         return True
 
+    def state_dict(self):
+        """Checkpoint: rows, the persistent Choco state x_hat / s (communicator.py:179-182) and
+        the iteration counter."""
+        P = self.numel
+        return {"kind": "choco", "iter": int(self.iter), "row_base": int(self.row_base), "k": int(self.k),
+                "rows": self.x[:, :P].detach().clone(), "x_hat": self.x_hat[:, :P].detach().clone(),
+                "s": self.s[:, :P].detach().clone()}
+
+    def load_state_dict(self, state):
+        P = self.numel
+        if state.get("kind") != "choco" or int(state["row_base"]) != self.row_base or \
+                int(state["k"]) != self.k or tuple(state["rows"].shape) != (self.n_local, P):
+            raise ValueError("checkpoint does not match this Choco worker group")
+        with torch.no_grad():
+            self.x[:, :P].copy_(state["rows"])
+            self.x_hat[:, :P].copy_(state["x_hat"])
+            self.s[:, :P].copy_(state["s"])
+        self.iter = int(state["iter"])
+
     def communicate(self):
         it = self.iter
         self.iter += 1

@@ -358,6 +358,19 @@ class VirtualWorkerGroup:
             mixed[b].record(cur)
         return True
 
+    def state_dict(self):
+        """Checkpoint: the workers' rows and the iteration counter (resume on the same schedule)."""
+        return {"kind": "decen", "iter": int(self.iter), "row_base": int(self.row_base),
+                "rows": self.rows.detach().clone()}
+
+    def load_state_dict(self, state):
+        if state.get("kind") != "decen" or int(state["row_base"]) != self.row_base or \
+                tuple(state["rows"].shape) != tuple(self.rows.shape):
+            raise ValueError("checkpoint does not match this worker group")
+        with torch.no_grad():
+            self.rows.copy_(state["rows"])
+        self.iter = int(state["iter"])
+
     def communicate(self):
         """One round at the group's own iteration counter; returns seconds like the reference's
         communicate() (0 for a skipped round)."""

@@ -1,0 +1,391 @@
+"""GPU training harness around the gossip hot path: train_mpi.py:34-201 with synthetic batches.
+
+The reference's run(rank, size) (train_mpi.py:58-168) trains one model per MPI rank on the CPU
+and calls communicator.communicate(model) after every optimizer step.  This harness keeps that
+loop -- forward, loss, accuracy bookkeeping, backward, update_learning_rate, SGD step,
+zero_grad, communicate -- with two layouts:
+
+  * VirtualTrainer (one process, one GPU): all `size` workers' models live on the GPU and
+    their parameters are re-homed into ONE VirtualWorkerGroup / ChocoWorkerGroup arena, so each
+    batch runs `size` forward/backward/step sequences and then a single gossip launch for all
+    workers (the "8 virtual workers on one MI355X" mode of BASELINE configs 1-2);
+  * RankTrainer (torchrun, one process per worker): the drop-in decenCommunicator /
+    ChocoCommunicator on this rank's model, exactly the reference's per-rank call pattern.
+
+Data is synthetic (no dataset download on the GPU box): per worker a fixed seeded stream of
+MNIST-shaped (1x28x28) or CIFAR-shaped batches with random labels.  The Recorder writes the
+reference's seven per-rank logs (util.py:378-419); checkpoints hold the worker rows, the
+Choco state (x_hat, s) and the iteration counter so a run resumes on the same schedule.
+"""
+import os
+import time
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .choco import ChocoWorkerGroup
+from .engine import VirtualWorkerGroup
+from .graph_manager import FixedProcessor, MatchaProcessor
+from .topologies import select_graph
+
+
+# ----------------------------------------------------------------------------- model / meters
+class MNIST_MLP(nn.Module):
+    """models/MLP.py:5-25: 784 -> 500 -> 500 -> num_classes, ReLU, weights in self.layers."""
+
+    def __init__(self, num_classes):
+        super(MNIST_MLP, self).__init__()
+        self.layers = nn.ModuleList([nn.Linear(28 * 28, 500), nn.Linear(500, 500), nn.Linear(500, num_classes)])
+
+    def forward(self, x):
+        x = x.view(-1, 28 * 28)
+        x = F.relu(self.layers[0](x))
+        x = F.relu(self.layers[1](x))
+        return self.layers[2](x)
+
+
+def comp_accuracy(output, target, topk=(1,)):
+    """util.py:342-356 -- top-k accuracy in percent."""
+    with torch.no_grad():
+        maxk = max(topk)
+        batch_size = target.size(0)
+        _, pred = output.topk(maxk, 1, True, True)
+        pred = pred.t()
+        correct = pred.eq(target.view(1, -1).expand_as(pred))
+        return [correct[:k].reshape(-1).float().sum(0, keepdim=True).mul_(100.0 / batch_size) for k in topk]
+
+
+class AverageMeter(object):
+    """util.py:358-373."""
+
+    def __init__(self):
+        self.reset()
+
+    def reset(self):
+        self.val = 0
+        self.avg = 0
+        self.sum = 0
+        self.count = 0
+
+    def update(self, val, n=1):
+        self.val = val
+        self.sum += val * n
+        self.count += n
+        self.avg = self.sum / self.count
+
+
+class Recorder(object):
+    """util.py:376-419 -- per-rank timing / accuracy logs, same folder and file names."""
+
+    def __init__(self, args, rank):
+        self.record_accuracy = []
+        self.record_timing = []
+        self.record_comp_timing = []
+        self.record_comm_timing = []
+        self.record_losses = []
+        self.record_trainacc = []
+        self.total_record_timing = []
+        self.args = args
+        self.rank = rank
+        self.saveFolderName = args.savePath + args.name + '_' + args.model
+        if rank == 0 and not os.path.isdir(self.saveFolderName) and self.args.save:
+            os.makedirs(self.saveFolderName, exist_ok=True)
+
+    def add_new(self, record_time, comp_time, comm_time, epoch_time, top1, losses, test_acc):
+        self.total_record_timing.append(record_time)
+        self.record_timing.append(epoch_time)
+        self.record_comp_timing.append(comp_time)
+        self.record_comm_timing.append(comm_time)
+        self.record_trainacc.append(top1)
+        self.record_losses.append(losses)
+        self.record_accuracy.append(test_acc)
+
+    def log_path(self, suffix):
+        return (self.saveFolderName + '/dsgd-lr' + str(self.args.lr) + '-budget' + str(self.args.budget) +
+                '-r' + str(self.rank) + '-' + suffix + '.log')
+
+    def save_to_file(self):
+        for suffix, data in (("recordtime", self.total_record_timing), ("time", self.record_timing),
+                             ("comptime", self.record_comp_timing), ("commtime", self.record_comm_timing),
+                             ("acc", self.record_accuracy), ("losses", self.record_losses),
+                             ("tacc", self.record_trainacc)):
+            np.savetxt(self.log_path(suffix), np.asarray(data, dtype=np.float64), delimiter=',')
+        with open(self.saveFolderName + '/ExpDescription', 'w') as f:
+            f.write(str(self.args) + '\n')
+            f.write(self.args.description + '\n')
+
+
+def update_learning_rate(optimizer, epoch, args, itr=None, itr_per_epoch=None):
+    """train_mpi.py:171-201: linear warmup from 0.1 over 5 epochs when lr > 0.1, then x0.1 at
+    epochs 100 and 150."""
+    base_lr = 0.1
+    target_lr = args.lr
+    lr_schedule = [100, 150]
+    if args.warmup and epoch < 5:
+        if target_lr <= base_lr:
+            lr = target_lr
+        else:
+            count = epoch * itr_per_epoch + itr + 1
+            lr = base_lr + (target_lr - base_lr) * (count / (5 * itr_per_epoch))
+    else:
+        lr = target_lr
+        for e in lr_schedule:
+            if epoch >= e:
+                lr *= 0.1
+    for group in optimizer.param_groups:
+        group['lr'] = lr
+    return lr
+
+
+# ----------------------------------------------------------------------------- synthetic data
+def synthetic_batches(worker, n_batches, bs, shape=(1, 28, 28), num_classes=100, seed=1234, device="cuda"):
+    """A fixed stream of (data, target) batches for one worker (the partition_dataset stand-in:
+    util.py:115-254 downloads datasets, which the GPU box cannot)."""
+    g = torch.Generator(device="cpu")
+    g.manual_seed(seed * 1000 + worker)
+    out = []
+    for _ in range(n_batches):
+        data = torch.randn((bs,) + tuple(shape), generator=g)
+        target = torch.randint(0, num_classes, (bs,), generator=g)
+        out.append((data.to(device), target.to(device)))
+    return out
+
+
+# ----------------------------------------------------------------------------- harness
+def make_topology(args, rank, size, iterations):
+    """train_mpi.py:69-75 (MatchaProcessor when args.matcha, else FixedProcessor)."""
+    subGraphs = select_graph(args.graphid)
+    if args.matcha:
+        return MatchaProcessor(subGraphs, args.budget, rank, size, iterations, False)
+    return FixedProcessor(subGraphs, args.budget, rank, size, iterations, True)
+
+
+def sync_rows(rows):
+    """sync_allreduce (train_mpi.py:34-56) for workers held as rows: every row becomes
+    (sum over workers in rank order) / size."""
+    with torch.no_grad():
+        acc = rows[0].clone()
+        for r in range(1, rows.shape[0]):
+            acc.add_(rows[r])
+        acc.div_(float(rows.shape[0]))
+        rows.copy_(acc.expand_as(rows))
+
+
+class VirtualTrainer:
+    """All workers of the topology on this GPU; one gossip launch per batch for all of them."""
+
+    def __init__(self, args, model_fn, n_batches, device="cuda"):
+        self.args = args
+        size = args.size
+        np.random.seed(args.randomSeed)                          # train_mpi.py:62
+        torch.manual_seed(args.randomSeed)
+        self.GP = make_topology(args, 0, size, args.epoch * n_batches)
+        self.models = []
+        for r in range(size):
+            torch.manual_seed(args.randomSeed + r)                # train_mpi.py:61, per rank
+            self.models.append(model_fn().to(device))
+        if args.compress:
+            self.group = ChocoWorkerGroup(self.GP, self.models, ratio=args.ratio,
+                                          consensus_lr=args.consensus_lr)
+        else:
+            self.group = VirtualWorkerGroup(self.GP, self.models)
+        sync_rows(self.group.rows)
+        self.optimizers = [torch.optim.SGD(m.parameters(), lr=args.lr, momentum=args.momentum,
+                                           weight_decay=5e-4, nesterov=args.nesterov, dampening=0)
+                           for m in self.models]
+        self.criterion = nn.CrossEntropyLoss()
+        self.data = [synthetic_batches(r, n_batches, args.bs, args.shape, args.num_classes, args.randomSeed,
+                                       device) for r in range(size)]
+        self.n_batches = n_batches
+        self.recorders = [Recorder(args, r) for r in range(size)] if args.save else None
+        self.epoch = 0
+
+    def communicate(self):
+        return self.group.communicate()
+
+    def train_epoch(self, on_round=None):
+        """One epoch of train_mpi.py:109-168 for every worker; returns per-worker stats."""
+        args = self.args
+        size = len(self.models)
+        epoch = self.epoch
+        comp = [0.0] * size
+        comm_time = 0.0
+        losses = [AverageMeter() for _ in range(size)]
+        top1 = [AverageMeter() for _ in range(size)]
+        tic = time.time()
+        for m in self.models:
+            m.train()
+        for b in range(self.n_batches):
+            for r, (m, opt) in enumerate(zip(self.models, self.optimizers)):
+                t0 = time.time()
+                data, target = self.data[r][b]
+                output = m(data)
+                loss = self.criterion(output, target)
+                acc1 = comp_accuracy(output, target)
+                losses[r].update(loss.item(), data.size(0))
+                top1[r].update(acc1[0].item(), data.size(0))
+                loss.backward()
+                update_learning_rate(opt, epoch, args, itr=b, itr_per_epoch=self.n_batches)
+                opt.step()
+                opt.zero_grad()
+                comp[r] += time.time() - t0
+            if on_round is not None:
+                on_round("before", self)
+            comm_time += self.communicate()
+            if on_round is not None:
+                on_round("after", self)
+        record_time = time.time() - tic
+        stats = []
+        for r in range(size):
+            test_acc = top1[r].avg             # no test split in the synthetic stream
+            stats.append({"worker": r, "loss": losses[r].avg, "train_acc": top1[r].avg,
+                          "comp_time": comp[r], "comm_time": comm_time})
+            if self.recorders is not None:
+                self.recorders[r].add_new(record_time, comp[r], comm_time, comp[r] + comm_time, top1[r].avg,
+                                          losses[r].avg, test_acc)
+                if epoch % 10 == 0:
+                    self.recorders[r].save_to_file()
+        self.epoch += 1
+        return stats
+
+    def finish(self):
+        if self.recorders is not None:
+            for rec in self.recorders:
+                rec.save_to_file()
+
+    # checkpoint / resume: worker rows, Choco state, iteration and epoch counters, optimizers
+    def state_dict(self):
+        return {"group": self.group.state_dict(), "epoch": self.epoch,
+                "optimizers": [o.state_dict() for o in self.optimizers]}
+
+    def load_state_dict(self, state):
+        self.group.load_state_dict(state["group"])
+        self.epoch = int(state["epoch"])
+        for o, s in zip(self.optimizers, state["optimizers"]):
+            o.load_state_dict(s)
+
+    def save(self, path):
+        torch.save(self.state_dict(), path)
+
+    def load(self, path):
+        self.load_state_dict(torch.load(path, map_location="cuda", weights_only=True))
+
+
+class RankTrainer:
+    """One worker per process (torchrun): train_mpi.py's run(rank, size) with the drop-in
+    communicators -- sync through RCCL all-reduce, then per batch step + communicate(model)."""
+
+    def __init__(self, args, model_fn, n_batches, rank, size, transport=None, device="cuda"):
+        from .communicator import ChocoCommunicator, centralizedCommunicator, decenCommunicator
+        self.args = args
+        self.rank, self.size = rank, size
+        torch.manual_seed(args.randomSeed + rank)                # train_mpi.py:61
+        np.random.seed(args.randomSeed)                          # train_mpi.py:62
+        self.GP = make_topology(args, rank, size, args.epoch * n_batches)
+        if args.compress:
+            self.communicator = ChocoCommunicator(rank, size, self.GP, args.ratio, args.consensus_lr,
+                                                  transport=transport)
+        else:
+            self.communicator = decenCommunicator(rank, size, self.GP, transport=transport)
+        self.model = model_fn().to(device)
+        self.optimizer = torch.optim.SGD(self.model.parameters(), lr=args.lr, momentum=args.momentum,
+                                         weight_decay=5e-4, nesterov=args.nesterov, dampening=0)
+        self.criterion = nn.CrossEntropyLoss()
+        centralizedCommunicator(rank, size, transport=transport).communicate(self.model)   # sync_allreduce
+        self.data = synthetic_batches(rank, n_batches, args.bs, args.shape, args.num_classes, args.randomSeed,
+                                      device)
+        self.n_batches = n_batches
+        self.recorder = Recorder(args, rank) if args.save else None
+        self.epoch = 0
+
+    def train_epoch(self):
+        args = self.args
+        comp_time = comm_time = 0.0
+        losses, top1 = AverageMeter(), AverageMeter()
+        tic = time.time()
+        self.model.train()
+        for b, (data, target) in enumerate(self.data):
+            t0 = time.time()
+            output = self.model(data)
+            loss = self.criterion(output, target)
+            acc1 = comp_accuracy(output, target)
+            losses.update(loss.item(), data.size(0))
+            top1.update(acc1[0].item(), data.size(0))
+            loss.backward()
+            update_learning_rate(self.optimizer, self.epoch, args, itr=b, itr_per_epoch=self.n_batches)
+            self.optimizer.step()
+            self.optimizer.zero_grad()
+            comp_time += time.time() - t0
+            comm_time += self.communicator.communicate(self.model)          # train_mpi.py:142
+        if self.recorder is not None:
+            self.recorder.add_new(time.time() - tic, comp_time, comm_time, comp_time + comm_time, top1.avg,
+                                  losses.avg, top1.avg)
+            if self.epoch % 10 == 0:
+                self.recorder.save_to_file()
+        self.epoch += 1
+        return [{"worker": self.rank, "loss": losses.avg, "train_acc": top1.avg, "comp_time": comp_time,
+                 "comm_time": comm_time}]
+
+    def finish(self):
+        if self.recorder is not None:
+            self.recorder.save_to_file()
+
+
+class HarnessArgs:
+    """train_mpi.py:205-231 defaults, plus the harness's own (size, shape, num_classes, ratio)."""
+
+    def __init__(self, **kw):
+        self.name = "Vanilla DecenSGD-synthetic"
+        self.description = "MI355X gossip harness, synthetic batches"
+        self.model = "mlp"
+        self.lr = 0.8
+        self.momentum = 0.0
+        self.epoch = 1
+        self.bs = 64
+        self.warmup = True
+        self.nesterov = False
+        self.matcha = True
+        self.budget = 1.0
+        self.graphid = 0
+        self.savePath = "./saveModel"
+        self.save = False
+        self.compress = False
+        self.consensus_lr = 0.1
+        self.ratio = 0.9          # train_mpi.py:79 hard-codes ChocoCommunicator(..., 0.9, ...)
+        self.randomSeed = 1234
+        self.size = 8
+        self.shape = (1, 28, 28)
+        self.num_classes = 100    # train_mpi.py:84 select_model(100, args)
+        for k, v in kw.items():
+            if not hasattr(self, k):
+                raise TypeError(f"unknown harness argument {k!r}")
+            setattr(self, k, v)
+
+    def __str__(self):
+        return "Namespace(" + ", ".join(f"{k}={v!r}" for k, v in sorted(vars(self).items())) + ")"
+
+
+def model_factory(args):
+    if args.model == "mlp":
+        return lambda: MNIST_MLP(args.num_classes)
+    raise ValueError(f"model {args.model!r}: the harness ships the MLP plumbing config; pass a "
+                     "model_fn to VirtualTrainer for other architectures")
+
+
+def epoch_summary(stats, epoch):
+    loss = float(np.mean([s["loss"] for s in stats]))
+    acc = float(np.mean([s["train_acc"] for s in stats]))
+    comp = float(np.mean([s["comp_time"] for s in stats]))
+    return (f"{epoch:0>3}  workers: {len(stats)}, loss: {loss:.3f}, train_acc: {acc:.3f}, "
+            f"comp_time: {comp:.3f}, comm_time: {stats[0]['comm_time']:.3f}")
+
+
+def iterations_for(args, n_batches):
+    return args.epoch * n_batches
+
+
+__all__ = ["MNIST_MLP", "comp_accuracy", "AverageMeter", "Recorder", "update_learning_rate",
+           "synthetic_batches", "make_topology", "sync_rows", "VirtualTrainer", "RankTrainer", "HarnessArgs",
+           "model_factory", "epoch_summary", "iterations_for"]

@@ -1,0 +1,108 @@
+"""GPU: the training harness drives the gossip path exactly (every round vs the oracle), and
+checkpoints resume on the same schedule."""
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def _args(pkg, **kw):
+    base = dict(size=8, epoch=2, bs=16, budget=0.5, graphid=0, lr=0.1)
+    base.update(kw)
+    return pkg.harness.HarnessArgs(**base)
+
+
+@pytest.mark.parametrize("matcha", [True, False])
+def test_virtual_trainer_rounds_match_oracle(pkg, O, matcha):
+    """Every communicate() of the harness is one reference gossip round of the post-step rows."""
+    H = pkg.harness
+    args = _args(pkg, matcha=matcha)
+    tr = H.VirtualTrainer(args, H.model_factory(args), n_batches=3)
+    GP = tr.GP
+    partner = np.asarray(GP.neighbors_info, np.int32)
+    seen = {"rounds": 0}
+    rows0 = tr.group.rows.cpu().numpy()
+    assert all(np.array_equal(rows0[0], rows0[r]) for r in range(8))      # sync_allreduce
+    state = {}
+
+    def hook(when, t):
+        if when == "before":
+            state["X"] = t.group.rows.cpu().numpy().copy()
+            state["it"] = t.group.iter
+            return
+        it = state["it"]
+        flags = np.asarray(GP.active_flags[it], np.uint8)
+        M = len(flags)
+        want = O.decen_round(state["X"], partner[:M], flags, GP.neighbor_weight) if flags.any() else state["X"]
+        got = t.group.rows.cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), want.view(np.uint32)), f"round {it}"
+        seen["rounds"] += 1
+
+    for _ in range(args.epoch):
+        stats = tr.train_epoch(on_round=hook)
+        assert len(stats) == 8 and all(np.isfinite(s["loss"]) for s in stats)
+    assert seen["rounds"] == 6 and tr.group.iter == 6
+    # parameters are views into the arena: the models see the mixed values
+    p0 = next(tr.models[3].parameters())
+    assert p0.data.data_ptr() >= tr.group.arena.data_ptr()
+
+
+def test_virtual_trainer_choco_rounds_match_oracle(pkg, O):
+    H = pkg.harness
+    args = _args(pkg, compress=True, budget=1.0, ratio=0.9)
+    tr = H.VirtualTrainer(args, H.model_factory(args), n_batches=2)
+    GP = tr.GP
+    partner = np.asarray(GP.neighbors_info, np.int32)
+    P = tr.group.numel
+    XH = np.zeros((8, P), np.float32)
+    S = np.zeros((8, P), np.float32)
+    st = {}
+
+    def hook(when, t):
+        if when == "before":
+            st["X"] = t.group.rows.cpu().numpy().copy()
+            st["it"] = t.group.iter
+            return
+        flags = np.asarray(GP.active_flags[st["it"]], np.uint8)
+        X = st["X"]
+        O.choco_round(X, XH, S, partner[:len(flags)], flags, GP.neighbor_weight, t.group.k, args.consensus_lr)
+        assert np.array_equal(t.group.rows.cpu().numpy().view(np.uint32), X.view(np.uint32))
+
+    for _ in range(args.epoch):
+        tr.train_epoch(on_round=hook)
+    assert np.array_equal(tr.group.x_hat[:, :P].cpu().numpy(), XH)
+    assert np.array_equal(tr.group.s[:, :P].cpu().numpy(), S)
+
+
+@pytest.mark.parametrize("compress", [False, True])
+def test_checkpoint_resume_same_schedule(pkg, tmp_path, compress):
+    H = pkg.harness
+    args = _args(pkg, compress=compress, epoch=2, budget=0.5)
+    a = H.VirtualTrainer(args, H.model_factory(args), n_batches=3)
+    a.train_epoch()
+    path = str(tmp_path / "ckpt.pt")
+    a.save(path)
+    a.train_epoch()
+    b = H.VirtualTrainer(args, H.model_factory(args), n_batches=3)
+    b.load(path)
+    assert b.group.iter == 3 and b.epoch == 1
+    b.train_epoch()
+    assert b.group.iter == a.group.iter == 6
+    ra, rb = a.group.rows, b.group.rows
+    assert torch.allclose(ra, rb, rtol=0, atol=1e-6), float((ra - rb).abs().max())
+    with pytest.raises(ValueError):
+        wrong = H.HarnessArgs(size=8, epoch=1, bs=16, graphid=0, compress=compress, num_classes=10)
+        c = H.VirtualTrainer(wrong, H.model_factory(wrong), n_batches=1)
+        c.load(path)
+
+
+def test_recorder_through_trainer(pkg, tmp_path):
+    H = pkg.harness
+    args = _args(pkg, save=True, savePath=str(tmp_path) + "/", epoch=1)
+    tr = H.VirtualTrainer(args, H.model_factory(args), n_batches=2)
+    tr.train_epoch()
+    tr.finish()
+    import os
+    files = os.listdir(str(tmp_path / (args.name + "_mlp")))
+    assert len([f for f in files if f.endswith(".log")]) == 7 * 8
