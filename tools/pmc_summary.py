@@ -63,7 +63,17 @@ def main(src, dst):
         }
         if f_kib is not None and w_kib is not None:
             mix[name]["hbm_bytes_per_launch"] = 2 * 1024 * f_kib + 1024 * w_kib
-    out = {"source": src, "kernels": kernels, "mix_pmc": mix,
+    allk = {}
+    for name in set(fetch) | set(write):
+        f = fetch.get(name, [])
+        w = write.get(name, [])
+        if not f or not w:
+            continue
+        allk[name] = {"launches": min(len(f), len(w)),
+                      "hbm_read_bytes_corrected": 2 * 1024 * sum(f) / len(f),
+                      "hbm_write_bytes": 1024 * sum(w) / len(w),
+                      "hbm_bytes_per_launch": 2 * 1024 * sum(f) / len(f) + 1024 * sum(w) / len(w)}
+    out = {"source": src, "kernels": kernels, "mix_pmc": mix, "pmc_all": allk,
            "note": "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB -> bytes x1024"}
     os.makedirs(os.path.dirname(dst), exist_ok=True)
     with open(dst, "w") as f:
