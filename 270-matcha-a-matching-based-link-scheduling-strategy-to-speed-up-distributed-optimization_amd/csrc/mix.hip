@@ -40,17 +40,28 @@ struct VT<2> { typedef float type __attribute__((ext_vector_type(2))); };
 template <>
 struct VT<1> { typedef float type __attribute__((ext_vector_type(1))); };
 
+// Row pointers arrive as generic pointers; accessing them through the global address space makes
+// the compiler emit global_load/store (counted on vmcnt only) instead of flat_* (counted on vmcnt
+// AND lgkmcnt, so every LDS or scalar-load wait in the loop would also drain the HBM stream).
+template <typename F>
+using GPtr = __attribute__((address_space(1))) F*;
+
 template <bool NT, typename F>
 __device__ __forceinline__ F ld(const float* p) {
-    if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const F*>(p));
-    else return *reinterpret_cast<const F*>(p);
+    const GPtr<const F> g = (GPtr<const F>)(p);
+    if constexpr (NT) return __builtin_nontemporal_load(g);
+    else return *g;
 }
 
 template <bool NT, typename F>
 __device__ __forceinline__ void st(float* p, const F& v) {
-    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<F*>(p));
-    else *reinterpret_cast<F*>(p) = v;
+    const GPtr<F> g = (GPtr<F>)(p);
+    if constexpr (NT) __builtin_nontemporal_store(v, g);
+    else *g = v;
 }
+
+__device__ __forceinline__ float ld1(const float* p) { return *(GPtr<const float>)(p); }
+__device__ __forceinline__ void st1(float* p, float v) { *(GPtr<float>)(p) = v; }
 
 
 // Plan record of this iteration, decoded into LDS (see mx_plan_build); returns the bit mask of
@@ -137,7 +148,7 @@ __device__ __forceinline__ void load_slot(F (&v)[U], const float* row, int64_t g
             v[u] = ld<NT, F>(row + c);
         } else {
 #pragma unroll
-            for (int j = 0; j < VEC; ++j) v[u][j] = (c + j < lim) ? row[c + j] : 0.0f;
+            for (int j = 0; j < VEC; ++j) v[u][j] = (c + j < lim) ? ld1(row + c + j) : 0.0f;
         }
     }
 }
@@ -149,7 +160,7 @@ __device__ __forceinline__ void store_one(float* row, int64_t c, int64_t lim, bo
     } else {
 #pragma unroll
         for (int j = 0; j < VEC; ++j)
-            if (c + j < lim) row[c + j] = a[j];
+            if (c + j < lim) st1(row + c + j, a[j]);
     }
 }
 
@@ -172,6 +183,13 @@ __global__ __launch_bounds__(kTPB) void mix_kernel(float* const* __restrict__ se
     const int32_t* deg = sp.w + mx::kPlanHeader;
     const float* sw = reinterpret_cast<const float*>(deg + n_local);
     const int32_t* src = deg + 2 * n_local;
+    int dg[NS];                               // wave-uniform degrees (0 beyond n_local)
+    int maxd = 0;
+#pragma unroll
+    for (int r = 0; r < NS; ++r) {
+        dg[r] = r < n_local ? __builtin_amdgcn_readfirstlane(deg[r]) : 0;
+        maxd = dg[r] > maxd ? dg[r] : maxd;
+    }
 
     Sched sc;
     sc.init<VEC, U>(chunked != 0, nseg, seg_len, tile_off, total_tiles);
@@ -205,30 +223,41 @@ __global__ __launch_bounds__(kTPB) void mix_kernel(float* const* __restrict__ se
         }
         float* const* ptrs = seg_ptrs + (int64_t)seg * n_slots;
         const bool full = seg_vec[seg] && (g + (U - 1) * kTPB) * VEC + VEC <= lim;
-        for (int r = 0; r < n_local; ++r) {
-            const int d = deg[r];
-            if (d == 0) continue;
-            F acc[U];
+        // Edge-major FMA chains: step e adds every row's e-th partner (rows unrolled, so the NS
+        // slot lookups and LDS reads of one step are independent and overlap); per row the
+        // partners still come in ascending matching order and the self term last, exactly the
+        // reference's rounding sequence.
+        F acc[NS][U];
+#pragma unroll
+        for (int r = 0; r < NS; ++r)
 #pragma unroll
             for (int u = 0; u < U; ++u)
 #pragma unroll
-                for (int j = 0; j < VEC; ++j) acc[u][j] = 0.0f;
-            for (int e = 0; e < d; ++e) {
-                const int sl = src[r * M + e];
+                for (int j = 0; j < VEC; ++j) acc[r][u][j] = 0.0f;
+        for (int e = 0; e < maxd; ++e) {
 #pragma unroll
-                for (int u = 0; u < U; ++u) {
-                    const F x = lds[sl][u][tid];
+            for (int r = 0; r < NS; ++r) {
+                if (e < dg[r]) {
+                    const int sl = __builtin_amdgcn_readfirstlane(src[r * M + e]);
 #pragma unroll
-                    for (int j = 0; j < VEC; ++j) acc[u][j] = __builtin_fmaf(alpha, x[j], acc[u][j]);
+                    for (int u = 0; u < U; ++u) {
+                        const F x = lds[sl][u][tid];
+#pragma unroll
+                        for (int j = 0; j < VEC; ++j) acc[r][u][j] = __builtin_fmaf(alpha, x[j], acc[r][u][j]);
+                    }
                 }
             }
+        }
+#pragma unroll
+        for (int r = 0; r < NS; ++r) {
+            if (dg[r] == 0) continue;
             const float s = sw[r];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const F xs = lds[r][u][tid];
 #pragma unroll
-                for (int j = 0; j < VEC; ++j) acc[u][j] = __builtin_fmaf(s, xs[j], acc[u][j]);
-                store_one<VEC, NT>(ptrs[r], (g + (int64_t)u * kTPB) * VEC, lim, full, acc[u]);
+                for (int j = 0; j < VEC; ++j) acc[r][u][j] = __builtin_fmaf(s, xs[j], acc[r][u][j]);
+                store_one<VEC, NT>(ptrs[r], (g + (int64_t)u * kTPB) * VEC, lim, full, acc[r][u]);
             }
         }
         if (i + 1 < sc.niter) {
@@ -250,7 +279,7 @@ __global__ __launch_bounds__(kTPB) void mix_kernel(float* const* __restrict__ se
 template <int NS>
 using RegVec = float __attribute__((ext_vector_type(NS * 4)));
 
-template <int NS, bool NT, bool PF>
+template <int NS, int U, bool NT, bool PF>
 __global__ __launch_bounds__(kTPB) void mix_kernel_reg(float* const* __restrict__ seg_ptrs,
                                                        const int64_t* __restrict__ seg_len,
                                                        const int64_t* __restrict__ tile_off,
@@ -267,65 +296,79 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_reg(float* const* __restrict_
     const int32_t* src = deg + 2 * n_local;
 
     Sched sc;
-    sc.init<4, 1>(chunked != 0, nseg, seg_len, tile_off, total_tiles);
+    sc.init<4, U>(chunked != 0, nseg, seg_len, tile_off, total_tiles);
     if (sc.niter == 0) return;
-    auto load_all = [&](RegVec<NS>& a, int seg, int64_t g, int64_t lim) {
+    // U accesses per lane per slot: columns (g + u * 256) * 4 .. +3, u < U
+    auto load_all = [&](RegVec<NS> (&a)[U], int seg, int64_t g, int64_t lim) {
         float* const* ptrs = seg_ptrs + (int64_t)seg * n_slots;
         const bool vec_ok = seg_vec[seg] != 0;
 #pragma unroll
         for (int k = 0; k < NS; ++k) {
             if ((need >> k) & 1ull) {
-                F q[1];
-                load_slot<4, 1, NT>(q, ptrs[k], g, lim, vec_ok);
-                a[4 * k + 0] = q[0][0];
-                a[4 * k + 1] = q[0][1];
-                a[4 * k + 2] = q[0][2];
-                a[4 * k + 3] = q[0][3];
+                F q[U];
+                load_slot<4, U, NT>(q, ptrs[k], g, lim, vec_ok);
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    a[u][4 * k + 0] = q[u][0];
+                    a[u][4 * k + 1] = q[u][1];
+                    a[u][4 * k + 2] = q[u][2];
+                    a[u][4 * k + 3] = q[u][3];
+                }
             }
         }
     };
     int seg;
     int64_t g, lim;
-    sc.at<4, 1>(0, seg, g, lim);
-    RegVec<NS> cur, nxt;
+    sc.at<4, U>(0, seg, g, lim);
+    RegVec<NS> cur[U], nxt[PF ? U : 1];
     load_all(cur, seg, g, lim);
     for (int64_t i = 0; i < sc.niter; ++i) {
         int nseg_i = 0;
         int64_t ng = 0, nlim = 0;
-        if (PF && i + 1 < sc.niter) {
-            sc.at<4, 1>(i + 1, nseg_i, ng, nlim);
-            load_all(nxt, nseg_i, ng, nlim);
+        if constexpr (PF) {
+            if (i + 1 < sc.niter) {
+                sc.at<4, U>(i + 1, nseg_i, ng, nlim);
+                load_all(nxt, nseg_i, ng, nlim);
+            }
         }
         float* const* ptrs = seg_ptrs + (int64_t)seg * n_slots;
-        const int64_t c = g * 4;
-        const bool full = seg_vec[seg] && c + 4 <= lim;
+        const bool full = seg_vec[seg] && (g + (U - 1) * kTPB) * 4 + 4 <= lim;
         for (int r = 0; r < n_local; ++r) {
             const int d = deg[r];
             if (d == 0) continue;
-            F acc = {0.0f, 0.0f, 0.0f, 0.0f};
+            F acc[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc[u] = F{0.0f, 0.0f, 0.0f, 0.0f};
             for (int e = 0; e < d; ++e) {
                 const int s4 = 4 * __builtin_amdgcn_readfirstlane(src[r * M + e]);
-                acc[0] = __builtin_fmaf(alpha, cur[s4 + 0], acc[0]);
-                acc[1] = __builtin_fmaf(alpha, cur[s4 + 1], acc[1]);
-                acc[2] = __builtin_fmaf(alpha, cur[s4 + 2], acc[2]);
-                acc[3] = __builtin_fmaf(alpha, cur[s4 + 3], acc[3]);
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    acc[u][0] = __builtin_fmaf(alpha, cur[u][s4 + 0], acc[u][0]);
+                    acc[u][1] = __builtin_fmaf(alpha, cur[u][s4 + 1], acc[u][1]);
+                    acc[u][2] = __builtin_fmaf(alpha, cur[u][s4 + 2], acc[u][2]);
+                    acc[u][3] = __builtin_fmaf(alpha, cur[u][s4 + 3], acc[u][3]);
+                }
             }
             const int r4 = 4 * __builtin_amdgcn_readfirstlane(r);
             const float s = sw[r];
-            acc[0] = __builtin_fmaf(s, cur[r4 + 0], acc[0]);
-            acc[1] = __builtin_fmaf(s, cur[r4 + 1], acc[1]);
-            acc[2] = __builtin_fmaf(s, cur[r4 + 2], acc[2]);
-            acc[3] = __builtin_fmaf(s, cur[r4 + 3], acc[3]);
-            store_one<4, NT>(ptrs[r], c, lim, full, acc);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                acc[u][0] = __builtin_fmaf(s, cur[u][r4 + 0], acc[u][0]);
+                acc[u][1] = __builtin_fmaf(s, cur[u][r4 + 1], acc[u][1]);
+                acc[u][2] = __builtin_fmaf(s, cur[u][r4 + 2], acc[u][2]);
+                acc[u][3] = __builtin_fmaf(s, cur[u][r4 + 3], acc[u][3]);
+                store_one<4, NT>(ptrs[r], (g + (int64_t)u * kTPB) * 4, lim, full, acc[u]);
+            }
         }
         if (i + 1 < sc.niter) {
-            if (PF) {
+            if constexpr (PF) {
                 seg = nseg_i;
                 g = ng;
                 lim = nlim;
-                cur = nxt;
+#pragma unroll
+                for (int u = 0; u < U; ++u) cur[u] = nxt[u];
             } else {
-                sc.at<4, 1>(i + 1, seg, g, lim);
+                sc.at<4, U>(i + 1, seg, g, lim);
                 load_all(cur, seg, g, lim);
             }
         }
@@ -345,13 +388,14 @@ Cfg pick(int n_slots) {
 }
 
 // tuning state (mx_mix_set / mx_mix_get); defaults from tools/mixtune.py sweeps on MI355X
-// (8 x 25.6M graph-0 rounds): register-indexed + non-temporal + tile stride at 4 WGs/CU ran at
-// 0.95x the time of torch's copy_ of the same bytes; balanced chunks were 20-30% slower (every
-// workgroup streaming its own far-apart range loses the chip-wide DRAM row locality of the
-// tile sweep); prefetch did not pay at this occupancy.
+// (8 x 25.6M graph-0 rounds): register-indexed + non-temporal + tile stride; with global (not
+// flat) loads 2 WGs/CU beat 3 / 4 by 5-9 % (fewer concurrent DRAM streams, latency still hidden)
+// and ran at 0.94x the time of torch's copy_ of the same bytes; 2 / 4 accesses per lane per row
+// and prefetch were 3-5 % slower; balanced contiguous chunks 20-30 % slower (each workgroup
+// streaming its own far-apart range loses the chip-wide DRAM row locality of the tile sweep).
 struct Tune {
-    int blocks_per_cu = 4;
-    int unroll = 1;      // 1 or 2 accesses per lane per row per tile (NS = 8 config only)
+    int blocks_per_cu = 2;
+    int unroll = 1;      // 1, 2 or 4 accesses per lane per row per tile (NS = 8 configs only; LDS kernel <= 2)
     int nontemporal = 1;
     int prefetch = 0;
     int regidx = 1;      // 1: register-indexed kernel (n_slots <= 8; wider spills), 0: LDS-column kernel
@@ -359,7 +403,12 @@ struct Tune {
 };
 Tune g_tune;
 
-int unroll_for(int ns) { return (ns == 8 && !g_tune.regidx) ? g_tune.unroll : 1; }
+// accesses per lane per slot per tile: the NS = 8 kernels take 1, 2 or 4 (the LDS one 1 or 2)
+int unroll_for(int ns) {
+    if (ns != 8) return 1;
+    if (!g_tune.regidx && g_tune.unroll > 2) return 2;
+    return g_tune.unroll;
+}
 
 int cu_count() {
     static int v = [] {
@@ -390,11 +439,11 @@ int launch(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_o
     return MX_OK;
 }
 
-template <int NS, bool NT, bool PF>
+template <int NS, int U, bool NT, bool PF>
 int launch_reg(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_off,
                const uint8_t* seg_vec, int nseg, int n_slots, const int32_t* plan, int64_t iter,
                int n_local, int M, float alpha, int64_t total_tiles, hipStream_t st) {
-    hipLaunchKernelGGL((mix_kernel_reg<NS, NT, PF>), dim3((unsigned)grid_for(total_tiles)), dim3(kTPB),
+    hipLaunchKernelGGL((mix_kernel_reg<NS, U, NT, PF>), dim3((unsigned)grid_for(total_tiles)), dim3(kTPB),
                        0, st, seg_ptrs, seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan,
                        iter, n_local, M, alpha, (nseg == 1 && g_tune.chunked) ? 1 : 0);
     MX_LAUNCH_CHECK();
@@ -415,7 +464,7 @@ extern "C" int mx_mix_set(const char* key, int value) {
         MX_CHECK(value >= 1 && value <= 64, "mx_mix_set: blocks_per_cu %d", value);
         slot = &g_tune.blocks_per_cu;
     } else if (!strcmp(key, "unroll")) {
-        MX_CHECK(value == 1 || value == 2, "mx_mix_set: unroll %d", value);
+        MX_CHECK(value == 1 || value == 2 || value == 4, "mx_mix_set: unroll %d", value);
         slot = &g_tune.unroll;
     } else if (!strcmp(key, "nontemporal")) {
         slot = &g_tune.nontemporal;
@@ -483,14 +532,18 @@ extern "C" int mx_gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_
         case 2: return launch<V, N, U, false, true>(MX_ARGS);                 \
         default: return launch<V, N, U, true, true>(MX_ARGS);                 \
     }
-#define MX_DISPATCH_REG(N)                                                    \
+#define MX_DISPATCH_REG(N, U)                                                 \
     switch (key) {                                                            \
-        case 0: return launch_reg<N, false, false>(MX_ARGS);                  \
-        case 1: return launch_reg<N, true, false>(MX_ARGS);                   \
-        case 2: return launch_reg<N, false, true>(MX_ARGS);                   \
-        default: return launch_reg<N, true, true>(MX_ARGS);                   \
+        case 0: return launch_reg<N, U, false, false>(MX_ARGS);               \
+        case 1: return launch_reg<N, U, true, false>(MX_ARGS);                \
+        case 2: return launch_reg<N, U, false, U == 1>(MX_ARGS);              \
+        default: return launch_reg<N, U, true, U == 1>(MX_ARGS);              \
     }
-    if (g_tune.regidx && c.ns == 8) { MX_DISPATCH_REG(8) }
+    if (g_tune.regidx && c.ns == 8) {
+        if (unroll_for(8) == 4) { MX_DISPATCH_REG(8, 4) }
+        if (unroll_for(8) == 2) { MX_DISPATCH_REG(8, 2) }
+        MX_DISPATCH_REG(8, 1)
+    }
     switch (c.ns) {
         case 8:
             if (unroll_for(8) == 2) { MX_DISPATCH(4, 8, 2) }

@@ -38,8 +38,12 @@ __global__ __launch_bounds__(kTPB) void seg_copy_kernel(float* const* __restrict
             if (i < total) {
                 while (off[s + 1] <= i) ++s;
                 const int64_t k = i - off[s];
-                if (kGather) flat[i] = ptrs[s][k];
-                else ptrs[s][k] = flat[i];
+                // tensor pointers come from a table: address them as global memory (global_* not
+                // flat_* instructions)
+                typedef __attribute__((address_space(1))) float gfloat;
+                gfloat* p = (gfloat*)(ptrs[s]);
+                if (kGather) flat[i] = p[k];
+                else p[k] = flat[i];
             }
         }
         __syncthreads();

@@ -278,8 +278,8 @@ def test_flatten_unflatten_scatter(pkg):
 
 
 # ------------------------------------------------------------------------------------ tuning variants
-VARIANTS = [(bpc, u, nt, pf, rg, ch) for bpc in (1, 5) for u in (1, 2) for nt in (0, 1) for pf in (0, 1)
-            for rg in (0, 1) for ch in (0, 1) if not (rg and u == 2)]
+VARIANTS = [(bpc, u, nt, pf, rg, ch) for bpc in (1, 5) for u in (1, 2, 4) for nt in (0, 1) for pf in (0, 1)
+            for rg in (0, 1) for ch in (0, 1) if not (u == 4 and not rg) and not (u > 1 and pf)]
 
 
 @pytest.mark.parametrize("bpc,u,nt,pf,rg,ch", VARIANTS)

@@ -78,6 +78,40 @@ __global__ __launch_bounds__(256) void k_rmw8(f4* __restrict__ x, int64_t ld4, f
     }
 }
 
+// N rows of ldv VEC-float vectors, in place; each lane loads its column of every row, then stores
+template <int N, int VEC>
+__global__ __launch_bounds__(256) void k_rmwN(float* __restrict__ x, int64_t ldv, float a) {
+    typedef float vt __attribute__((ext_vector_type(VEC)));
+    vt* X = reinterpret_cast<vt*>(x);
+    for (int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x; c < ldv; c += (int64_t)gridDim.x * 256) {
+        vt v[N];
+#pragma unroll
+        for (int r = 0; r < N; ++r) v[r] = __builtin_nontemporal_load(X + r * ldv + c);
+#pragma unroll
+        for (int r = 0; r < N; ++r) __builtin_nontemporal_store(v[r] * a, X + r * ldv + c);
+    }
+}
+
+// 8 rows, U quads per lane per row per tile (per-row contiguous chunk of U*4 KB per block); ROT:
+// block b visits the rows starting at row b % 8 (staggers which row the chip hits first)
+template <int U, bool ROT>
+__global__ __launch_bounds__(256) void k_rmw8u(f4* __restrict__ x, int64_t ld4, float a) {
+    const int64_t tile = 256 * U;
+    const int r0 = ROT ? (int)(blockIdx.x & 7) : 0;
+    for (int64_t b = (int64_t)blockIdx.x * tile; b < ld4; b += (int64_t)gridDim.x * tile) {
+        f4 v[8][U];
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr)
+#pragma unroll
+            for (int u = 0; u < U; ++u) v[rr][u] = __builtin_nontemporal_load(x + ((rr + r0) & 7) * ld4 + b + u * 256 + threadIdx.x);
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr)
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                __builtin_nontemporal_store(v[rr][u] * a, x + ((rr + r0) & 7) * ld4 + b + u * 256 + threadIdx.x);
+    }
+}
+
 template <bool NT, int U>
 __global__ __launch_bounds__(256) void k_read(const f4* __restrict__ s, float* out, int64_t n4) {
     const int64_t tile = 256 * U;
@@ -160,6 +194,7 @@ int main() {
     }
     // rmw8 with padded row strides: does the distance between the 8 rows matter (channel mapping)?
     for (int bpc : {3, 4, 5, 6}) {
+        if (getenv("PROBE_WIDE")) break;
         const int grid = cus * bpc;
         for (int64_t pad4 : {0, 16, 64, 192, 256, 1024, 4096 + 64, 65536 + 256}) {
             const int64_t ld4 = P / 4 + pad4;
@@ -170,6 +205,28 @@ int main() {
         }
         report("rmw1", bpc, 1, 1, round_bytes,
                time_ms([&] { hipLaunchKernelGGL((k_rmw1<true, 1>), dim3(grid), dim3(256), 0, 0, A, n4, 1.0f); }));
+    }
+    // many rows, small per-row chunks (the wide-slot mixing layouts)
+    if (getenv("PROBE_WIDE")) {
+        const int64_t total = rows * P;   // same 819.2 MB arena
+        for (int bpc : {2, 4, 8}) {
+            const int grid = cus * bpc;
+#define RW(N, V)                                                                                   \
+    report("rmw" #N "_vec" #V, bpc, 1, V, round_bytes, time_ms([&] {                             \
+        hipLaunchKernelGGL((k_rmwN<N, V>), dim3(grid), dim3(256), 0, 0, (float*)A, total / N / V, 1.0f); \
+    }))
+            RW(8, 4); RW(16, 4); RW(16, 2); RW(32, 4); RW(32, 2); RW(32, 1); RW(64, 2); RW(64, 1);
+#undef RW
+#define RU(U, ROT)                                                                                 \
+    report("rmw8_U" #U "_rot" #ROT, bpc, 1, U, round_bytes, time_ms([&] {                        \
+        hipLaunchKernelGGL((k_rmw8u<U, ROT>), dim3(grid), dim3(256), 0, 0, A, P / 4, 1.0f);        \
+    }))
+            RU(1, false); RU(2, false); RU(4, false); RU(1, true); RU(2, true); RU(4, true);
+#undef RU
+            report("rmw1", bpc, 1, 1, round_bytes,
+                   time_ms([&] { hipLaunchKernelGGL((k_rmw1<true, 1>), dim3(grid), dim3(256), 0, 0, A, n4, 1.0f); }));
+        }
+        return 0;
     }
     report("hipMemcpyDtoD", 0, 0, 0, round_bytes,
            time_ms([&] { CK(hipMemcpyAsync(B, A, n4 * 16, hipMemcpyDeviceToDevice, 0)); }));
