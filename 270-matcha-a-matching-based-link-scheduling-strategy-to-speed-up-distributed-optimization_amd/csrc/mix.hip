@@ -400,6 +400,7 @@ struct Tune {
     int prefetch = 0;
     int regidx = 1;      // 1: register-indexed kernel (n_slots <= 8; wider spills), 0: LDS-column kernel
     int chunked = 0;     // single-segment layouts: 1 = equal contiguous chunk per workgroup, 0 = tile stride
+    int grid = 0;        // > 0: exact persistent grid size (overrides blocks_per_cu)
 };
 Tune g_tune;
 
@@ -423,7 +424,7 @@ int cu_count() {
 // grid: CUs x blocks_per_cu persistent workgroups, never more than there are tiles; a single
 // segment is split into equal contiguous chunks (chunked = 1)
 inline int64_t grid_for(int64_t total_tiles) {
-    int64_t grid = (int64_t)cu_count() * g_tune.blocks_per_cu;
+    int64_t grid = g_tune.grid > 0 ? (int64_t)g_tune.grid : (int64_t)cu_count() * g_tune.blocks_per_cu;
     if (grid > total_tiles) grid = total_tiles;
     return grid < 1 ? 1 : grid;
 }
@@ -475,6 +476,9 @@ extern "C" int mx_mix_set(const char* key, int value) {
     } else if (!strcmp(key, "regidx")) {
         slot = &g_tune.regidx;
         value = value ? 1 : 0;
+    } else if (!strcmp(key, "grid")) {
+        MX_CHECK(value >= 0 && value <= 65536, "mx_mix_set: grid %d", value);
+        slot = &g_tune.grid;
     } else if (!strcmp(key, "chunked")) {
         slot = &g_tune.chunked;
         value = value ? 1 : 0;
@@ -492,6 +496,7 @@ extern "C" int mx_mix_get(const char* key) {
     if (!strcmp(key, "prefetch")) return g_tune.prefetch;
     if (!strcmp(key, "regidx")) return g_tune.regidx;
     if (!strcmp(key, "chunked")) return g_tune.chunked;
+    if (!strcmp(key, "grid")) return g_tune.grid;
     mx::set_error("mx_mix_get: unknown key '%s'", key);
     return MX_ERR_INVALID;
 }

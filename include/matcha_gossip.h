@@ -93,11 +93,13 @@ int mx_plan_build(const uint8_t* flags_dev, int64_t T, int M, const int32_t* par
 int mx_mix_tile(int n_slots);
 /* Tuning knobs of the mixing kernel (process-wide), by name:
  *   blocks_per_cu  persistent workgroups per CU (grid = CUs x this, capped by the tile count)
- *   unroll         16-byte accesses per lane per slot per iteration, 1 or 2 (LDS kernel, n_slots <= 8)
+ *   unroll         16-byte accesses per lane per slot per iteration, n_slots <= 8: 1, 2 or 4
+ *                  (register-indexed kernel), 1 or 2 (LDS kernel)
  *   nontemporal    streaming (non-temporal) load/store hints
  *   prefetch       issue the next iteration's loads before mixing/storing the current one
  *   regidx         register-indexed kernel (no LDS) instead of the LDS-column one, n_slots <= 8
  *   chunked        single-segment layouts: equal contiguous chunk per workgroup (1) or tile stride (0)
+ *   grid           > 0: exact persistent grid size (overrides blocks_per_cu); 0 = CUs x blocks_per_cu
  * "unroll" changes the tile size: rebuild layouts (mx_mix_layout) after setting it.
  * mx_mix_get returns the current value (negative on an unknown key). */
 int mx_mix_set(const char* key, int value);

@@ -36,16 +36,17 @@ def timeit(fn, reps=40, warm=5):
     return float(np.median(ms)), float(ms.min())
 
 
-KEYS = ("blocks_per_cu", "unroll", "nontemporal", "prefetch", "regidx", "chunked")
+KEYS = ("blocks_per_cu", "unroll", "nontemporal", "prefetch", "regidx", "chunked", "grid")
 configs = []
 for spec in sys.argv[1:] or ["sweep"]:
     if spec == "sweep":
         for rg, pf in ((0, 0), (0, 1), (1, 0), (1, 1)):
             for ch in (0, 1):
                 for bpc in (3, 4, 5, 6, 8):
-                    configs.append((bpc, 1, 1, pf, rg, ch))
+                    configs.append((bpc, 1, 1, pf, rg, ch, 0))
     else:
-        configs.append(tuple(int(x) for x in spec.split(",")))
+        cfg = tuple(int(x) for x in spec.split(","))
+        configs.append(cfg + (0,) * (len(KEYS) - len(cfg)))
 src = torch.empty((n, P), device="cuda")
 dst = torch.empty_like(src)
 refs = []
@@ -56,7 +57,7 @@ for cfg in configs:
     pkg.engine.set_mix_tuning(**dict(zip(KEYS, cfg)))
     lay = pkg.Layout([P], [[grp.arena[r].data_ptr()] for r in range(n)], grp.engine.n_slots)
     med, mn = timeit(lambda: grp.engine.mix(0, lay))
-    res.append({"cfg": "bpc=%d U=%d NT=%d PF=%d REG=%d CH=%d" % cfg, "med_us": med * 1e3, "min_us": mn * 1e3,
+    res.append({"cfg": "bpc=%d U=%d NT=%d PF=%d REG=%d CH=%d GRID=%d" % cfg, "med_us": med * 1e3, "min_us": mn * 1e3,
                 "TBps": BYTES / med / 1e9, "frac": BYTES / med / 1e9 / 8.0})
     print(json.dumps(res[-1]), flush=True)
 med, mn = timeit(lambda: dst.copy_(src))
