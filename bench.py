@@ -38,6 +38,11 @@ def parse():
     ap.add_argument("--budget", type=float, default=1.0, help="1.0 = full rounds (headline)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--choco", type=int, default=1, help="also time ChocoSGD rounds (VGG-16 size, top-1%%)")
+    ap.add_argument("--choco-params", type=int, default=14_774_436, help="Choco figure row size (VGG-16)")
+    ap.add_argument("--transport", choices=("rccl", "gloo"), default="rccl",
+                    help="N > 1 partner exchange: rccl (the product path, one GPU per rank) or gloo "
+                         "(tests/gloo_transport.py: host staging, lets N ranks share one GPU to test "
+                         "the multi-process path; never a performance number)")
     return ap.parse_args()
 
 
@@ -77,12 +82,21 @@ def pmc_traffic(kernel_prefix="mix_kernel"):
     return (max(vals) if vals else None), os.path.relpath(files[-1], ROOT)
 
 
-def choco_figure(pkg, GP, rank, world, K, W, P=14_774_436, ratio=0.99, gamma=0.1):
+def max_over_ranks(x, world, dev):
+    import torch.distributed as dist
+    if world == 1:
+        return x
+    t = torch.tensor([x], device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99, gamma=0.1):
     """Secondary figure: ChocoSGD rounds (BASELINE config: VGG-16 size, top-1 %, graph 0, every
     matching active) on the same GPUs -- top-k compress + [N > 1] message exchange + fused apply."""
     import torch.distributed as dist
     grp = pkg.ChocoWorkerGroup(GP, numel=P, ratio=ratio, consensus_lr=gamma, rank=rank, nranks=world,
-                               comm=None if world == 1 else pkg.engine.default_comm())
+                               comm=comm)
     for r in range(grp.n_local):
         pkg._lib.check(pkg.lib.mx_synth_fill(grp.rows[r].data_ptr(), P, 1234 + grp.row_base + r, None))
     for it in range(W):
@@ -96,12 +110,8 @@ def choco_figure(pkg, GP, rank, world, K, W, P=14_774_436, ratio=0.99, gamma=0.1
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    el = time.perf_counter() - t
-    if world > 1:
-        tt = torch.tensor([el], device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        el = float(tt.item())
-    out = {"config": f"VGG-16 size P={P}, ratio {ratio} (k={grp.k}), gamma {gamma}, graph 0 full rounds",
+    el = max_over_ranks(time.perf_counter() - t, world, dev)
+    out = {"config": f"P={P} (VGG-16 size by default), ratio {ratio} (k={grp.k}), gamma {gamma}, graph 0 full rounds",
            "rounds_per_s": K / el, "ms_per_round": 1e3 * el / K}
     del grp
     torch.cuda.empty_cache()
@@ -126,18 +136,32 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
-    torch.cuda.set_device(local)
     import torch.distributed as dist
-    if world > 1:
+    gloo = args.transport == "gloo"
+    if gloo:
+        local = local % torch.cuda.device_count()
+    torch.cuda.set_device(local)
+    if world > 1 and gloo:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    elif world > 1:
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    dev = "cpu" if gloo else "cuda"
     import importlib
     pkg = importlib.import_module(PKG_NAME)
+    comm = None
+    if world > 1:
+        if gloo:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            from gloo_transport import GlooTransport
+            comm = GlooTransport(pkg)
+        else:
+            comm = pkg.engine.default_comm()
 
     n, P = args.workers, args.params
     K, W = args.steps, args.warmup
     np.random.seed(1234)
     GP = pkg.MatchaProcessor(pkg.select_graph(args.graph), args.budget, rank, n, W + 2 * K, True)
-    group = pkg.VirtualWorkerGroup(GP, numel=P, rank=rank, nranks=world)
+    group = pkg.VirtualWorkerGroup(GP, numel=P, rank=rank, nranks=world, comm=comm)
     for r in range(group.n_local):
         pkg._lib.check(pkg.lib.mx_synth_fill(group.rows[r].data_ptr(), P, 1234 + group.row_base + r, None))
     torch.cuda.synchronize()
@@ -156,10 +180,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     step_ms = np.array([a.elapsed_time(b) for a, b in ev])
-    if world > 1:
-        tt = torch.tensor([elapsed], device="cuda")
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    elapsed = max_over_ranks(elapsed, world, dev)
     # mixing kernel alone (N > 1: without the RCCL exchange) -> its HBM roofline
     stream = torch.cuda.current_stream()
     mev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
@@ -174,7 +195,7 @@ def main():
     if args.budget >= 1.0:
         np.random.seed(1234)
         GPm = pkg.MatchaProcessor(pkg.select_graph(args.graph), 0.5, rank, n, W + K, True)
-        gm = pkg.VirtualWorkerGroup(GPm, numel=P, rank=rank, nranks=world, comm=group.engine.comm)
+        gm = pkg.VirtualWorkerGroup(GPm, numel=P, rank=rank, nranks=world, comm=comm)
         for r in range(gm.n_local):
             pkg._lib.check(pkg.lib.mx_synth_fill(gm.rows[r].data_ptr(), P, 1234 + gm.row_base + r, None))
         for it in range(W):
@@ -188,18 +209,15 @@ def main():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        el = time.perf_counter() - t1
-        if world > 1:
-            tt = torch.tensor([el], device="cuda")
-            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-            el = float(tt.item())
+        el = max_over_ranks(time.perf_counter() - t1, world, dev)
         fl = np.asarray(GPm.active_flags[W:W + K])
         matcha = {"budget": 0.5, "rounds_per_s": K / el, "probabilities": [round(float(x), 6) for x in GPm.probabilities],
                   "alpha": GPm.neighbor_weight, "mean_active_matchings": float(fl.sum(1).mean()),
                   "skipped_rounds": int((fl.sum(1) == 0).sum())}
         del gm
 
-    choco = choco_figure(pkg, GP, rank, world, max(5, K // 5), 3) if args.choco else None
+    choco = (choco_figure(pkg, GP, rank, world, max(5, K // 5), 3, comm, dev, P=args.choco_params)
+             if args.choco else None)
 
     partner = np.asarray(GP.neighbors_info, np.int32)
     flags = np.asarray(GP.active_flags[W:W + K], np.uint8)
@@ -259,7 +277,8 @@ def main():
             "config": {"workload": f"graph {args.graph} ({n} workers), P={P} fp32 per worker, "
                                    f"budget {args.budget} ({'every matching active' if args.budget >= 1 else 'MATCHA schedule'})",
                        "workers": n, "params_per_worker": P, "graph": args.graph, "budget": args.budget,
-                       "parallelism": f"{n} workers over {world} GPU(s), contiguous blocks"},
+                       "parallelism": f"{n} workers over {world} GPU(s), contiguous blocks",
+                       "transport": args.transport if world > 1 else None},
             "roofline": {"bound": "hbm", "kernel": "mix_kernel (mx_gossip_mix)",
                          "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK, "traffic": traffic,
@@ -292,6 +311,8 @@ def main():
         print(json.dumps(out))
     if world > 1:
         dist.barrier()
+        if not gloo:
+            comm.close()
         dist.destroy_process_group()
 
 

@@ -1,0 +1,101 @@
+"""One rank of the multi-process GPU test (launched by tests/test_gpu_multiproc.py via torchrun).
+
+Every rank shares GPU 0 and holds a contiguous block of the topology's workers; partner rows
+cross process boundaries through tests/gloo_transport.GlooTransport (RCCL refuses two ranks on
+one GPU).  Each case runs several rounds, gathers all rows and compares them bit-exactly with the
+single-process oracle.  Exit status 0 = every case matched."""
+import importlib
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+for p in (ROOT, HERE, os.path.join(ROOT, "oracle")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+import oracle as O  # noqa: E402
+from conftest import PKG_NAME, Topo  # noqa: E402
+from gloo_transport import GlooTransport, gather_rows  # noqa: E402
+
+
+def decen_case(pkg, T, gid, P, rounds, chunk_cols=None, seed=5):
+    rank, world = dist.get_rank(), dist.get_world_size()
+    n = pkg.GRAPH_SIZES[gid]
+    gp = pkg.GraphProcessor(pkg.select_graph(gid), 1.0, 0, n, 4, True)
+    M = len(gp.neighbors_info)
+    rng = np.random.RandomState(seed)
+    flags = (rng.uniform(size=(rounds, M)) < 0.6).astype(np.uint8)
+    flags[0] = 1
+    topo = Topo(gp.neighbors_info, 0.21, flags)
+    grp = pkg.VirtualWorkerGroup(topo, numel=P, rank=rank, nranks=world, comm=T, chunk_cols=chunk_cols)
+    X = np.stack([O.synth(77 + i, P) for i in range(n)])
+    grp.rows.copy_(torch.from_numpy(X[grp.row_base:grp.row_base + grp.n_local]))
+    for it in range(rounds):
+        grp.communicate()
+        if flags[it].any():
+            X = O.decen_round(X, topo.neighbors_info, flags[it], 0.21)
+    got = gather_rows(grp.rows, grp.row_base, n)
+    return bool(np.array_equal(got.view(np.uint32), X.view(np.uint32)))
+
+
+def choco_case(pkg, T, P, ratio, rounds, seed=9):
+    rank, world = dist.get_rank(), dist.get_world_size()
+    n = 8
+    gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, n, 4, True)
+    M = len(gp.neighbors_info)
+    rng = np.random.RandomState(seed)
+    flags = (rng.uniform(size=(rounds, M)) < 0.6).astype(np.uint8)
+    flags[0] = 1
+    topo = Topo(gp.neighbors_info, 2 / 7, flags)
+    grp = pkg.ChocoWorkerGroup(topo, numel=P, ratio=ratio, consensus_lr=0.1, rank=rank, nranks=world, comm=T)
+    X = np.stack([O.synth(99 + i, P) for i in range(n)])
+    XH = np.zeros_like(X)
+    S = np.zeros_like(X)
+    grp.rows.copy_(torch.from_numpy(X[grp.row_base:grp.row_base + grp.n_local]))
+    for it in range(rounds):
+        grp.communicate()
+        if flags[it].any():
+            O.choco_round(X, XH, S, np.asarray(topo.neighbors_info, np.int32), flags[it], 2 / 7, grp.k, 0.1)
+    got = gather_rows(grp.rows, grp.row_base, n)
+    gxh = gather_rows(grp.x_hat[:, :P], grp.row_base, n)
+    return bool(np.array_equal(got.view(np.uint32), X.view(np.uint32)) and np.array_equal(gxh, XH))
+
+
+def centralized_case(pkg, T):
+    rank, world = dist.get_rank(), dist.get_world_size()
+    m = torch.nn.Linear(7, 5).cuda()
+    with torch.no_grad():
+        for p in m.parameters():
+            p.copy_(torch.full_like(p, float(rank + 1)))
+    pkg.centralizedCommunicator(rank, world, transport=T).communicate(m)
+    want = sum(range(1, world + 1)) / world
+    return all(bool(torch.all(p == want)) for p in m.parameters())
+
+
+def main():
+    dist.init_process_group("gloo")
+    torch.cuda.set_device(0)
+    pkg = importlib.import_module(PKG_NAME)
+    T = GlooTransport(pkg)
+    res = {
+        "decen_g0": decen_case(pkg, T, 0, 30_011, 5),
+        "decen_g2": decen_case(pkg, T, 2, 9_001, 4),
+        "decen_g0_chunked": decen_case(pkg, T, 0, 70_001, 4, chunk_cols=16_384),
+        "choco_g0": choco_case(pkg, T, 40_003, 0.9, 4),
+        "centralized": centralized_case(pkg, T),
+    }
+    torch.cuda.synchronize()
+    if dist.get_rank() == 0:
+        print(json.dumps({"world": dist.get_world_size(), **res}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+    sys.exit(0 if all(res.values()) else 1)
+
+
+if __name__ == "__main__":
+    main()
