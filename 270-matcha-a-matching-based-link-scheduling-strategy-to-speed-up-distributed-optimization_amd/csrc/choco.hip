@@ -265,8 +265,10 @@ __global__ __launch_bounds__(kTPB) void select_lo(Rows R, int64_t S, double frac
     }
 }
 
-// ---- B: one block per chunk; keys with top digit >= b_lo -> (value, local index) in the chunk's
-// region, in index order (wave w, step j, lane l holds elements 4(c*1024 + 256w + 64j + l) .. +3).
+// ---- B: persistent blocks, one 4096-element chunk per block iteration; keys with top digit >=
+// b_lo -> (value, local index) in the chunk's region, in index order (wave w, step j, lane l
+// holds elements 4(c*1024 + 256w + 64j + l) .. +3).  The next chunk's x / x_hat loads are issued
+// before the current chunk is ranked and written, so the stream never waits on the scans.
 // cnt[4c + 0..3] = {0, candidates > T, candidates == T, candidates}.
 // fallback = 1: runs only if fewer than k candidates were kept, then keeps every key.
 __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int fallback) {
@@ -276,53 +278,82 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int fallback) {
         if (v.st->cand_n >= R.k) return;
         b_lo = 0;
     }
-    __shared__ uint32_t wtot[kWaves];
+    __shared__ uint32_t wtot[2][kWaves];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t c = blockIdx.x;
+    const int64_t nc = n_chunks(R.P);
     const bool vec = (((uintptr_t)v.x | (uintptr_t)v.xh) & 15) == 0;
-    const int64_t q0 = c * (kChunk / 4) + wave * kSubQuads;
-    float d[4][4];
-    uint32_t keep = 0;                           // bit 4j + e: element e of step j is kept
-    uint32_t incl[4], m[4];
-    uint32_t tot = 0;
+    const f4* x4 = reinterpret_cast<const f4*>(v.x);
+    const f4* h4 = reinterpret_cast<const f4*>(v.xh);
+    auto whole = [&](int64_t c) { return vec && (c + 1) * kChunk <= R.P; };
+    f4 ax[4], ah[4];                               // raw loads of the next full chunk
+    auto issue = [&](int64_t c) {
+        const int64_t q0 = c * (kChunk / 4) + wave * kSubQuads + lane;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int n = load_quad(v.x, v.xh, q0 + j * 64 + lane, R.P, vec, d[j]);
-        m[j] = 0;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            const bool f = e < n && (key_of(d[j][e]) >> kTopShift) >= b_lo;
-            keep |= (f ? 1u : 0u) << (4 * j + e);
-            m[j] += f;
+        for (int j = 0; j < 4; ++j) {
+            ax[j] = __builtin_nontemporal_load(x4 + q0 + j * 64);
+            ah[j] = h4 ? __builtin_nontemporal_load(h4 + q0 + j * 64) : f4{0.0f, 0.0f, 0.0f, 0.0f};
         }
-        incl[j] = wave_incl_scan(m[j]);
-        tot += __shfl(incl[j], 63, 64);
-    }
-    if (lane == 0) wtot[wave] = tot;
-    __syncthreads();
-    uint32_t pos = 0, all = 0;
-    for (int w = 0; w < kWaves; ++w) {
-        pos += w < wave ? wtot[w] : 0;
-        all += wtot[w];
-    }
-    float* cv = v.cval + c * kChunk;
-    uint16_t* cl = v.cloc + c * kChunk;
+    };
+    int64_t c = blockIdx.x;
+    if (c < nc && whole(c)) issue(c);
+    for (int par = 0; c < nc; c += gridDim.x, par ^= 1) {
+        float d[4][4];
+        int n[4];
+        if (whole(c)) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        uint32_t p = pos + incl[j] - m[j];
+            for (int j = 0; j < 4; ++j) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-            if ((keep >> (4 * j + e)) & 1u) {
-                cv[p] = d[j][e];
-                cl[p] = (uint16_t)(kSub * wave + 4 * (64 * j + lane) + e);
-                ++p;
+                for (int e = 0; e < 4; ++e) d[j][e] = h4 ? __fsub_rn(ax[j][e], ah[j][e]) : ax[j][e];
+                n[j] = 4;
             }
+        } else {
+            const int64_t q0 = c * (kChunk / 4) + wave * kSubQuads;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) n[j] = load_quad(v.x, v.xh, q0 + j * 64 + lane, R.P, vec, d[j]);
         }
-        pos += __shfl(incl[j], 63, 64);
-    }
-    if (threadIdx.x == 0) {
-        v.cnt[4 * c + 0] = 0;
-        v.cnt[4 * c + 3] = all;
+        const int64_t cn = c + gridDim.x;
+        if (cn < nc && whole(cn)) issue(cn);
+        uint32_t keep = 0;                           // bit 4j + e: element e of step j is kept
+        uint32_t incl[4], m[4];
+        uint32_t tot = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            m[j] = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const bool f = e < n[j] && (key_of(d[j][e]) >> kTopShift) >= b_lo;
+                keep |= (f ? 1u : 0u) << (4 * j + e);
+                m[j] += f;
+            }
+            incl[j] = wave_incl_scan(m[j]);
+            tot += __shfl(incl[j], 63, 64);
+        }
+        if (lane == 0) wtot[par][wave] = tot;
+        __syncthreads();                             // double-buffered by parity: one barrier
+        uint32_t pos = 0, all = 0;
+        for (int w = 0; w < kWaves; ++w) {
+            pos += w < wave ? wtot[par][w] : 0;
+            all += wtot[par][w];
+        }
+        float* cv = v.cval + c * kChunk;
+        uint16_t* cl = v.cloc + c * kChunk;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            uint32_t p = pos + incl[j] - m[j];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                if ((keep >> (4 * j + e)) & 1u) {
+                    cv[p] = d[j][e];
+                    cl[p] = (uint16_t)(kSub * wave + 4 * (64 * j + lane) + e);
+                    ++p;
+                }
+            }
+            pos += __shfl(incl[j], 63, 64);
+        }
+        if (threadIdx.x == 0) {
+            v.cnt[4 * c + 0] = 0;
+            v.cnt[4 * c + 3] = all;
+        }
     }
 }
 
@@ -544,10 +575,12 @@ __global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, floa
     const int tid = threadIdx.x;
     const bool vec = len == kTile && (((uintptr_t)xr | (uintptr_t)sr | (uintptr_t)hr) & 15) == 0;
     constexpr int kQ = kTile / 4 / kTPB;       // quads per lane
-    if (vec) {
+    f4 xv[kQ];                                 // x is loaded up front: its stream overlaps the
+    if (vec) {                                 // message phase instead of following it
 #pragma unroll
         for (int j = 0; j < kQ; ++j) {
             const int q = j * kTPB + tid;
+            xv[j] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(xr) + q);
             reinterpret_cast<f4*>(ls)[q] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(sr) + q);
             reinterpret_cast<f4*>(lh)[q] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(hr) + q);
         }
@@ -593,7 +626,7 @@ __global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, floa
 #pragma unroll
         for (int j = 0; j < kQ; ++j) {
             const int q = j * kTPB + tid;
-            f4 a = __builtin_nontemporal_load(reinterpret_cast<const f4*>(xr) + q);
+            f4 a = xv[j];
             const f4 sv = reinterpret_cast<const f4*>(ls)[q];
             const f4 hv = reinterpret_cast<const f4*>(lh)[q];
 #pragma unroll
@@ -620,6 +653,7 @@ unsigned clamp_grid(int64_t n, int64_t per, int64_t cap) {
 }  // namespace
 
 int g_sample_stride = 0;   // 0 = auto (about kSampleTarget sampled elements per row)
+int g_compact_blocks = 2048;  // persistent compaction blocks over all rows
 
 int64_t sample_stride(int64_t P) {
     const int64_t nc = n_chunks(P);
@@ -641,11 +675,17 @@ extern "C" int mx_topk_set(const char* key, int64_t value) {
         g_sample_stride = (int)value;
         return MX_OK;
     }
+    if (!strcmp(key, "compact_blocks")) {
+        MX_CHECK(value >= 1 && value <= (1 << 20), "mx_topk_set: compact_blocks %lld", (long long)value);
+        g_compact_blocks = (int)value;
+        return MX_OK;
+    }
     MX_CHECK(false, "mx_topk_set: unknown key '%s'", key);
 }
 
 extern "C" int64_t mx_topk_get(const char* key) {
     if (key && !strcmp(key, "sample_stride")) return g_sample_stride;
+    if (key && !strcmp(key, "compact_blocks")) return g_compact_blocks;
     mx::set_error("mx_topk_get: unknown key '%s'", key ? key : "(null)");
     return MX_ERR_INVALID;
 }
@@ -674,7 +714,7 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
     }
     const double frac = (double)sampled / (double)P;
     MX_CHECK(nc <= 0x7fffffff, "mx_topk_abs_diff_rows: P too large");
-    const unsigned bgrid = (unsigned)nc;                                       // one block per chunk
+    const unsigned bgrid = clamp_grid(nc, 1, (g_compact_blocks + nrows - 1) / nrows);   // persistent
     const unsigned wgrid = (unsigned)((nc + kWaves - 1) / kWaves);          // one wave per chunk
     const unsigned sgrid = clamp_grid(nsamp, 4 * kWaves, (1024 + nrows - 1) / nrows);
     const unsigned cgrid = clamp_grid(wgrid, 2, (2048 + nrows - 1) / nrows);

@@ -21,6 +21,8 @@ gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, n, 4, True)
 K = 20
 topo = Topo(gp.neighbors_info, 2 / 7, np.ones((K + 5, 5), np.uint8))
 grp = pkg.ChocoWorkerGroup(topo, numel=P, ratio=ratio, consensus_lr=0.1)
+if os.environ.get("CHOCO_COMPACT_BLOCKS"):
+    pkg._lib.check(pkg.lib.mx_topk_set(b"compact_blocks", int(os.environ["CHOCO_COMPACT_BLOCKS"])))
 for i in range(n):
     pkg.lib.mx_synth_fill(grp.rows[i].data_ptr(), P, 1234 + i, None)
 for it in range(5):
@@ -41,6 +43,6 @@ deg = np.zeros(n, int)
 for g in range(5):
     deg += np.asarray(gp.neighbors_info[g]) >= 0
 alg = int(n * (8 * P + 16 * P) + sum(int(d + 1) * k * (12 + 8) + k * 8 for d in deg))
-print(json.dumps({"P": P, "ratio": ratio, "k": k, "round_ms_median": float(np.median(ms)),
+print(json.dumps({"compact_blocks": int(pkg.lib.mx_topk_get(b"compact_blocks")), "P": P, "ratio": ratio, "k": k, "round_ms_median": float(np.median(ms)),
                   "round_ms_min": float(ms.min()), "rounds_per_s": 1e3 / float(np.median(ms)),
                   "alg_bytes_min": alg, "eff_TBps": alg / (np.median(ms) * 1e-3) / 1e12}))
