@@ -190,6 +190,22 @@ def main():
         mev[j][1].record(stream)
     torch.cuda.synchronize()
     mix_ms = np.array([a.elapsed_time(b) for a, b in mev])
+    # same-box context for the roofline fraction: torch's copy_ of the same bytes (read + write of
+    # the active rows), timed the same way right after the mixing launches
+    ref_copy_ms = None
+    if world == 1:
+        nbytes = group.n_local * P * 4
+        src_t = torch.empty(nbytes // 4, dtype=torch.float32, device="cuda")
+        dst_t = torch.empty_like(src_t)
+        dst_t.copy_(src_t)
+        cev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
+        for a, b in cev:
+            a.record(stream)
+            dst_t.copy_(src_t)
+            b.record(stream)
+        torch.cuda.synchronize()
+        ref_copy_ms = float(np.mean([a.elapsed_time(b) for a, b in cev]))
+        del src_t, dst_t
     # secondary figure: a MATCHA C_b = 0.5 schedule on the same workers (random subsets per round)
     matcha = None
     if args.budget >= 1.0:
@@ -284,6 +300,8 @@ def main():
                          "frac": achieved / HBM_PEAK, "traffic": traffic,
                          "traffic_source": traffic_src, "bytes_per_launch": mix_bytes,
                          "avg_launch_ms": mix_avg_ms,
+                         "same_box_torch_copy_ms": ref_copy_ms,
+                         "vs_same_box_copy": (ref_copy_ms / mix_avg_ms) if ref_copy_ms else None,
                          "tuning": pkg.engine.mix_tuning(),
                          "note": "achieved = algorithmic bytes (2 x active rows x P x 4 [+ slab rows]) / "
                                  "mean per-launch duration, HIP events on the launch stream"},
