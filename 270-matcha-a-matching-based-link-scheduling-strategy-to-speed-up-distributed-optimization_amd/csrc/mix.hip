@@ -184,6 +184,7 @@ __global__ __launch_bounds__(kTPB) void mix_kernel(float* const* __restrict__ se
     const float* sw = reinterpret_cast<const float*>(deg + n_local);
     const int32_t* src = deg + 2 * n_local;
     int dg[NS];                               // wave-uniform degrees (0 beyond n_local)
+    const int dgv = (threadIdx.x & 63) < n_local ? deg[threadIdx.x & 63] : 0;   // lane r: row r's degree
     int maxd = 0;
 #pragma unroll
     for (int r = 0; r < NS; ++r) {
@@ -192,7 +193,7 @@ __global__ __launch_bounds__(kTPB) void mix_kernel(float* const* __restrict__ se
     }
 
     Sched sc;
-    sc.init<VEC, U>(chunked != 0, nseg, seg_len, tile_off, total_tiles);
+    sc.init<VEC, U>((chunked & 1) != 0, nseg, seg_len, tile_off, total_tiles);
     if (sc.niter == 0) return;
     F v[NS][U];
     auto load_all = [&](int seg, int64_t g, int64_t lim) {
@@ -234,16 +235,41 @@ __global__ __launch_bounds__(kTPB) void mix_kernel(float* const* __restrict__ se
             for (int u = 0; u < U; ++u)
 #pragma unroll
                 for (int j = 0; j < VEC; ++j) acc[r][u][j] = 0.0f;
-        for (int e = 0; e < maxd; ++e) {
+        if (NS >= 16 && (chunked & 2)) {
+            // One LDS read per step fetches every row's e-th slot at once (lane r holds row r's,
+            // -1 past its degree); v_readlane hands each row its slot as a scalar with no memory
+            // round trip, and rows past their degree keep their accumulator through a select.
+            const int lr = tid & 63;
+            for (int e = 0; e < maxd; ++e) {
+                const int myv = (lr < n_local && e < dgv) ? src[lr * M + e] : -1;
 #pragma unroll
-            for (int r = 0; r < NS; ++r) {
-                if (e < dg[r]) {
-                    const int sl = __builtin_amdgcn_readfirstlane(src[r * M + e]);
+                for (int r = 0; r < NS; ++r) {
+                    const int sl = __builtin_amdgcn_readlane(myv, r);
+                    const bool on = sl >= 0;
+                    const int sa = on ? sl : 0;
 #pragma unroll
                     for (int u = 0; u < U; ++u) {
-                        const F x = lds[sl][u][tid];
+                        const F x = lds[sa][u][tid];
 #pragma unroll
-                        for (int j = 0; j < VEC; ++j) acc[r][u][j] = __builtin_fmaf(alpha, x[j], acc[r][u][j]);
+                        for (int j = 0; j < VEC; ++j) {
+                            const float f = __builtin_fmaf(alpha, x[j], acc[r][u][j]);
+                            acc[r][u][j] = on ? f : acc[r][u][j];
+                        }
+                    }
+                }
+            }
+        } else {
+            for (int e = 0; e < maxd; ++e) {
+#pragma unroll
+                for (int r = 0; r < NS; ++r) {
+                    if (e < dg[r]) {
+                        const int sl = __builtin_amdgcn_readfirstlane(src[r * M + e]);
+#pragma unroll
+                        for (int u = 0; u < U; ++u) {
+                            const F x = lds[sl][u][tid];
+#pragma unroll
+                            for (int j = 0; j < VEC; ++j) acc[r][u][j] = __builtin_fmaf(alpha, x[j], acc[r][u][j]);
+                        }
                     }
                 }
             }
@@ -401,6 +427,7 @@ struct Tune {
     int regidx = 1;      // 1: register-indexed kernel (n_slots <= 8; wider spills), 0: LDS-column kernel
     int chunked = 0;     // single-segment layouts: 1 = equal contiguous chunk per workgroup, 0 = tile stride
     int grid = 0;        // > 0: exact persistent grid size (overrides blocks_per_cu)
+    int readlane_min = 32;  // LDS kernel: slot counts >= this fetch a step's slots with one read + v_readlane
 };
 Tune g_tune;
 
@@ -433,9 +460,10 @@ template <int VEC, int NS, int U, bool NT, bool PF>
 int launch(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_off,
            const uint8_t* seg_vec, int nseg, int n_slots, const int32_t* plan, int64_t iter,
            int n_local, int M, float alpha, int64_t total_tiles, hipStream_t st) {
+    const int mode = ((nseg == 1 && g_tune.chunked) ? 1 : 0) | (NS >= g_tune.readlane_min ? 2 : 0);
     hipLaunchKernelGGL((mix_kernel<VEC, NS, U, NT, PF>), dim3((unsigned)grid_for(total_tiles)), dim3(kTPB),
                        0, st, seg_ptrs, seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan,
-                       iter, n_local, M, alpha, (nseg == 1 && g_tune.chunked) ? 1 : 0);
+                       iter, n_local, M, alpha, mode);
     MX_LAUNCH_CHECK();
     return MX_OK;
 }
@@ -476,6 +504,9 @@ extern "C" int mx_mix_set(const char* key, int value) {
     } else if (!strcmp(key, "regidx")) {
         slot = &g_tune.regidx;
         value = value ? 1 : 0;
+    } else if (!strcmp(key, "readlane_min")) {
+        MX_CHECK(value >= 8 && value <= 128, "mx_mix_set: readlane_min %d", value);
+        slot = &g_tune.readlane_min;
     } else if (!strcmp(key, "grid")) {
         MX_CHECK(value >= 0 && value <= 65536, "mx_mix_set: grid %d", value);
         slot = &g_tune.grid;
@@ -497,6 +528,7 @@ extern "C" int mx_mix_get(const char* key) {
     if (!strcmp(key, "regidx")) return g_tune.regidx;
     if (!strcmp(key, "chunked")) return g_tune.chunked;
     if (!strcmp(key, "grid")) return g_tune.grid;
+    if (!strcmp(key, "readlane_min")) return g_tune.readlane_min;
     mx::set_error("mx_mix_get: unknown key '%s'", key);
     return MX_ERR_INVALID;
 }

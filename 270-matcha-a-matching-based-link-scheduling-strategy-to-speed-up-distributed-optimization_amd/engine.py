@@ -22,7 +22,7 @@ from ._lib import MXError, check, lib, require_device, stream_ptr
 
 ROW_ALIGN = 64  # arena rows padded to 256 B
 
-TUNE_KEYS = ("blocks_per_cu", "unroll", "nontemporal", "prefetch", "regidx", "chunked", "grid")
+TUNE_KEYS = ("blocks_per_cu", "unroll", "nontemporal", "prefetch", "regidx", "chunked", "grid", "readlane_min")
 
 
 def mix_tuning():
