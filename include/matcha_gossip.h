@@ -101,7 +101,7 @@ int mx_mix_tile(int n_slots);
  *   chunked        single-segment layouts: equal contiguous chunk per workgroup (1) or tile stride (0)
  *   grid           > 0: exact persistent grid size (overrides blocks_per_cu); 0 = CUs x blocks_per_cu
  *   readlane_min   LDS kernel: slot-count classes >= this (16 / 32 / 64) fetch one step's slots with
- * *                  one LDS read + v_readlane and keep short chains by select (default 32)
+ *                  one LDS read + v_readlane and keep short chains by select (default 32)
  * "unroll" changes the tile size: rebuild layouts (mx_mix_layout) after setting it.
  * mx_mix_get returns the current value (negative on an unknown key). */
 int mx_mix_set(const char* key, int value);
