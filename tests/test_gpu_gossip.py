@@ -318,11 +318,16 @@ def test_mix_every_tuning_variant(pkg, O, bpc, u, nt, pf, rg, ch):
         pkg.engine.set_mix_tuning(**saved)
 
 
-@pytest.mark.parametrize("n,p,seed,P", [(32, 0.2, 7, 70_001), (64, 0.1, 1234, 50_003), (24, 0.3, 3, 9_999)])
-def test_mix_er_graphs_wide_configs(pkg, O, n, p, seed, P):
-    """Random ER topologies decomposed by the host path: 24 / 32 / 64 slots exercise the
-    (VEC 4, NS 16 / 32 / 64) LDS kernels; MATCHA-like random flags, 4 rounds, bit-exact."""
+@pytest.mark.parametrize("readlane_min", [32, 16, 128])
+@pytest.mark.parametrize("n,p,seed,P", [(32, 0.2, 7, 70_001), (64, 0.1, 1234, 50_003), (24, 0.3, 3, 9_999),
+                                        (16, 0.4, 5, 1024 * 7), (64, 0.1, 1234, 256 * 9)])
+def test_mix_er_graphs_wide_configs(pkg, O, n, p, seed, P, readlane_min):
+    """Random ER topologies decomposed by the host path: 16 / 24 / 32 / 64 slots exercise the
+    NS 16 / 32 / 64 LDS kernels with both edge-step forms (per-row lookups, one read +
+    v_readlane); MATCHA-like random flags, 4 rounds, ragged and whole-tile widths, bit-exact."""
     import random as pyrandom
+    saved = pkg.engine.mix_tuning()
+    pkg.engine.set_mix_tuning(readlane_min=readlane_min)
     pyrandom.seed(0)
     gp = pkg.GraphProcessor(pkg.erdos_renyi(n, p, seed), 1.0, 0, n, 4, False)
     M = len(gp.neighbors_info)
@@ -331,13 +336,16 @@ def test_mix_er_graphs_wide_configs(pkg, O, n, p, seed, P):
     flags = (rng.uniform(size=(4, M)) < 0.5).astype(np.uint8)
     flags[0] = 1
     topo = Topo(gp.neighbors_info, 0.05, flags)
-    grp = pkg.VirtualWorkerGroup(topo, numel=P)
-    X = np.stack([O.synth(11 * seed + i, P) for i in range(n)])
-    grp.rows.copy_(torch.from_numpy(X))
-    for f in flags:
-        grp.communicate()
-        X = O.decen_round(X, topo.neighbors_info, f, 0.05)
-    got = grp.rows.cpu().numpy()
+    try:
+        grp = pkg.VirtualWorkerGroup(topo, numel=P)
+        X = np.stack([O.synth(11 * seed + i, P) for i in range(n)])
+        grp.rows.copy_(torch.from_numpy(X))
+        for f in flags:
+            grp.communicate()
+            X = O.decen_round(X, topo.neighbors_info, f, 0.05)
+        got = grp.rows.cpu().numpy()
+    finally:
+        pkg.engine.set_mix_tuning(**saved)
     assert np.array_equal(got.view(np.uint32), X.view(np.uint32))
 
 
