@@ -60,12 +60,10 @@ class LoopbackHub:
     may be stepped one after another in one thread."""
 
     def __init__(self, nranks):
-        import ctypes
         self.nranks = nranks
         self.live = {}          # worker id -> device pointer of its current row
         self.snap = {}          # (it, worker id) -> torch tensor copy of the pre-round row
-        self.hip = ctypes.CDLL("libamdhip64.so")
-        self.hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+        self._pkg = importlib.import_module(PKG_NAME)
 
     def register(self, row_base, row_ptrs):
         for r, p in enumerate(row_ptrs):
@@ -75,7 +73,18 @@ class LoopbackHub:
         return LoopbackComm(self, rank)
 
     def copy(self, dst, src, nbytes):
-        assert self.hip.hipMemcpy(int(dst), int(src), int(nbytes), 3) == 0   # device to device
+        """device to device between raw pointers, through the library's own segment gather (so
+        the test never loads a second HIP runtime next to torch's)"""
+        import torch
+        n = int(nbytes) // 4
+        lib, _lib = self._pkg.lib, self._pkg._lib
+        ptrs = torch.tensor([int(src)], dtype=torch.int64, device="cuda")
+        off = torch.tensor([0, n], dtype=torch.int64, device="cuda")
+        tmp = torch.empty(n, dtype=torch.float32, device="cuda")
+        _lib.check(lib.mx_gather(ptrs.data_ptr(), off.data_ptr(), 1, n, tmp.data_ptr(), _lib.stream_ptr()))
+        ptrs.fill_(int(dst))
+        _lib.check(lib.mx_scatter(ptrs.data_ptr(), off.data_ptr(), 1, n, tmp.data_ptr(), _lib.stream_ptr()))
+        torch.cuda.synchronize()
 
 
 class LoopbackComm:
