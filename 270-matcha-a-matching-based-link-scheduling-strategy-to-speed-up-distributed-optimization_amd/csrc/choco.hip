@@ -8,21 +8,23 @@
 // output in index order) with ONE full streaming pass over x / x_hat:
 //   S  sample_kernel   12-bit histogram of the magnitude key's top digit (bits 19..30: exponent +
 //                      4 mantissa bits) over every S-th 1024-element piece (S = 1: all of them);
-//      select_lo       one block per row: the digit b_lo such that the sampled keys at or above it
-//                      cover k (S = 1: exactly the digit of the k-th largest key; S > 1: k scaled to
-//                      the sample, with a 25 % + 4 sigma margin);
-//   B  compact_kernel  THE full pass: one block per 4096-element chunk stores every key whose
-//                      digit is >= b_lo as (value, chunk-local index) into the chunk's own region,
-//                      in index order (wave scans + one barrier; no atomics);
+//   B  compact_kernel  THE full pass.  Every block resolves the candidate floor b_lo from the
+//                      sample (S = 1: exactly the digit of the k-th largest key; S > 1: k scaled
+//                      to the sample with a 25 % + 4 sigma margin), then, one 4096-element chunk
+//                      per block iteration, stores every key whose digit is >= b_lo as (value,
+//                      chunk-local index) into the chunk's own region in index order (wave scans
+//                      + one barrier) and counts its top digit into the 12-bit candidate histogram;
 //      count_kernel    candidates per row; compact_kernel(fallback) re-runs with b_lo = 0 in the
 //                      (sample-dependent, rare) case that fewer than k were kept -- the result is
 //                      exact either way;
-//   C  cand_hist/select_cand (12 + 10 + 9 bits) radix-select the exact threshold key T and the
-//      number of its ties to take, over the candidates only; cand_mark counts > T / == T per
-//      chunk; scan_kernel turns them into output offsets; write_cand emits the selected
-//      candidates in index order (values = x - x_hat, int64 indices).
+//   C  cand_hist<10>, cand_hist<9>: the 10- and 9-bit digits of the candidates matching the
+//      prefix resolved so far; every block of a pass re-resolves the previous histograms itself
+//      (find_bin, read-only), so no one-block select launches sit between the passes;
+//      cand_mark resolves the exact threshold key T and the number of its ties to take, and
+//      counts > T / == T per chunk; scan_kernel turns them into output offsets; write_cand emits
+//      the selected candidates in index order (values = x - x_hat, int64 indices).
 // Everything stays on the device; no host round trip.  All local workers' rows are processed by
-// the same launches (blockIdx.y = row).
+// the same launches (blockIdx.y = row): 10 launches per round for any number of rows.
 #include "mx_common.h"
 
 namespace {
@@ -38,12 +40,12 @@ constexpr int kLowBits = 9;                  // bits 0..8
 constexpr int kScanTPB = 1024;
 constexpr int64_t kSampleTarget = 1 << 18;   // sampled elements per row (auto stride)
 
+constexpr int kHistWords = 2 * kTopBins + (1 << kMidBits) + (1 << kLowBits);   // hs, h12, h10, h9
+
 struct SelState {
     uint32_t b0;          // lowest top digit kept as a candidate (b_lo)
-    uint32_t T;           // exact threshold key (after the candidate passes)
-    uint32_t prefix;      // candidate-pass prefix (bits fixed so far, shifted to full key)
-    uint32_t mask;
-    int64_t need;         // keys still to take at/below the current bin / prefix
+    uint32_t T;           // exact threshold key (cand_mark)
+    int64_t need;         // ties of T to take (cand_mark)
     int64_t cand_n;       // candidates kept by compact_kernel
 };
 
@@ -58,7 +60,7 @@ __host__ __device__ inline WorkLayout layout(int64_t P) {
     const int64_t nc = n_chunks(P);
     WorkLayout w;
     w.hist = 0;
-    w.state = w.hist + sizeof(uint32_t) * kTopBins;
+    w.state = w.hist + sizeof(uint32_t) * kHistWords;
     w.cnt = w.state + 64;
     w.off = w.cnt + sizeof(int64_t) * 4 * (size_t)nc;
     w.cval = (w.off + sizeof(int64_t) * 2 * (size_t)nc + 255) / 256 * 256;
@@ -83,7 +85,10 @@ struct Rows {
 struct RowView {
     const float* x;
     const float* xh;
-    uint32_t* hist;
+    uint32_t* hs;         // sampled top digits
+    uint32_t* h12;        // candidates' top digits
+    uint32_t* h10;        // next 10 bits of the candidates in the threshold bin
+    uint32_t* h9;         // last 9 bits
     SelState* st;
     int64_t* cnt;
     int64_t* off;
@@ -100,7 +105,10 @@ __device__ __forceinline__ RowView row_view(const Rows& R) {
     RowView v;
     v.x = R.x + (int64_t)r * R.ld;
     v.xh = R.xh ? R.xh + (int64_t)r * R.ld : nullptr;
-    v.hist = reinterpret_cast<uint32_t*>(wb + w.hist);
+    v.hs = reinterpret_cast<uint32_t*>(wb + w.hist);
+    v.h12 = v.hs + kTopBins;
+    v.h10 = v.h12 + kTopBins;
+    v.h9 = v.h10 + (1 << kMidBits);
     v.st = reinterpret_cast<SelState*>(wb + w.state);
     v.cnt = reinterpret_cast<int64_t*>(wb + w.cnt);
     v.off = reinterpret_cast<int64_t*>(wb + w.off);
@@ -166,13 +174,13 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
-// zero every row's top-digit histogram (one launch for the batch)
+// zero every row's histograms (sample, 12 / 10 / 9-bit candidate digits): one launch per batch
 __global__ __launch_bounds__(kTPB) void zero_hist(Rows R) {
     const RowView v = row_view(R);
-    for (int i = threadIdx.x; i < kTopBins; i += kTPB) v.hist[i] = 0;
+    for (int i = threadIdx.x; i < kHistWords; i += kTPB) v.hs[i] = 0;
 }
 
-// ---- S: top-digit histogram over every S-th chunk, one wave per sampled chunk
+// ---- S: top-digit histogram over every S-th 1024-element piece, one wave per sampled piece
 __global__ __launch_bounds__(kTPB) void sample_kernel(Rows R, int64_t S) {
     const RowView v = row_view(R);
     __shared__ uint32_t h[kTopBins];
@@ -195,90 +203,117 @@ __global__ __launch_bounds__(kTPB) void sample_kernel(Rows R, int64_t S) {
     }
     __syncthreads();
     for (int i = threadIdx.x; i < kTopBins; i += kTPB)
-        if (h[i]) atomicAdd(&v.hist[i], h[i]);
+        if (h[i]) atomicAdd(&v.hs[i], h[i]);
 }
 
-// one block: the bin holding the need-th largest count, scanning bins from the top; bin 0 with
-// rank `need - total` when the histogram holds fewer than `need` keys.  Re-zeroes the histogram.
+// Block-wide: the bin holding the need-th largest key of a finished histogram, scanning bins from
+// the top; *rem = rank of that key inside its bin.  bin 0 / rem = need - total when the histogram
+// holds fewer than `need` keys.  Read-only (every block of a kernel resolves the same answer),
+// so no separate one-block select launch sits between the passes.
 template <int NBINS>
-__device__ void select_bin(uint32_t* __restrict__ hist, int64_t need, int* bin_out, int64_t* need_out,
-                           int64_t* total_out) {
+__device__ void find_bin(const uint32_t* __restrict__ hist, int64_t need, int* bin, int64_t* rem,
+                         int64_t* total) {
     constexpr int kPer = NBINS / kTPB;
     __shared__ int64_t part[kTPB];
+    __shared__ int s_bin;
+    __shared__ int64_t s_rem, s_total;
     const int t = threadIdx.x;
     int64_t mine = 0;
     for (int j = 0; j < kPer; ++j) mine += hist[NBINS - 1 - (t * kPer + j)];
     part[t] = mine;
     if (t == 0) {
-        *bin_out = 0;
-        *need_out = need;
+        s_bin = 0;
+        s_rem = need;
     }
     __syncthreads();
     for (int off = 1; off < kTPB; off <<= 1) {          // inclusive scan from the top bins down
-        const int64_t v = t >= off ? part[t - off] : 0;
+        const int64_t x = t >= off ? part[t - off] : 0;
         __syncthreads();
-        part[t] += v;
+        part[t] += x;
         __syncthreads();
     }
     const int64_t before = part[t] - mine;
     if (t == kTPB - 1) {
-        *total_out = part[t];
-        if (part[t] < need) *need_out = need - part[t];
+        s_total = part[t];
+        if (part[t] < need) s_rem = need - part[t];
     }
     if (before < need && part[t] >= need) {
         int64_t acc = before;
         for (int j = 0; j < kPer; ++j) {
-            const int bin = NBINS - 1 - (t * kPer + j);
-            const int64_t c = hist[bin];
+            const int b = NBINS - 1 - (t * kPer + j);
+            const int64_t c = hist[b];
             if (acc + c >= need) {
-                *bin_out = bin;
-                *need_out = need - acc;
+                s_bin = b;
+                s_rem = need - acc;
                 break;
             }
             acc += c;
         }
     }
     __syncthreads();
-    for (int i = t; i < NBINS; i += kTPB) hist[i] = 0;     // ready for the next use
+    *bin = s_bin;
+    *rem = s_rem;
+    *total = s_total;
+    __syncthreads();                                     // the shared answer may be reused
 }
 
-// one block per row: b_lo from the (sampled) top-digit histogram
-__global__ __launch_bounds__(kTPB) void select_lo(Rows R, int64_t S, double frac) {
-    const RowView v = row_view(R);
-    SelState* st = v.st;
-    __shared__ int bin;
-    __shared__ int64_t need, total;
-    int64_t want = R.k;
-    if (S > 1) {
-        const double e = (double)R.k * frac;
-        want = (int64_t)ceil(1.25 * e + 4.0 * sqrt(e) + 16.0);
+// Threshold resolved so far from the finished candidate histograms: `stages` of 12 / 10 / 9 bits.
+struct Resolved {
+    uint32_t prefix, mask;
+    int64_t need;                                        // keys still to take at/below prefix
+};
+
+__device__ Resolved resolve(const RowView& v, int64_t k, int stages) {
+    Resolved z{0u, 0u, k};
+    int b;
+    int64_t rem, tot;
+    find_bin<kTopBins>(v.h12, z.need, &b, &rem, &tot);
+    z.prefix = (uint32_t)b << kTopShift;
+    z.mask = 0xfffu << kTopShift;
+    z.need = rem;
+    if (stages >= 2) {
+        find_bin<1 << kMidBits>(v.h10, z.need, &b, &rem, &tot);
+        z.prefix |= (uint32_t)b << kMidShift;
+        z.mask |= ((1u << kMidBits) - 1) << kMidShift;
+        z.need = rem;
     }
-    select_bin<kTopBins>(v.hist, want, &bin, &need, &total);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        st->b0 = total < want ? 0u : (uint32_t)bin;     // too few sampled keys: keep everything
-        st->prefix = 0;
-        st->mask = 0;
-        st->need = R.k;
-        st->cand_n = 0;
-        st->T = 0;
+    if (stages >= 3) {
+        find_bin<1 << kLowBits>(v.h9, z.need, &b, &rem, &tot);
+        z.prefix |= (uint32_t)b;
+        z.mask = 0xffffffffu;
+        z.need = rem;
     }
+    return z;
 }
 
 // ---- B: persistent blocks, one 4096-element chunk per block iteration; keys with top digit >=
 // b_lo -> (value, local index) in the chunk's region, in index order (wave w, step j, lane l
-// holds elements 4(c*1024 + 256w + 64j + l) .. +3).  The next chunk's x / x_hat loads are issued
-// before the current chunk is ranked and written, so the stream never waits on the scans.
+// holds elements 4(c*1024 + 256w + 64j + l) .. +3), and their top digits into the 12-bit
+// candidate histogram.  b_lo comes from the sampled histogram (every block resolves it): S = 1 the
+// exact digit of the k-th largest key; S > 1 k scaled to the sample with a 25 % + 4 sigma margin.
+// The next chunk's x / x_hat loads are issued before the current chunk is ranked and written.
 // cnt[4c + 0..3] = {0, candidates > T, candidates == T, candidates}.
 // fallback = 1: runs only if fewer than k candidates were kept, then keeps every key.
-__global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int fallback) {
+__global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double frac, int fallback) {
     const RowView v = row_view(R);
-    uint32_t b_lo = v.st->b0;
+    uint32_t b_lo = 0;
     if (fallback) {
         if (v.st->cand_n >= R.k) return;
-        b_lo = 0;
+    } else {
+        int64_t want = R.k;
+        if (S > 1) {
+            const double e = (double)R.k * frac;
+            want = (int64_t)ceil(1.25 * e + 4.0 * sqrt(e) + 16.0);
+        }
+        int b;
+        int64_t rem, tot;
+        find_bin<kTopBins>(v.hs, want, &b, &rem, &tot);
+        b_lo = tot < want ? 0u : (uint32_t)b;               // too few sampled keys: keep everything
+        if (blockIdx.x == 0 && threadIdx.x == 0) v.st->b0 = b_lo;
     }
     __shared__ uint32_t wtot[2][kWaves];
+    __shared__ uint32_t h[kTopBins];
+    for (int i = threadIdx.x; i < kTopBins; i += kTPB) h[i] = 0;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t nc = n_chunks(R.P);
     const bool vec = (((uintptr_t)v.x | (uintptr_t)v.xh) & 15) == 0;
@@ -296,6 +331,7 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int fallback) {
     };
     int64_t c = blockIdx.x;
     if (c < nc && whole(c)) issue(c);
+    __syncthreads();                               // h zeroed
     for (int par = 0; c < nc; c += gridDim.x, par ^= 1) {
         float d[4][4];
         int n[4];
@@ -321,9 +357,11 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int fallback) {
             m[j] = 0;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const bool f = e < n[j] && (key_of(d[j][e]) >> kTopShift) >= b_lo;
+                const uint32_t dg = key_of(d[j][e]) >> kTopShift;
+                const bool f = e < n[j] && dg >= b_lo;
                 keep |= (f ? 1u : 0u) << (4 * j + e);
                 m[j] += f;
+                if (f) atomicAdd(&h[dg], 1u);
             }
             incl[j] = wave_incl_scan(m[j]);
             tot += __shfl(incl[j], 63, 64);
@@ -355,13 +393,18 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int fallback) {
             v.cnt[4 * c + 3] = all;
         }
     }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kTopBins; i += kTPB)
+        if (h[i]) atomicAdd(&v.h12[i], h[i]);
 }
 
-// one block per row: total candidates
+// one block per row: total candidates; if they are fewer than k the fallback pass will run, so
+// its 12-bit histogram starts from zero again
 __global__ __launch_bounds__(kScanTPB) void count_kernel(Rows R) {
     const RowView v = row_view(R);
     const int64_t nc = n_chunks(R.P);
     __shared__ int64_t ws[kScanTPB / 64];
+    __shared__ int64_t s_tot;
     int64_t s = 0;
     for (int64_t c = threadIdx.x; c < nc; c += kScanTPB) s += v.cnt[4 * c + 3];
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
@@ -371,54 +414,50 @@ __global__ __launch_bounds__(kScanTPB) void count_kernel(Rows R) {
         int64_t t = 0;
         for (int w = 0; w < kScanTPB / 64; ++w) t += ws[w];
         v.st->cand_n = t;
+        s_tot = t;
     }
+    __syncthreads();
+    if (s_tot < R.k)
+        for (int i = threadIdx.x; i < kTopBins; i += kScanTPB) v.h12[i] = 0;
 }
 
-// candidate histogram of `bits` bits at `shift`, restricted to keys matching st->prefix/mask;
-// one wave per chunk region; the block's LDS histogram is flushed once (few global atomics)
+// candidate histogram of the next digit (10 bits at 9, or 9 bits at 0) among candidates matching
+// the prefix resolved so far; one wave per chunk region; LDS histogram flushed once per block
 template <int BITS>
-__global__ __launch_bounds__(kTPB) void cand_hist(Rows R, int shift) {
+__global__ __launch_bounds__(kTPB) void cand_hist(Rows R) {
     const RowView v = row_view(R);
     constexpr int NB = 1 << BITS;
+    constexpr int stages = BITS == kMidBits ? 1 : 2;
+    constexpr int shift = BITS == kMidBits ? kMidShift : 0;
     __shared__ uint32_t h[NB];
+    const Resolved z = resolve(v, R.k, stages);
     for (int i = threadIdx.x; i < NB; i += kTPB) h[i] = 0;
     __syncthreads();
-    const uint32_t prefix = v.st->prefix, mask = v.st->mask;
     const int64_t nchunks = n_chunks(R.P);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int64_t c = (int64_t)blockIdx.x * kWaves + wave; c < nchunks; c += (int64_t)gridDim.x * kWaves) {
         const int64_t nc = v.cnt[4 * c + 3];
         for (int64_t i = lane; i < nc; i += 64) {
             const uint32_t key = key_of(v.cval[c * kChunk + i]);
-            if ((key & mask) == prefix) atomicAdd(&h[(key >> shift) & (NB - 1)], 1u);
+            if ((key & z.mask) == z.prefix) atomicAdd(&h[(key >> shift) & (NB - 1)], 1u);
         }
     }
     __syncthreads();
+    uint32_t* out = BITS == kMidBits ? v.h10 : v.h9;
     for (int i = threadIdx.x; i < NB; i += kTPB)
-        if (h[i]) atomicAdd(&v.hist[i], h[i]);
+        if (h[i]) atomicAdd(&out[i], h[i]);
 }
 
-template <int BITS>
-__global__ __launch_bounds__(kTPB) void select_cand(Rows R, int shift) {
-    const RowView v = row_view(R);
-    SelState* st = v.st;
-    constexpr int NB = 1 << BITS;
-    __shared__ int bin;
-    __shared__ int64_t need, total;
-    select_bin<NB>(v.hist, st->need, &bin, &need, &total);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        st->prefix |= (uint32_t)bin << shift;
-        st->mask |= (uint32_t)(NB - 1) << shift;
-        st->need = need;
-        if (shift == 0) st->T = st->prefix;
-    }
-}
-
-// one wave per chunk region: counts of candidates > T and == T, written without atomics
+// the exact threshold key T and how many of its ties to take; per chunk region (one wave each)
+// the counts of candidates > T and == T, written without atomics
 __global__ __launch_bounds__(kTPB) void cand_mark(Rows R) {
     const RowView v = row_view(R);
-    const uint32_t T = v.st->T;
+    const Resolved z = resolve(v, R.k, 3);
+    const uint32_t T = z.prefix;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        v.st->T = T;
+        v.st->need = z.need;
+    }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t nchunks = n_chunks(R.P);
     for (int64_t c = (int64_t)blockIdx.x * kWaves + wave; c < nchunks; c += (int64_t)gridDim.x * kWaves) {
@@ -724,18 +763,13 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
     MX_LAUNCH_CHECK()
     MX_L(zero_hist, one, kTPB);
     MX_L(sample_kernel, dim3(sgrid, nrows), kTPB, S);
-    MX_L(select_lo, one, kTPB, S, frac);
-    MX_L(compact_kernel, dim3(bgrid, nrows), kTPB, 0);
+    MX_L(compact_kernel, dim3(bgrid, nrows), kTPB, S, frac, 0);
     if (S > 1) {
         MX_L(count_kernel, one, kScanTPB);
-        MX_L(compact_kernel, dim3(bgrid, nrows), kTPB, 1);
+        MX_L(compact_kernel, dim3(bgrid, nrows), kTPB, S, frac, 1);
     }
-    MX_L(cand_hist<kTopBits>, dim3(cgrid, nrows), kTPB, kTopShift);
-    MX_L(select_cand<kTopBits>, one, kTPB, kTopShift);
-    MX_L(cand_hist<kMidBits>, dim3(cgrid, nrows), kTPB, kMidShift);
-    MX_L(select_cand<kMidBits>, one, kTPB, kMidShift);
-    MX_L(cand_hist<kLowBits>, dim3(cgrid, nrows), kTPB, 0);
-    MX_L(select_cand<kLowBits>, one, kTPB, 0);
+    MX_L(cand_hist<kMidBits>, dim3(cgrid, nrows), kTPB);
+    MX_L(cand_hist<kLowBits>, dim3(cgrid, nrows), kTPB);
     MX_L(cand_mark, dim3(cgrid, nrows), kTPB);
     MX_L(scan_kernel, one, kScanTPB);
     MX_L(write_cand, dim3(wgrid, nrows), kTPB);
