@@ -62,10 +62,16 @@ def cpu_baseline(pkg, partner, alpha, n, P, seconds):
     t = time.time()
     O.baseline_rounds(rows, partner, flags, alpha, threads=threads)
     el = time.time() - t
+    # single-process variant: every worker's sequence on one core
+    t = time.time()
+    O.baseline_rounds(rows, partner, flags[:1], alpha, threads=1)
+    el1 = time.time() - t
     return {"value": rounds / el, "unit": "rounds/s", "cores": threads, "kind": "port",
             "sample": f"{rounds} full rounds, graph {0}, {n} workers x {P} fp32 (same workload), "
                       f"{el:.1f} s; oracle/matcha_oracle.c orc_baseline_rounds, {threads} OpenMP threads "
-                      f"(one per worker, like the mpirun ranks) of {os.cpu_count()} host CPUs"}
+                      f"(one per worker, like the mpirun ranks) of {os.cpu_count()} host CPUs",
+            "single_core": {"value": 1.0 / el1, "unit": "rounds/s", "cores": 1,
+                            "sample": f"1 full round, all {n} workers on one thread, {el1:.1f} s"}}
 
 
 def pmc_traffic(kernel_prefix="mix_kernel"):
