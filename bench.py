@@ -179,14 +179,18 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    ev = timed_rounds(group, W, K)
+    for j in range(K):                           # the timed rounds: back to back, nothing else
+        group.step(W + j)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    step_ms = np.array([a.elapsed_time(b) for a, b in ev])
     elapsed = max_over_ranks(elapsed, world, dev)
+    # per-round HIP events (diagnostic, outside the timed region): K more rounds
+    ev = timed_rounds(group, W + K, K)
+    torch.cuda.synchronize()
+    step_ms = np.array([a.elapsed_time(b) for a, b in ev])
     # mixing kernel alone (N > 1: without the RCCL exchange) -> its HBM roofline
     stream = torch.cuda.current_stream()
     mev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
