@@ -174,9 +174,16 @@ def sync_rows(rows):
 
 
 class VirtualTrainer:
-    """All workers of the topology on this GPU; one gossip launch per batch for all of them."""
+    """All workers of the topology on this GPU; one gossip launch per batch for all of them.
 
-    def __init__(self, args, model_fn, n_batches, device="cuda"):
+    batched=False: each worker runs its own forward / backward / torch.optim.SGD step, exactly
+    train_mpi.py's per-rank sequence.  batched=True: the workers' parameters are addressed as
+    stacked [n, ...] views of the worker arena, one vmap'd forward / backward computes every
+    worker's gradients (torch.func), and the SGD update (weight decay, momentum, Nesterov; the
+    element-wise op sequence of torch.optim.SGD) runs once over the stacked views -- a training
+    step for all workers is a handful of batched launches plus the gossip kernel."""
+
+    def __init__(self, args, model_fn, n_batches, device="cuda", batched=False):
         self.args = args
         size = args.size
         np.random.seed(args.randomSeed)                          # train_mpi.py:62
@@ -201,9 +208,55 @@ class VirtualTrainer:
         self.n_batches = n_batches
         self.recorders = [Recorder(args, r) for r in range(size)] if args.save else None
         self.epoch = 0
+        self.batched = bool(batched)
+        if self.batched:
+            self._setup_batched()
 
     def communicate(self):
         return self.group.communicate()
+
+    # ------------------------------------------------------------------ batched workers
+    def _setup_batched(self):
+        from torch.func import functional_call, grad_and_value, vmap
+        m0 = self.models[0]
+        rows = self.group.rows
+        n = rows.shape[0]
+        self._stack = {}
+        off = 0
+        for name, p in m0.named_parameters():          # the arena's adoption order
+            k = p.numel()
+            self._stack[name] = rows[:, off:off + k].view((n,) + tuple(p.shape))
+            off += k
+        self._mom = {}
+
+        def loss_fn(params, x, y):
+            out = functional_call(m0, params, (x,))
+            return F.cross_entropy(out, y), out
+
+        self._grad_fn = vmap(grad_and_value(loss_fn, has_aux=True))
+        self._data_stacked = [(torch.stack([self.data[r][b][0] for r in range(n)]),
+                               torch.stack([self.data[r][b][1] for r in range(n)]))
+                              for b in range(self.n_batches)]
+
+    def _batched_step(self, b, lr):
+        """Every worker's forward / backward / SGD step for batch b; per-worker (loss, acc)."""
+        args = self.args
+        X, Y = self._data_stacked[b]
+        grads, (loss, out) = self._grad_fn(self._stack, X, Y)
+        wd, mom = 5e-4, args.momentum
+        with torch.no_grad():
+            for name, p in self._stack.items():         # torch.optim.SGD's element-wise sequence
+                d_p = grads[name].add(p, alpha=wd)
+                if mom != 0:
+                    buf = self._mom.get(name)
+                    if buf is None:
+                        buf = self._mom[name] = d_p.clone()
+                    else:
+                        buf.mul_(mom).add_(d_p)
+                    d_p = d_p.add(buf, alpha=mom) if args.nesterov else buf
+                p.add_(d_p, alpha=-lr)
+            acc = (out.argmax(-1) == Y).float().mean(-1) * 100.0
+        return loss.detach(), acc
 
     def train_epoch(self, on_round=None):
         """One epoch of train_mpi.py:109-168 for every worker; returns per-worker stats."""
@@ -218,22 +271,34 @@ class VirtualTrainer:
         for m in self.models:
             m.train()
         for b in range(self.n_batches):
-            for r, (m, opt) in enumerate(zip(self.models, self.optimizers)):
+            if self.batched:
                 t0 = time.time()
-                data, target = self.data[r][b]
-                output = m(data)
-                loss = self.criterion(output, target)
-                acc1 = comp_accuracy(output, target)
-                losses[r].update(loss.item(), data.size(0))
-                top1[r].update(acc1[0].item(), data.size(0))
-                loss.backward()
-                update_learning_rate(opt, epoch, args, itr=b, itr_per_epoch=self.n_batches)
-                opt.step()
-                opt.zero_grad()
-                comp[r] += time.time() - t0
+                lr = update_learning_rate(self.optimizers[0], epoch, args, itr=b, itr_per_epoch=self.n_batches)
+                loss_b, acc_b = self._batched_step(b, lr)
+                lb, ab = loss_b.cpu().tolist(), acc_b.cpu().tolist()
+                bs = self._data_stacked[b][1].shape[1]
+                dt = (time.time() - t0) / size
+                for r in range(size):
+                    losses[r].update(lb[r], bs)
+                    top1[r].update(ab[r], bs)
+                    comp[r] += dt
+            else:
+                for r, (m, opt) in enumerate(zip(self.models, self.optimizers)):
+                    t0 = time.time()
+                    data, target = self.data[r][b]
+                    output = m(data)
+                    loss = self.criterion(output, target)
+                    acc1 = comp_accuracy(output, target)
+                    losses[r].update(loss.item(), data.size(0))
+                    top1[r].update(acc1[0].item(), data.size(0))
+                    loss.backward()
+                    update_learning_rate(opt, epoch, args, itr=b, itr_per_epoch=self.n_batches)
+                    opt.step()
+                    opt.zero_grad()
+                    comp[r] += time.time() - t0
             if on_round is not None:
                 on_round("before", self)
-            comm_time += self.communicate()
+            comm_time += self.communicate()                  # train_mpi.py:142, all workers at once
             if on_round is not None:
                 on_round("after", self)
         record_time = time.time() - tic
@@ -257,14 +322,19 @@ class VirtualTrainer:
 
     # checkpoint / resume: worker rows, Choco state, iteration and epoch counters, optimizers
     def state_dict(self):
-        return {"group": self.group.state_dict(), "epoch": self.epoch,
-                "optimizers": [o.state_dict() for o in self.optimizers]}
+        out = {"group": self.group.state_dict(), "epoch": self.epoch,
+               "optimizers": [o.state_dict() for o in self.optimizers]}
+        if self.batched:
+            out["momentum"] = {k: v.detach().clone() for k, v in self._mom.items()}
+        return out
 
     def load_state_dict(self, state):
         self.group.load_state_dict(state["group"])
         self.epoch = int(state["epoch"])
         for o, s in zip(self.optimizers, state["optimizers"]):
             o.load_state_dict(s)
+        if self.batched:
+            self._mom = {k: v.clone() for k, v in state.get("momentum", {}).items()}
 
     def save(self, path):
         torch.save(self.state_dict(), path)

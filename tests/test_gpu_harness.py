@@ -13,12 +13,12 @@ def _args(pkg, **kw):
     return pkg.harness.HarnessArgs(**base)
 
 
-@pytest.mark.parametrize("matcha", [True, False])
-def test_virtual_trainer_rounds_match_oracle(pkg, O, matcha):
+@pytest.mark.parametrize("matcha,batched", [(True, False), (False, False), (True, True)])
+def test_virtual_trainer_rounds_match_oracle(pkg, O, matcha, batched):
     """Every communicate() of the harness is one reference gossip round of the post-step rows."""
     H = pkg.harness
     args = _args(pkg, matcha=matcha)
-    tr = H.VirtualTrainer(args, H.model_factory(args), n_batches=3)
+    tr = H.VirtualTrainer(args, H.model_factory(args), n_batches=3, batched=batched)
     GP = tr.GP
     partner = np.asarray(GP.neighbors_info, np.int32)
     seen = {"rounds": 0}
@@ -106,3 +106,19 @@ def test_recorder_through_trainer(pkg, tmp_path):
     import os
     files = os.listdir(str(tmp_path / (args.name + "_mlp")))
     assert len([f for f in files if f.endswith(".log")]) == 7 * 8
+
+
+@pytest.mark.parametrize("momentum,nesterov", [(0.0, False), (0.9, False), (0.9, True)])
+def test_batched_step_matches_per_worker_sgd(pkg, momentum, nesterov):
+    """The vmap'd all-worker step gives each worker what its own torch.optim.SGD step gives
+    (gradients via one batched backward: equal to fp32 rounding of the GEMM reductions)."""
+    H = pkg.harness
+    args = _args(pkg, momentum=momentum, nesterov=nesterov, epoch=2, lr=0.05)
+    seq = H.VirtualTrainer(args, H.model_factory(args), n_batches=2)
+    bat = H.VirtualTrainer(args, H.model_factory(args), n_batches=2, batched=True)
+    assert torch.equal(seq.group.rows, bat.group.rows)
+    for _ in range(2):
+        seq.train_epoch()
+        bat.train_epoch()
+    assert torch.allclose(seq.group.rows, bat.group.rows, rtol=1e-4, atol=1e-6), \
+        float((seq.group.rows - bat.group.rows).abs().max())

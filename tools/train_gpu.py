@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--batches", default=20, type=int, help="batches per epoch")
     ap.add_argument("--checkpoint", default=None)
     ap.add_argument("--resume", default=None)
+    ap.add_argument("--batched", action="store_true", help="one vmap'd step for all virtual workers")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -54,13 +55,18 @@ def main():
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
         tr = H.RankTrainer(args, H.model_factory(args), a.batches, rank, world)
     else:
-        tr = H.VirtualTrainer(args, H.model_factory(args), a.batches)
+        tr = H.VirtualTrainer(args, H.model_factory(args), a.batches, batched=a.batched)
         if a.resume:
             tr.load(a.resume)
+    import time
     while tr.epoch < args.epoch:
+        torch.cuda.synchronize()
+        t = time.time()
         stats = tr.train_epoch()
+        torch.cuda.synchronize()
         if rank == 0:
-            print(H.epoch_summary(stats, tr.epoch - 1), flush=True)
+            print(H.epoch_summary(stats, tr.epoch - 1) + f", wall: {time.time() - t:.3f} s "
+                  f"({a.batches / (time.time() - t):.1f} iterations/s)", flush=True)
     tr.finish()
     if a.checkpoint and world == 1:
         tr.save(a.checkpoint)
