@@ -452,10 +452,6 @@ def epoch_summary(stats, epoch):
             f"comp_time: {comp:.3f}, comm_time: {stats[0]['comm_time']:.3f}")
 
 
-def iterations_for(args, n_batches):
-    return args.epoch * n_batches
-
-
 __all__ = ["MNIST_MLP", "comp_accuracy", "AverageMeter", "Recorder", "update_learning_rate",
            "synthetic_batches", "make_topology", "sync_rows", "VirtualTrainer", "RankTrainer", "HarnessArgs",
-           "model_factory", "epoch_summary", "iterations_for"]
+           "model_factory", "epoch_summary"]
