@@ -52,3 +52,14 @@ def test_bench_multiprocess_path():
     out = json.loads(line)
     assert out["n_gpus"] == 2 and out["value"] > 0 and out["xgmi"]["max_link_bytes_per_round"] > 0
     assert out["choco"]["rounds_per_s"] > 0 and out["cpu_baseline"] is None
+
+
+def test_dropin_communicators_one_process_per_worker():
+    """train_mpi.py's deployment: 8 processes, one worker each, decenCommunicator /
+    ChocoCommunicator(rank, 8, GP, ...).communicate(model) with GPU- and CPU-resident models,
+    bit-exact vs the oracle every round (8 ranks share GPU 0; gloo transport)."""
+    r = _torchrun(8, [os.path.join(HERE, "mp_dropin.py")], timeout=280)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["world"] == 8 and all(v for k, v in res.items() if k != "world"), res
