@@ -112,6 +112,31 @@ __global__ __launch_bounds__(256) void k_rmw8u(f4* __restrict__ x, int64_t ld4, 
     }
 }
 
+// Choco compaction read pattern: R rows of x and x_hat (2R streams), 4096-element chunks.
+// FLAT = 0: grid (G, R), block (b, r) walks row r's chunks (every row streams concurrently);
+// FLAT = 1: 1-D grid walks flat (row, chunk) indices, so the chip works through one row at a time.
+template <int FLAT>
+__global__ __launch_bounds__(256) void k_read_rows(const f4* __restrict__ x, const f4* __restrict__ xh,
+                                                   int64_t ld4, int64_t nc, int rows, float* out) {
+    f4 acc = {0, 0, 0, 0};
+    const int64_t total = FLAT ? nc * rows : nc;
+    const int64_t start = blockIdx.x, step = gridDim.x;
+    for (int64_t f = start; f < total; f += step) {
+        const int64_t r = FLAT ? f / nc : blockIdx.y;
+        const int64_t c = FLAT ? f % nc : f;
+        const int64_t q0 = r * ld4 + c * 1024 + threadIdx.x;
+        f4 a[4], b[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            a[j] = __builtin_nontemporal_load(x + q0 + j * 256);
+            b[j] = __builtin_nontemporal_load(xh + q0 + j * 256);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc += a[j] - b[j];
+    }
+    if (acc.x + acc.y + acc.z + acc.w == 1.2345f) out[0] = 1.0f;
+}
+
 template <bool NT, int U>
 __global__ __launch_bounds__(256) void k_read(const f4* __restrict__ s, float* out, int64_t n4) {
     const int64_t tile = 256 * U;
@@ -205,6 +230,21 @@ int main() {
         }
         report("rmw1", bpc, 1, 1, round_bytes,
                time_ms([&] { hipLaunchKernelGGL((k_rmw1<true, 1>), dim3(grid), dim3(256), 0, 0, A, n4, 1.0f); }));
+    }
+    if (getenv("PROBE_ROWS")) {        // Choco compaction: 8 rows x 14,774,436 of x and x_hat
+        const int64_t Pc = 14774436 / 4096 * 4096, rowsc = 8, ld4 = Pc / 4, ncc = Pc / 4096;
+        const double bytes = 2.0 * rowsc * Pc * 4;
+        f4* Xh = B;                          // x rows in A, x_hat rows in B (both 819 MB buffers)
+        for (int g : {256, 512, 1024, 2048}) {
+            report("rows_concurrent", g, 1, 0, bytes, time_ms([&] {
+                hipLaunchKernelGGL((k_read_rows<0>), dim3(g / 8, 8), dim3(256), 0, 0, A, Xh, ld4, ncc, 8, out);
+            }));
+            report("rows_flat", g, 1, 0, bytes, time_ms([&] {
+                hipLaunchKernelGGL((k_read_rows<1>), dim3(g), dim3(256), 0, 0, A, Xh, ld4, ncc, 8, out);
+            }));
+        }
+        (void)rowsc;
+        return 0;
     }
     // many rows, small per-row chunks (the wide-slot mixing layouts)
     if (getenv("PROBE_WIDE")) {
