@@ -8,10 +8,13 @@
 // their own xGMI links concurrently.  Edges inside a GPU are not moved at all: the mixing
 // kernel reads those rows straight from HBM.
 //
-// Posting order (both directions): matching ascending, then sender worker id ascending --
-// identical to the receive-slot numbering of plan_kernel (plan.hip), so slab slot k of the
-// round always holds the row the plan expects.  Sends to / receives from one peer pair up in
-// posting order, as RCCL point-to-point requires.
+// Each row crosses a link at most once per round: a local worker whose active partners include
+// several workers on one peer GPU (different matchings) is sent to that peer once, and the peer
+// receives it into one slab slot that all its local partners read.  Posting order (both
+// directions): first appearance of the (worker, destination GPU) pair in (matching ascending,
+// sender worker id ascending) order -- identical to the receive-slot numbering of plan_kernel
+// (plan.hip), so slab slot k of the round always holds the row the plan expects.  Sends to /
+// receives from one peer pair up in posting order, as RCCL point-to-point requires.
 #include <rccl/rccl.h>
 
 #include <vector>
@@ -61,6 +64,8 @@ extern "C" int mx_exchange_plan(const uint8_t* flags_row, int M, const int32_t* 
     MX_CHECK(M >= 1 && n_global >= 1 && n_local >= 1 && row_base >= 0 && row_base + n_local <= n_global,
              "mx_exchange_plan: M=%d n=%d block [%d, %d)", M, n_global, row_base, row_base + n_local);
     auto is_local = [&](int w) { return w >= row_base && w < row_base + n_local; };
+    std::vector<uint8_t> sent((size_t)n_local * (size_t)(n_global > 0 ? n_global : 1), 0);  // [row][peer]
+    std::vector<uint8_t> got((size_t)n_global, 0);                                         // by worker
     int cnt = 0, remote = 0;
     for (int g = 0; g < M; ++g) {
         if (!flags_row[g]) continue;
@@ -72,7 +77,16 @@ extern "C" int mx_exchange_plan(const uint8_t* flags_row, int M, const int32_t* 
             const bool pl = is_local(p), ql = is_local(q);
             if (pl == ql) continue;
             const int peer = pl ? owner[q] : owner[p];
-            MX_CHECK(peer >= 0 && peer != my_rank, "mx_exchange_plan: worker owned by bad rank %d", peer);
+            MX_CHECK(peer >= 0 && peer != my_rank && peer < n_global,
+                     "mx_exchange_plan: worker owned by bad rank %d", peer);
+            if (pl) {                               // send p's row to peer once per round
+                uint8_t& done = sent[(size_t)(p - row_base) * n_global + peer];
+                if (done) continue;
+                done = 1;
+            } else {                                // receive p's row once per round
+                if (got[p]) continue;
+                got[p] = 1;
+            }
             if (ops) {
                 MX_CHECK(cnt < cap, "mx_exchange_plan: more than %d operations", cap);
                 int32_t* o = ops + 4 * cnt;

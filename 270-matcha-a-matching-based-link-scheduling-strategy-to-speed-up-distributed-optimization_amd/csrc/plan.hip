@@ -6,12 +6,17 @@
 //         if flag and neighbors_info[graph_id][rank] != -1: degree += 1; use that partner
 //     selfweight = 1 - degree * alpha
 // For each local row the record lists its partners' slots in matching order, so the mixing
-// kernel reproduces the reference's FMA order exactly.  Partners owned by another rank are
-// given receive-slab slots in (matching asc, sender id asc) order, the order in which
-// mx_exchange_round (exchange.cpp) posts its RCCL receives.
+// kernel reproduces the reference's FMA order exactly.  Partners owned by another rank get one
+// receive-slab slot per distinct worker, numbered by first appearance in (matching asc, sender
+// id asc) order -- the order in which mx_exchange_round (exchange.cpp) posts its RCCL receives.
+// A remote worker that partners several local rows in one round (different matchings) is
+// received ONCE and its slot is shared: its row crosses the link once per round, not once per
+// edge.
 #include "mx_common.h"
 
 namespace {
+constexpr int kMaxRemote = 64;                 // the mixing kernels take at most 64 slots
+
 __global__ __launch_bounds__(256) void plan_kernel(const uint8_t* __restrict__ flags, int64_t T,
                                                    int M, const int32_t* __restrict__ partner,
                                                    int n, int row_base, int n_local, double alpha,
@@ -26,6 +31,7 @@ __global__ __launch_bounds__(256) void plan_kernel(const uint8_t* __restrict__ f
     int32_t* src = sw + n_local;
     for (int r = 0; r < n_local; ++r) deg[r] = 0;
     int any = 0, remote = 0;
+    int32_t who[kMaxRemote];                   // slab slot -> remote worker (first appearance)
     for (int g = 0; g < M; ++g) {
         if (!f[g]) continue;
         any = 1;
@@ -34,7 +40,15 @@ __global__ __launch_bounds__(256) void plan_kernel(const uint8_t* __restrict__ f
             if (q < row_base || q >= row_base + n_local) continue;
             const int r = q - row_base;
             const bool p_local = (p >= row_base && p < row_base + n_local);
-            const int slot = p_local ? p - row_base : n_local + remote++;
+            int slot;
+            if (p_local) {
+                slot = p - row_base;
+            } else {
+                int k = 0;
+                while (k < remote && who[k] != p) ++k;
+                if (k == remote) who[remote++] = p;
+                slot = n_local + k;
+            }
             src[r * M + deg[r]] = slot;
             deg[r] += 1;
         }

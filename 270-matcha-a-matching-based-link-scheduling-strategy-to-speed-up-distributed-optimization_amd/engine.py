@@ -66,17 +66,19 @@ def validate_partner(partner):
 
 
 def max_incoming_remote(partner, row_base, n_local):
-    """Receive-slab rows needed when every matching is active (upper bound over all rounds)."""
+    """Receive-slab rows needed when every matching is active (upper bound over all rounds): the
+    distinct remote workers that partner a local worker in some matching -- each is received
+    once per round however many local partners it has (mx_exchange_plan / plan_kernel)."""
     M, n = partner.shape
-    cnt = 0
+    remote = set()
     for g in range(M):
         for p in range(n):
             q = int(partner[g, p])
             if q < 0:
                 continue
             if row_base <= q < row_base + n_local and not (row_base <= p < row_base + n_local):
-                cnt += 1
-    return cnt
+                remote.add(p)
+    return len(remote)
 
 
 class RcclComm:

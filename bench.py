@@ -259,20 +259,19 @@ def main():
             if f[g]:
                 deg += partner[g] >= 0
         act = sum(1 for i in range(group.row_base, group.row_base + group.n_local) if deg[i] > 0)
-        remote = 0
-        links = {}
+        moved = set()                  # (worker, destination GPU): each row crosses a link once
         for g in range(len(f)):
             if not f[g]:
                 continue
             for p in range(n):
                 q = partner[g, p]
-                if q < 0:
-                    continue
-                a, b = eng.owner[p], eng.owner[q]
-                if a != b:
-                    links[(a, b)] = links.get((a, b), 0) + P * 4     # p's row travels a -> b
-                    if b == rank:
-                        remote += 1
+                if q >= 0 and eng.owner[p] != eng.owner[q]:
+                    moved.add((p, int(eng.owner[q])))
+        links = {}
+        for p, b in moved:
+            a = int(eng.owner[p])
+            links[(a, b)] = links.get((a, b), 0) + P * 4     # p's row travels a -> b
+        remote = sum(1 for p, b in moved if b == rank)
         hbm_bytes.append(2 * act * P * 4 + remote * P * 4)
         link_bytes.append(max(links.values()) if links else 0)
         pair = {}

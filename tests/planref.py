@@ -2,7 +2,8 @@
 
 For iteration flags `flags_row`, rows [row_base, row_base + n_local) of `partner` [M][n]:
 each local row's partners in ascending matching order as slots (slot < n_local: local row,
-slot >= n_local: receive-slab row numbered in (matching asc, sender id asc) order), and the
+slot >= n_local: receive-slab row of a distinct remote worker, numbered by first appearance in
+(matching asc, sender id asc) order), and the
 selfweight f32(1 - degree * alpha) (communicator.py:99-117)."""
 import numpy as np
 
@@ -20,8 +21,9 @@ def py_plan(flags_row, partner, row_base, n_local, alpha):
                 continue
             if row_base <= p < row_base + n_local:
                 src[q - row_base].append(p - row_base)
-            else:
-                src[q - row_base].append(n_local + len(senders))
-                senders.append(p)
+            else:                     # one slab slot per distinct remote worker
+                if p not in senders:
+                    senders.append(p)
+                src[q - row_base].append(n_local + senders.index(p))
     sw = [np.float32(1.0 - len(s) * alpha) for s in src]
     return int(any(flags_row)), len(senders), src, sw, senders

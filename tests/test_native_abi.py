@@ -68,3 +68,30 @@ def test_dropin_shims_resolve(pkg):
         assert m.get_top_k is pkg.get_top_k
     finally:
         sys.path.remove(d)
+
+
+def test_exchange_plan_moves_each_row_once_per_link(pkg):
+    """Graph 0 split over 2 GPUs ({0-3}, {4-7}), every matching active: 6 cross edges, but workers
+    0 (partners 4, 7), 1 (5, 7) and 3 (6, 7) each cross the link once, and 7 (partners 0, 1, 3)
+    once the other way -- 3 rows 0 -> 1 and 4 rows 1 -> 0 instead of 6 + 6 (mx_exchange_plan)."""
+    import ctypes
+    import numpy as np
+    gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, 8, 4, True)
+    partner = np.ascontiguousarray(np.asarray(gp.neighbors_info, np.int32))
+    M = partner.shape[0]
+    owner = pkg.engine.owner_table(8, 2)
+    flags = np.ones(M, np.uint8)
+    for rank, (base, nl) in enumerate(pkg.partition(8, 2)):
+        cnt = ctypes.c_int(0)
+        assert pkg.lib.mx_exchange_plan(flags.ctypes.data, M, partner.ctypes.data, 8, owner.ctypes.data, rank,
+                                        base, nl, None, 0, ctypes.byref(cnt)) == 0
+        ops = np.zeros((cnt.value, 4), np.int32)
+        assert pkg.lib.mx_exchange_plan(flags.ctypes.data, M, partner.ctypes.data, 8, owner.ctypes.data, rank,
+                                        base, nl, ops.ctypes.data, cnt.value, ctypes.byref(cnt)) == 0
+        sends = sorted(int(o[3]) for o in ops if o[0] == 0)
+        recvs = [int(o[3]) for o in ops if o[0] == 1]
+        assert len(set(sends)) == len(sends) and len(set(recvs)) == len(recvs)
+        assert [int(o[2]) for o in ops if o[0] == 1] == list(range(len(recvs)))    # slab slots
+        assert (len(sends), len(recvs)) == ((3, 4) if rank == 0 else (4, 3))
+        assert sends == ([0, 1, 3] if rank == 0 else [4, 5, 6, 7])
+        assert pkg.engine.max_incoming_remote(partner, base, nl) == len(recvs)
