@@ -176,9 +176,11 @@ int mx_choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64
 /* ---------------------------------------------------------------- cross-GPU exchange (RCCL)
  * One process per GPU; workers partitioned by owner[].  mx_exchange_round posts, inside one
  * ncclGroupStart/End, an ncclSend of every local row whose active partner lives on another
- * rank and an ncclRecv of every remote partner row into the receive slab -- the pairwise
- * comm.sendrecv of decenCommunicator.averaging (communicator.py:110) over xGMI.
- * Order: matching ascending, then sender worker id ascending (matches mx_plan_build).
+ * rank (once per destination rank) and an ncclRecv of every distinct remote partner row into
+ * the receive slab -- the pairwise comm.sendrecv of decenCommunicator.averaging
+ * (communicator.py:110) over xGMI, with each row crossing a link at most once per round.
+ * Order: first appearance over (matching ascending, sender worker id ascending); slab slot k
+ * is the k-th distinct remote worker in that order (matches mx_plan_build).
  *   flags_row  uint8 [M] host;  partner int32 [M][n_global] host;  owner int32 [n_global] host
  *   rows       device float* [n_local] (host array of device pointers), P floats each
  *   slab       device base; slot k at slab + k * slab_ld
