@@ -15,11 +15,13 @@ from .compressors import get_top_k
 from .topologies import select_graph, erdos_renyi, GRAPH_SIZES
 from . import solver
 from . import harness
+from . import placement
+from .placement import best_placement, placement_cost
 
 __all__ = [
     "MXError", "lib", "GraphProcessor", "FixedProcessor", "MatchaProcessor", "GossipEngine",
     "VirtualWorkerGroup", "RcclComm", "Layout", "partition", "ChocoWorkerGroup", "topk_count",
     "Communicator", "decenCommunicator", "ChocoCommunicator", "centralizedCommunicator",
     "flatten_tensors", "unflatten_tensors", "scatter_tensors", "get_top_k", "select_graph",
-    "erdos_renyi", "GRAPH_SIZES", "solver", "harness",
+    "erdos_renyi", "GRAPH_SIZES", "solver", "harness", "placement", "best_placement", "placement_cost",
 ]

@@ -22,10 +22,15 @@ def topk_count(P, ratio):
 
 class ChocoWorkerGroup:
     def __init__(self, topology, models=None, numel=None, *, ratio, consensus_lr, rank=0, nranks=1,
-                 comm=None, adopt=True):
+                 comm=None, adopt=True, placement=None):
+        """placement: as VirtualWorkerGroup (None / "contiguous", "auto" or a worker order);
+        `workers` lists the worker id of each local row."""
         require_device()
+        from .placement import block_workers, place
         n = int(topology.size)
+        topology, self.placement = place(topology, nranks, placement)
         self.row_base, self.n_local = partition(n, nranks)[rank]
+        self.workers = block_workers(self.placement, self.row_base, self.n_local)
         if nranks > 1 and comm is None:
             comm = default_comm()
         self.engine = GossipEngine(topology, self.row_base, self.n_local, comm=comm,
@@ -114,12 +119,14 @@ class ChocoWorkerGroup:
         the iteration counter."""
         P = self.numel
         return {"kind": "choco", "iter": int(self.iter), "row_base": int(self.row_base), "k": int(self.k),
+                "workers": list(self.workers),
                 "rows": self.x[:, :P].detach().clone(), "x_hat": self.x_hat[:, :P].detach().clone(),
                 "s": self.s[:, :P].detach().clone()}
 
     def load_state_dict(self, state):
         P = self.numel
         if state.get("kind") != "choco" or int(state["row_base"]) != self.row_base or \
+                list(state.get("workers", self.workers)) != self.workers or \
                 int(state["k"]) != self.k or tuple(state["rows"].shape) != (self.n_local, P):
             raise ValueError("checkpoint does not match this Choco worker group")
         with torch.no_grad():

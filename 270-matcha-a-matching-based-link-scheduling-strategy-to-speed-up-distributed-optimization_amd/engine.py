@@ -253,14 +253,21 @@ class VirtualWorkerGroup:
                with adopt=True their parameters are re-homed into the arena as views (identity
                and shapes kept, so optimizers stay valid) and every round mixes them in place.
     numel   -- arena width when no models are given (synthetic workloads / benchmarks).
+    placement -- which workers share a GPU when nranks > 1: None / "contiguous" (blocks of
+               consecutive ids), "auto" (placement.best_placement: fewest rows over the busiest
+               xGMI pair) or an explicit worker order.  `workers` lists the worker id of each
+               local row (models are given in that order).
     """
 
     def __init__(self, topology, models=None, numel=None, *, rank=0, nranks=1, comm=None, adopt=True,
-                 chunk_cols=None):
+                 chunk_cols=None, placement=None):
         require_device()
+        from .placement import block_workers, place
         n = int(topology.size)
+        topology, self.placement = place(topology, nranks, placement)
         blocks = partition(n, nranks)
         self.row_base, self.n_local = blocks[rank]
+        self.workers = block_workers(self.placement, self.row_base, self.n_local)
         if nranks > 1 and comm is None:
             comm = default_comm()
         self.engine = GossipEngine(topology, self.row_base, self.n_local, comm=comm,
@@ -363,10 +370,11 @@ class VirtualWorkerGroup:
     def state_dict(self):
         """Checkpoint: the workers' rows and the iteration counter (resume on the same schedule)."""
         return {"kind": "decen", "iter": int(self.iter), "row_base": int(self.row_base),
-                "rows": self.rows.detach().clone()}
+                "workers": list(self.workers), "rows": self.rows.detach().clone()}
 
     def load_state_dict(self, state):
         if state.get("kind") != "decen" or int(state["row_base"]) != self.row_base or \
+                list(state.get("workers", self.workers)) != self.workers or \
                 tuple(state["rows"].shape) != tuple(self.rows.shape):
             raise ValueError("checkpoint does not match this worker group")
         with torch.no_grad():

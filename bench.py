@@ -43,6 +43,9 @@ def parse():
                     help="N > 1 partner exchange: rccl (the product path, one GPU per rank) or gloo "
                          "(tests/gloo_transport.py: host staging, lets N ranks share one GPU to test "
                          "the multi-process path; never a performance number)")
+    ap.add_argument("--placement", choices=("auto", "contiguous"), default="auto",
+                    help="N > 1: which workers share a GPU -- auto (placement.best_placement, fewest rows "
+                         "over the busiest xGMI pair) or contiguous id blocks")
     return ap.parse_args()
 
 
@@ -97,14 +100,14 @@ def max_over_ranks(x, world, dev):
     return float(t.item())
 
 
-def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99, gamma=0.1):
+def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99, gamma=0.1, placement=None):
     """Secondary figure: ChocoSGD rounds (BASELINE config: VGG-16 size, top-1 %, graph 0, every
     matching active) on the same GPUs -- top-k compress + [N > 1] message exchange + fused apply."""
     import torch.distributed as dist
     grp = pkg.ChocoWorkerGroup(GP, numel=P, ratio=ratio, consensus_lr=gamma, rank=rank, nranks=world,
-                               comm=comm)
+                               comm=comm, placement=placement)
     for r in range(grp.n_local):
-        pkg._lib.check(pkg.lib.mx_synth_fill(grp.rows[r].data_ptr(), P, 1234 + grp.row_base + r, None))
+        pkg._lib.check(pkg.lib.mx_synth_fill(grp.rows[r].data_ptr(), P, 1234 + grp.workers[r], None))
     for it in range(W):
         grp.step(it)
     torch.cuda.synchronize()
@@ -167,9 +170,9 @@ def main():
     K, W = args.steps, args.warmup
     np.random.seed(1234)
     GP = pkg.MatchaProcessor(pkg.select_graph(args.graph), args.budget, rank, n, W + 2 * K, True)
-    group = pkg.VirtualWorkerGroup(GP, numel=P, rank=rank, nranks=world, comm=comm)
+    group = pkg.VirtualWorkerGroup(GP, numel=P, rank=rank, nranks=world, comm=comm, placement=args.placement)
     for r in range(group.n_local):
-        pkg._lib.check(pkg.lib.mx_synth_fill(group.rows[r].data_ptr(), P, 1234 + group.row_base + r, None))
+        pkg._lib.check(pkg.lib.mx_synth_fill(group.rows[r].data_ptr(), P, 1234 + group.workers[r], None))
     torch.cuda.synchronize()
 
     for it in range(W):
@@ -221,9 +224,9 @@ def main():
     if args.budget >= 1.0:
         np.random.seed(1234)
         GPm = pkg.MatchaProcessor(pkg.select_graph(args.graph), 0.5, rank, n, W + K, True)
-        gm = pkg.VirtualWorkerGroup(GPm, numel=P, rank=rank, nranks=world, comm=comm)
+        gm = pkg.VirtualWorkerGroup(GPm, numel=P, rank=rank, nranks=world, comm=comm, placement=args.placement)
         for r in range(gm.n_local):
-            pkg._lib.check(pkg.lib.mx_synth_fill(gm.rows[r].data_ptr(), P, 1234 + gm.row_base + r, None))
+            pkg._lib.check(pkg.lib.mx_synth_fill(gm.rows[r].data_ptr(), P, 1234 + gm.workers[r], None))
         for it in range(W):
             gm.step(it)
         torch.cuda.synchronize()
@@ -242,14 +245,16 @@ def main():
                   "skipped_rounds": int((fl.sum(1) == 0).sum())}
         del gm
 
-    choco = (choco_figure(pkg, GP, rank, world, max(5, K // 5), 3, comm, dev, P=args.choco_params)
+    choco = (choco_figure(pkg, GP, rank, world, max(5, K // 5), 3, comm, dev, P=args.choco_params,
+                          placement=args.placement)
              if args.choco else None)
 
-    partner = np.asarray(GP.neighbors_info, np.int32)
     flags = np.asarray(GP.active_flags[W:W + K], np.uint8)
     # algorithmic HBM bytes of the mixing kernel on this GPU: every local row with degree > 0 read
-    # and written once, every received slab row read once
+    # and written once, every received slab row read once (positions of the engine's table: with a
+    # placement, worker group.workers[i] sits at position row_base + i)
     eng = group.engine
+    partner = eng.partner
     hbm_bytes = []
     link_bytes = []
     pair_bytes = []
@@ -302,7 +307,9 @@ def main():
             "config": {"workload": f"graph {args.graph} ({n} workers), P={P} fp32 per worker, "
                                    f"budget {args.budget} ({'every matching active' if args.budget >= 1 else 'MATCHA schedule'})",
                        "workers": n, "params_per_worker": P, "graph": args.graph, "budget": args.budget,
-                       "parallelism": f"{n} workers over {world} GPU(s), contiguous blocks",
+                       "parallelism": f"{n} workers over {world} GPU(s)" +
+                                      (f", placement {args.placement}" if world > 1 else ""),
+                       "placement": group.placement if world > 1 else None,
                        "transport": args.transport if world > 1 else None},
             "roofline": {"bound": "hbm", "kernel": "mix_kernel (mx_gossip_mix)",
                          "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",

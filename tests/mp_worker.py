@@ -23,7 +23,16 @@ from conftest import PKG_NAME, Topo  # noqa: E402
 from gloo_transport import GlooTransport, gather_rows  # noqa: E402
 
 
-def decen_case(pkg, T, gid, P, rounds, chunk_cols=None, seed=5):
+def by_worker(grp, rows):
+    """gathered rows are in the group's position order; put them in worker order"""
+    if grp.placement is None:
+        return rows
+    out = np.empty_like(rows)
+    out[grp.placement] = rows
+    return out
+
+
+def decen_case(pkg, T, gid, P, rounds, chunk_cols=None, seed=5, placement=None):
     rank, world = dist.get_rank(), dist.get_world_size()
     n = pkg.GRAPH_SIZES[gid]
     gp = pkg.GraphProcessor(pkg.select_graph(gid), 1.0, 0, n, 4, True)
@@ -32,18 +41,19 @@ def decen_case(pkg, T, gid, P, rounds, chunk_cols=None, seed=5):
     flags = (rng.uniform(size=(rounds, M)) < 0.6).astype(np.uint8)
     flags[0] = 1
     topo = Topo(gp.neighbors_info, 0.21, flags)
-    grp = pkg.VirtualWorkerGroup(topo, numel=P, rank=rank, nranks=world, comm=T, chunk_cols=chunk_cols)
+    grp = pkg.VirtualWorkerGroup(topo, numel=P, rank=rank, nranks=world, comm=T, chunk_cols=chunk_cols,
+                                 placement=placement)
     X = np.stack([O.synth(77 + i, P) for i in range(n)])
-    grp.rows.copy_(torch.from_numpy(X[grp.row_base:grp.row_base + grp.n_local]))
+    grp.rows.copy_(torch.from_numpy(X[grp.workers]))
     for it in range(rounds):
         grp.communicate()
         if flags[it].any():
             X = O.decen_round(X, topo.neighbors_info, flags[it], 0.21)
-    got = gather_rows(grp.rows, grp.row_base, n)
+    got = by_worker(grp, gather_rows(grp.rows, grp.row_base, n))
     return bool(np.array_equal(got.view(np.uint32), X.view(np.uint32)))
 
 
-def choco_case(pkg, T, P, ratio, rounds, seed=9):
+def choco_case(pkg, T, P, ratio, rounds, seed=9, placement=None):
     rank, world = dist.get_rank(), dist.get_world_size()
     n = 8
     gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, n, 4, True)
@@ -52,17 +62,18 @@ def choco_case(pkg, T, P, ratio, rounds, seed=9):
     flags = (rng.uniform(size=(rounds, M)) < 0.6).astype(np.uint8)
     flags[0] = 1
     topo = Topo(gp.neighbors_info, 2 / 7, flags)
-    grp = pkg.ChocoWorkerGroup(topo, numel=P, ratio=ratio, consensus_lr=0.1, rank=rank, nranks=world, comm=T)
+    grp = pkg.ChocoWorkerGroup(topo, numel=P, ratio=ratio, consensus_lr=0.1, rank=rank, nranks=world, comm=T,
+                               placement=placement)
     X = np.stack([O.synth(99 + i, P) for i in range(n)])
     XH = np.zeros_like(X)
     S = np.zeros_like(X)
-    grp.rows.copy_(torch.from_numpy(X[grp.row_base:grp.row_base + grp.n_local]))
+    grp.rows.copy_(torch.from_numpy(X[grp.workers]))
     for it in range(rounds):
         grp.communicate()
         if flags[it].any():
             O.choco_round(X, XH, S, np.asarray(topo.neighbors_info, np.int32), flags[it], 2 / 7, grp.k, 0.1)
-    got = gather_rows(grp.rows, grp.row_base, n)
-    gxh = gather_rows(grp.x_hat[:, :P], grp.row_base, n)
+    got = by_worker(grp, gather_rows(grp.rows, grp.row_base, n))
+    gxh = by_worker(grp, gather_rows(grp.x_hat[:, :P], grp.row_base, n))
     return bool(np.array_equal(got.view(np.uint32), X.view(np.uint32)) and np.array_equal(gxh, XH))
 
 
@@ -87,6 +98,8 @@ def main():
         "decen_g2": decen_case(pkg, T, 2, 9_001, 4),
         "decen_g0_chunked": decen_case(pkg, T, 0, 70_001, 4, chunk_cols=16_384),
         "choco_g0": choco_case(pkg, T, 40_003, 0.9, 4),
+        "decen_g2_placed": decen_case(pkg, T, 2, 9_001, 4, placement="auto"),
+        "choco_g0_placed": choco_case(pkg, T, 20_011, 0.9, 3, placement="auto"),
         "centralized": centralized_case(pkg, T),
     }
     torch.cuda.synchronize()

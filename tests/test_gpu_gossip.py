@@ -477,3 +477,75 @@ def test_choco_multirank_loopback(pkg, O, nranks):
         O.choco_round(X, XH, S, topo.neighbors_info, f, 2 / 7, k, 0.3)
         got = np.concatenate([g.rows.cpu().numpy() for g in groups])
         assert np.array_equal(got.view(np.uint32), X.view(np.uint32)), f"round {t}"
+
+
+@pytest.mark.parametrize("gid,nranks,placement", [(0, 2, "auto"), (0, 4, "auto"), (2, 4, "auto"),
+                                                  (4, 3, "auto"), (0, 2, [7, 2, 5, 0, 1, 6, 3, 4])])
+def test_multirank_placement_loopback(pkg, O, gid, nranks, placement):
+    """Groups built with a worker placement (placement.py): each rank holds the workers listed in
+    `workers`, the exchange moves the rows the relabeled plan names, and every worker ends each
+    round bit-identical to the single-process oracle on the original numbering."""
+    from conftest import LoopbackHub
+    n = pkg.GRAPH_SIZES[gid]
+    P = 9_001
+    gp = pkg.GraphProcessor(pkg.select_graph(gid), 1.0, 0, n, 4, True)
+    M = len(gp.neighbors_info)
+    rng = np.random.RandomState(gid * 10 + nranks)
+    flags = (rng.uniform(size=(5, M)) < 0.7).astype(np.uint8)
+    flags[0] = 1
+    topo = Topo(gp.neighbors_info, 0.21, flags)
+    hub = LoopbackHub(nranks)
+    groups = [pkg.VirtualWorkerGroup(topo, numel=P, rank=r, nranks=nranks, comm=hub.comm(r), placement=placement)
+              for r in range(nranks)]
+    held = [w for g in groups for w in g.workers]
+    assert sorted(held) == list(range(n))
+    if placement == "auto":
+        assert held == pkg.best_placement(np.asarray(gp.neighbors_info), nranks) or held == list(range(n))
+    else:
+        assert held == placement
+    X = np.stack([O.synth(900 + i, P) for i in range(n)])
+    for g in groups:
+        g.rows.copy_(torch.from_numpy(X[g.workers]))
+        hub.register(g.row_base, g._row_ptrs)
+    for it, f in enumerate(flags):
+        for g in groups:
+            g.step(it)
+        torch.cuda.synchronize()
+        X = O.decen_round(X, topo.neighbors_info, f, 0.21)
+        got = np.empty_like(X)
+        for g in groups:
+            got[g.workers] = g.rows.cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), X.view(np.uint32)), f"round {it}"
+    st = groups[0].state_dict()
+    assert st["workers"] == groups[0].workers
+    groups[0].load_state_dict(st)
+
+
+def test_choco_placement_loopback(pkg, O):
+    """ChocoWorkerGroups over 2 ranks with the searched placement: bit-exact vs the oracle."""
+    from conftest import LoopbackHub
+    n, P, ratio, nranks = 8, 20_011, 0.95, 2
+    gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, n, 4, True)
+    flags = np.array([[1, 1, 1, 1, 1], [1, 0, 1, 0, 1], [0, 1, 1, 1, 0]], np.uint8)
+    topo = Topo(gp.neighbors_info, 2 / 7, flags)
+    hub = LoopbackHub(nranks)
+    groups = [pkg.ChocoWorkerGroup(topo, numel=P, ratio=ratio, consensus_lr=0.3, rank=r, nranks=nranks,
+                                   comm=hub.comm(r), placement="auto") for r in range(nranks)]
+    assert [w for g in groups for w in g.workers] != list(range(n))
+    X = np.stack([O.synth(60 + i, P) for i in range(n)])
+    XH, S = np.zeros_like(X), np.zeros_like(X)
+    k = O.topk_k(P, ratio)
+    for g in groups:
+        g.rows.copy_(torch.from_numpy(X[g.workers]))
+    for t, f in enumerate(flags):
+        for g in groups:
+            g.compress(t)
+            hub.register(g.row_base, [g.msgs.data_ptr() + r * g.msg_ld for r in range(g.n_local)])
+        for g in groups:
+            g.average(t)
+        torch.cuda.synchronize()
+        O.choco_round(X, XH, S, topo.neighbors_info, f, 2 / 7, k, 0.3)
+        got = np.empty_like(X)
+        for g in groups:
+            got[g.workers] = g.rows.cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), X.view(np.uint32)), f"round {t}"
