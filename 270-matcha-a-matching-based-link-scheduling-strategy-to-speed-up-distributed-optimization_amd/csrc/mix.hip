@@ -401,6 +401,171 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_reg(float* const* __restrict_
     }
 }
 
+// Row-per-wave kernel (9-64 slots).  A tile is 16384 floats of slot data (NS slots x TW columns,
+// TW = 1024 / 512 / 256 for NS = 16 / 32 / 64 -- the LDS kernel's tiles, so layouts are shared):
+// the whole workgroup stages it in LDS with 16-byte loads (next tile's loads in flight in
+// registers while this one is mixed), then each wave takes whole (row, 256-column pass) items and
+// walks only that row's own partners: one wave-uniform slot per step, one ds_read_b128 and 4 FMAs
+// per lane.  The LDS-column kernel instead runs every row for max-degree steps in every lane,
+// with per-row lookups and selects -- VALU-bound at 32-64 slots.  Items are dealt to the 4 waves
+// by weight (degree + 1, ranked in wave 0, snake order), two items interleaved per wave for ILP.
+template <int NS, int TW, bool NT>
+__global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict__ seg_ptrs,
+                                                        const int64_t* __restrict__ seg_len,
+                                                        const int64_t* __restrict__ tile_off,
+                                                        const uint8_t* __restrict__ seg_vec, int nseg,
+                                                        int64_t total_tiles, int n_slots,
+                                                        const int32_t* __restrict__ plan, int64_t iter,
+                                                        int n_local, int M, float alpha) {
+    using F = typename VT<4>::type;
+    constexpr int C4 = TW / 4;            // float4 per slot per tile
+    constexpr int NQ = TW / 256;          // 256-column passes per row
+    constexpr int NI = NS * NQ;           // items per tile (<= 64: one per lane of wave 0)
+    constexpr int E4 = NS * C4 / kTPB;    // float4 staged per lane per tile
+    static_assert(NI <= 64 && NI % 4 == 0 && E4 >= 1 && C4 % 64 == 0, "row kernel geometry");
+    __shared__ F lds[NS * C4];
+    __shared__ PlanLds<NS> sp;
+    __shared__ int32_t wl[4][NI / 4];
+    const uint64_t need = load_plan<NS>(sp, plan, iter, n_local, M);
+    if (need == 0) return;
+    const int32_t* deg = sp.w + mx::kPlanHeader;
+    const float* sw = reinterpret_cast<const float*>(deg + n_local);
+    const int32_t* src = deg + 2 * n_local;
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int64_t niter = total_tiles > blockIdx.x ? (total_tiles - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
+    if (niter == 0) return;
+
+    // tile geometry (segment, first column, limit, 16-byte-vector ok) and staging
+    struct Geo {
+        float* const* ptrs;
+        int64_t col0, lim;
+        bool vec_ok;
+    };
+    auto geo = [&](int64_t tile) {
+        int lo = 0, hi = nseg;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (tile_off[mid] <= tile) lo = mid; else hi = mid;
+        }
+        Geo gq;
+        gq.ptrs = seg_ptrs + (int64_t)lo * n_slots;
+        gq.col0 = (tile - tile_off[lo]) * TW;
+        gq.lim = seg_len[lo];
+        gq.vec_ok = seg_vec[lo] != 0;
+        return gq;
+    };
+    F R[E4];
+    auto stage = [&](const Geo& gq) {
+#pragma unroll
+        for (int j = 0; j < E4; ++j) {
+            const int k = (wave * 64 + kTPB * j) / C4;            // wave-uniform slot
+            if ((need >> k) & 1ull) {
+                const int64_t c = gq.col0 + (int64_t)((wave * 64 + kTPB * j) % C4 + lane) * 4;
+                const float* row = gq.ptrs[k];
+                if (gq.vec_ok && c + 4 <= gq.lim) {
+                    R[j] = ld<NT, F>(row + c);
+                } else {
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) R[j][t] = (c + t < gq.lim) ? ld1(row + c + t) : 0.0f;
+                }
+            }
+        }
+    };
+
+    // deal the items (row r, pass q) = r * NQ + q to the waves: wave 0 ranks them by weight
+    if (wave == 0) {
+        const int r = lane / NQ;
+        const int w = (lane < NI && r < n_local && deg[r] > 0) ? deg[r] + 1 : 0;
+        int rank = 0;
+        for (int j = 0; j < NI; ++j) {
+            const int wj = __builtin_amdgcn_readlane(w, j);
+            rank += (wj > w) || (wj == w && j < lane);
+        }
+        const int round = rank >> 2, within = rank & 3;
+        if (lane < NI) wl[(round & 1) ? 3 - within : within][round] = w > 0 ? lane : -1;
+    }
+    Geo cur = geo(blockIdx.x);
+    stage(cur);
+    __syncthreads();
+    // ranks grow along a wave's list, so its unused (-1) entries form a suffix
+    int nmy = 0;
+    while (nmy < NI / 4 && wl[wave][nmy] >= 0) ++nmy;
+    nmy = __builtin_amdgcn_readfirstlane(nmy);
+
+    for (int64_t i = 0; i < niter; ++i) {
+        if (i) __syncthreads();                  // every wave is done reading the previous tile
+#pragma unroll
+        for (int j = 0; j < E4; ++j) {
+            const int k = (wave * 64 + kTPB * j) / C4;
+            if ((need >> k) & 1ull) lds[k * C4 + (wave * 64 + kTPB * j) % C4 + lane] = R[j];
+        }
+        __syncthreads();
+        Geo nxt = cur;
+        if (i + 1 < niter) {                     // next tile's loads fly while this one is mixed
+            nxt = geo(blockIdx.x + (i + 1) * gridDim.x);
+            stage(nxt);
+        }
+        auto finish = [&](int it, F acc) {
+            const int r = it / NQ;
+            const int col = (it % NQ) * 64 + lane;
+            const F xs = lds[r * C4 + col];
+            const float s = sw[r];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) acc[t] = __builtin_fmaf(s, xs[t], acc[t]);
+            const int64_t c = cur.col0 + (int64_t)col * 4;
+            store_one<4, NT>(cur.ptrs[r], c, cur.lim, cur.vec_ok && c + 4 <= cur.lim, acc);
+        };
+        int p = 0;
+        for (; p + 1 < nmy; p += 2) {            // two items interleaved
+            const int ia = __builtin_amdgcn_readfirstlane(wl[wave][p]);
+            const int ib = __builtin_amdgcn_readfirstlane(wl[wave][p + 1]);
+            const int ra = ia / NQ, rb = ib / NQ;
+            const int ca = (ia % NQ) * 64 + lane, cb = (ib % NQ) * 64 + lane;
+            const int da = deg[ra], db = deg[rb];
+            const int dmin = da < db ? da : db;
+            F a = F{0.0f, 0.0f, 0.0f, 0.0f}, b = F{0.0f, 0.0f, 0.0f, 0.0f};
+            int e = 0;
+            for (; e < dmin; ++e) {
+                const int sa = __builtin_amdgcn_readfirstlane(src[ra * M + e]);
+                const int sb = __builtin_amdgcn_readfirstlane(src[rb * M + e]);
+                const F xa = lds[sa * C4 + ca];
+                const F xb = lds[sb * C4 + cb];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    a[t] = __builtin_fmaf(alpha, xa[t], a[t]);
+                    b[t] = __builtin_fmaf(alpha, xb[t], b[t]);
+                }
+            }
+            for (int ea = e; ea < da; ++ea) {
+                const F xa = lds[__builtin_amdgcn_readfirstlane(src[ra * M + ea]) * C4 + ca];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) a[t] = __builtin_fmaf(alpha, xa[t], a[t]);
+            }
+            for (int eb = e; eb < db; ++eb) {
+                const F xb = lds[__builtin_amdgcn_readfirstlane(src[rb * M + eb]) * C4 + cb];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) b[t] = __builtin_fmaf(alpha, xb[t], b[t]);
+            }
+            finish(ia, a);
+            finish(ib, b);
+        }
+        if (p < nmy) {
+            const int ia = __builtin_amdgcn_readfirstlane(wl[wave][p]);
+            const int ra = ia / NQ, ca = (ia % NQ) * 64 + lane;
+            F a = F{0.0f, 0.0f, 0.0f, 0.0f};
+            for (int e = 0; e < deg[ra]; ++e) {
+                const F xa = lds[__builtin_amdgcn_readfirstlane(src[ra * M + e]) * C4 + ca];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) a[t] = __builtin_fmaf(alpha, xa[t], a[t]);
+            }
+            finish(ia, a);
+        }
+        cur = nxt;
+    }
+}
+
 struct Cfg {
     int vec, ns;
 };
@@ -428,6 +593,8 @@ struct Tune {
     int chunked = 0;     // single-segment layouts: 1 = equal contiguous chunk per workgroup, 0 = tile stride
     int grid = 0;        // > 0: exact persistent grid size (overrides blocks_per_cu)
     int readlane_min = 32;  // LDS kernel: slot counts >= this fetch a step's slots with one read + v_readlane
+    int rows = 2;        // row-per-wave kernel: 2 = every slot count (<= 8 slots with unroll 1 / 2),
+                         // 1 = 9-64 slots only (<= 8: register-indexed / LDS-column), 0 = never
 };
 Tune g_tune;
 
@@ -464,6 +631,17 @@ int launch(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_o
     hipLaunchKernelGGL((mix_kernel<VEC, NS, U, NT, PF>), dim3((unsigned)grid_for(total_tiles)), dim3(kTPB),
                        0, st, seg_ptrs, seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan,
                        iter, n_local, M, alpha, mode);
+    MX_LAUNCH_CHECK();
+    return MX_OK;
+}
+
+template <int NS, int TW, bool NT>
+int launch_rows(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_off,
+                const uint8_t* seg_vec, int nseg, int n_slots, const int32_t* plan, int64_t iter,
+                int n_local, int M, float alpha, int64_t total_tiles, hipStream_t st) {
+    hipLaunchKernelGGL((mix_kernel_rows<NS, TW, NT>), dim3((unsigned)grid_for(total_tiles)), dim3(kTPB),
+                       0, st, seg_ptrs, seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan,
+                       iter, n_local, M, alpha);
     MX_LAUNCH_CHECK();
     return MX_OK;
 }
@@ -513,6 +691,9 @@ extern "C" int mx_mix_set(const char* key, int value) {
     } else if (!strcmp(key, "chunked")) {
         slot = &g_tune.chunked;
         value = value ? 1 : 0;
+    } else if (!strcmp(key, "rows")) {
+        MX_CHECK(value >= 0 && value <= 2, "mx_mix_set: rows %d", value);
+        slot = &g_tune.rows;
     }
     MX_CHECK(slot, "mx_mix_set: unknown key '%s'", key);
     *slot = value;
@@ -529,8 +710,18 @@ extern "C" int mx_mix_get(const char* key) {
     if (!strcmp(key, "chunked")) return g_tune.chunked;
     if (!strcmp(key, "grid")) return g_tune.grid;
     if (!strcmp(key, "readlane_min")) return g_tune.readlane_min;
+    if (!strcmp(key, "rows")) return g_tune.rows;
     mx::set_error("mx_mix_get: unknown key '%s'", key);
     return MX_ERR_INVALID;
+}
+
+// mirrors mx_gossip_mix's dispatch
+extern "C" const char* mx_mix_kernel_name(int n_slots) {
+    const Cfg c = pick(n_slots);
+    if (c.vec == 0) return "";
+    if ((g_tune.rows && c.ns >= 16) || (g_tune.rows == 2 && unroll_for(8) <= 2)) return "mix_kernel_rows";
+    if (g_tune.regidx && c.ns == 8) return "mix_kernel_reg";
+    return "mix_kernel";
 }
 
 extern "C" int mx_mix_layout(const int64_t* seg_len_host, int nseg, int n_slots, int64_t* tile_off_host) {
@@ -575,6 +766,15 @@ extern "C" int mx_gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_
         case 1: return launch_reg<N, U, true, false>(MX_ARGS);                \
         case 2: return launch_reg<N, U, false, U == 1>(MX_ARGS);              \
         default: return launch_reg<N, U, true, U == 1>(MX_ARGS);              \
+    }
+    if ((g_tune.rows && c.ns >= 16) || (g_tune.rows == 2 && unroll_for(8) <= 2)) {
+        const bool nt = g_tune.nontemporal != 0;
+        if (c.ns == 8 && unroll_for(8) == 2)
+            return nt ? launch_rows<8, 2048, true>(MX_ARGS) : launch_rows<8, 2048, false>(MX_ARGS);
+        if (c.ns == 8) return nt ? launch_rows<8, 1024, true>(MX_ARGS) : launch_rows<8, 1024, false>(MX_ARGS);
+        if (c.ns == 16) return nt ? launch_rows<16, 1024, true>(MX_ARGS) : launch_rows<16, 1024, false>(MX_ARGS);
+        if (c.ns == 32) return nt ? launch_rows<32, 512, true>(MX_ARGS) : launch_rows<32, 512, false>(MX_ARGS);
+        return nt ? launch_rows<64, 256, true>(MX_ARGS) : launch_rows<64, 256, false>(MX_ARGS);
     }
     if (g_tune.regidx && c.ns == 8) {
         if (unroll_for(8) == 4) { MX_DISPATCH_REG(8, 4) }

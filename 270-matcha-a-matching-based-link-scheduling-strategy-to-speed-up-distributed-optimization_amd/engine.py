@@ -22,12 +22,18 @@ from ._lib import MXError, check, lib, require_device, stream_ptr
 
 ROW_ALIGN = 64  # arena rows padded to 256 B
 
-TUNE_KEYS = ("blocks_per_cu", "unroll", "nontemporal", "prefetch", "regidx", "chunked", "grid", "readlane_min")
+TUNE_KEYS = ("blocks_per_cu", "unroll", "nontemporal", "prefetch", "regidx", "chunked", "grid", "readlane_min",
+             "rows")
 
 
 def mix_tuning():
     """Current mixing-kernel knobs (include/matcha_gossip.h, mx_mix_set)."""
     return {k: int(lib.mx_mix_get(k.encode())) for k in TUNE_KEYS}
+
+
+def mix_kernel_name(n_slots):
+    """The kernel mx_gossip_mix launches for n_slots under the current knobs."""
+    return lib.mx_mix_kernel_name(int(n_slots)).decode()
 
 
 def set_mix_tuning(**knobs):

@@ -311,7 +311,7 @@ def main():
                                       (f", placement {args.placement}" if world > 1 else ""),
                        "placement": group.placement if world > 1 else None,
                        "transport": args.transport if world > 1 else None},
-            "roofline": {"bound": "hbm", "kernel": "mix_kernel (mx_gossip_mix)",
+            "roofline": {"bound": "hbm", "kernel": f"{pkg.engine.mix_kernel_name(eng.n_slots)} (mx_gossip_mix)",
                          "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK, "traffic": traffic,
                          "traffic_source": traffic_src, "bytes_per_launch": mix_bytes,

@@ -102,10 +102,16 @@ int mx_mix_tile(int n_slots);
  *   grid           > 0: exact persistent grid size (overrides blocks_per_cu); 0 = CUs x blocks_per_cu
  *   readlane_min   LDS kernel: slot-count classes >= this (16 / 32 / 64) fetch one step's slots with
  *                  one LDS read + v_readlane and keep short chains by select (default 32)
+ *   rows           row-per-wave kernel (tile staged in LDS, each wave walks whole rows' own
+ *                  partner lists): 2 = every slot count (default; <= 8 slots needs unroll 1 or 2),
+ *                  1 = 9-64 slots only, 0 = never
  * "unroll" changes the tile size: rebuild layouts (mx_mix_layout) after setting it.
- * mx_mix_get returns the current value (negative on an unknown key). */
+ * mx_mix_get returns the current value (negative on an unknown key).
+ * mx_mix_kernel_name: the kernel mx_gossip_mix launches for n_slots under the current knobs
+ * ("mix_kernel_rows", "mix_kernel_reg", "mix_kernel"; "" when n_slots > 64). */
 int mx_mix_set(const char* key, int value);
 int mx_mix_get(const char* key);
+const char* mx_mix_kernel_name(int n_slots);
 int mx_mix_layout(const int64_t* seg_len_host, int nseg, int n_slots, int64_t* tile_off_host);
 int mx_gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev,
                   const int64_t* tile_off_dev, const uint8_t* seg_vec_dev, int nseg,

@@ -284,50 +284,72 @@ VARIANTS = [(bpc, u, nt, pf, rg, ch) for bpc in (1, 5) for u in (1, 2, 4) for nt
 
 @pytest.mark.parametrize("bpc,u,nt,pf,rg,ch", VARIANTS)
 def test_mix_every_tuning_variant(pkg, O, bpc, u, nt, pf, rg, ch):
-    """Each kernel variant (LDS / register-indexed, unroll, non-temporal, prefetch, grid, chunked
-    vs tile-strided) is bit-exact on a flat arena, ragged multi-segment layouts and a 16-slot graph."""
+    """Each kernel variant for <= 8 slots besides the default row kernel (LDS-column /
+    register-indexed, unroll, non-temporal, prefetch, grid, chunked vs tile-strided) is bit-exact on
+    a flat arena, ragged multi-segment layouts and a 16-slot graph (row kernel)."""
     saved = pkg.engine.mix_tuning()
     try:
         pkg.engine.set_mix_tuning(blocks_per_cu=bpc, unroll=u, nontemporal=nt, prefetch=pf, regidx=rg,
-                                  chunked=ch)
-        for gid, lens in ((0, [1, 3, 1024, 1027, 5, 4096 + 3, 0, 77, 10_000]), (2, [1, 3, 1027, 5, 9000]),
-                          (0, [300_001])):
-            n = pkg.GRAPH_SIZES[gid]
-            gp = pkg.GraphProcessor(pkg.select_graph(gid), 1.0, 0, n, 4, True)
-            M = len(gp.neighbors_info)
-            flags = np.ones((3, M), np.uint8)
-            flags[1, 1::2] = 0
-            flags[2, ::3] = 0
-            topo = Topo(gp.neighbors_info, 0.21, flags)
-            eng = pkg.GossipEngine(topo)
-            P = sum(lens)
-            X = np.stack([O.synth(300 + i, P) for i in range(n)])
-            big = torch.from_numpy(np.concatenate([X, X[:, :4]], axis=1)).cuda()
-            base = 1 if gid == 2 else 0
-            cuts = np.cumsum([0] + lens)
-            ptrs = [[big[i].data_ptr() + 4 * (base + int(cuts[s])) for s in range(len(lens))] for i in range(n)]
-            big[:, base:base + P] = torch.from_numpy(X).cuda()
-            lay = pkg.Layout(lens, ptrs, eng.n_slots)
-            for it, f in enumerate(flags):
-                eng.mix(it, lay)
-                X = O.decen_round(X, topo.neighbors_info, f, 0.21)
-            torch.cuda.synchronize()
-            got = big[:, base:base + P].cpu().numpy()
-            assert np.array_equal(got.view(np.uint32), X.view(np.uint32)), f"graph {gid} lens {lens}"
+                                  chunked=ch, rows=1)
+        _layouts_bit_exact(pkg, O)
     finally:
         pkg.engine.set_mix_tuning(**saved)
 
 
-@pytest.mark.parametrize("readlane_min", [32, 16, 128])
+@pytest.mark.parametrize("bpc,nt,u", [(1, 0, 1), (2, 1, 1), (5, 1, 1), (4, 0, 1), (2, 1, 2), (1, 0, 2)])
+def test_mix_row_kernel_for_eight_slots(pkg, O, bpc, nt, u):
+    """rows = 2 routes <= 8 slots through the row-per-wave kernel too: bit-exact on the same
+    layouts (flat, ragged multi-segment, unaligned) as every other variant."""
+    saved = pkg.engine.mix_tuning()
+    try:
+        pkg.engine.set_mix_tuning(blocks_per_cu=bpc, nontemporal=nt, rows=2, unroll=u)
+        _layouts_bit_exact(pkg, O)
+    finally:
+        pkg.engine.set_mix_tuning(**saved)
+
+
+def _layouts_bit_exact(pkg, O):
+    """flat arena, ragged multi-segment layouts (graph 0) and an unaligned 16-slot graph, 3 rounds"""
+    for gid, lens in ((0, [1, 3, 1024, 1027, 5, 4096 + 3, 0, 77, 10_000]), (2, [1, 3, 1027, 5, 9000]),
+                      (0, [300_001])):
+        n = pkg.GRAPH_SIZES[gid]
+        gp = pkg.GraphProcessor(pkg.select_graph(gid), 1.0, 0, n, 4, True)
+        M = len(gp.neighbors_info)
+        flags = np.ones((3, M), np.uint8)
+        flags[1, 1::2] = 0
+        flags[2, ::3] = 0
+        topo = Topo(gp.neighbors_info, 0.21, flags)
+        eng = pkg.GossipEngine(topo)
+        P = sum(lens)
+        X = np.stack([O.synth(300 + i, P) for i in range(n)])
+        big = torch.from_numpy(np.concatenate([X, X[:, :4]], axis=1)).cuda()
+        base = 1 if gid == 2 else 0
+        cuts = np.cumsum([0] + lens)
+        ptrs = [[big[i].data_ptr() + 4 * (base + int(cuts[s])) for s in range(len(lens))] for i in range(n)]
+        big[:, base:base + P] = torch.from_numpy(X).cuda()
+        lay = pkg.Layout(lens, ptrs, eng.n_slots)
+        for it, f in enumerate(flags):
+            eng.mix(it, lay)
+            X = O.decen_round(X, topo.neighbors_info, f, 0.21)
+        torch.cuda.synchronize()
+        got = big[:, base:base + P].cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), X.view(np.uint32)), f"graph {gid} lens {lens}"
+
+
+@pytest.mark.parametrize("knobs", [{"rows": 1}, {"rows": 0, "readlane_min": 32}, {"rows": 0, "readlane_min": 16},
+                                   {"rows": 0, "readlane_min": 128}, {"rows": 1, "nontemporal": 0, "blocks_per_cu": 1}],
+                         ids=["rows", "lds-rl32", "lds-rl16", "lds-rl128", "rows-t-bpc1"])
 @pytest.mark.parametrize("n,p,seed,P", [(32, 0.2, 7, 70_001), (64, 0.1, 1234, 50_003), (24, 0.3, 3, 9_999),
-                                        (16, 0.4, 5, 1024 * 7), (64, 0.1, 1234, 256 * 9)])
-def test_mix_er_graphs_wide_configs(pkg, O, n, p, seed, P, readlane_min):
-    """Random ER topologies decomposed by the host path: 16 / 24 / 32 / 64 slots exercise the
-    NS 16 / 32 / 64 LDS kernels with both edge-step forms (per-row lookups, one read +
-    v_readlane); MATCHA-like random flags, 4 rounds, ragged and whole-tile widths, bit-exact."""
+                                        (16, 0.4, 5, 1024 * 7), (64, 0.1, 1234, 256 * 9), (48, 0.15, 11, 333),
+                                        (12, 0.5, 2, 100_003)])
+def test_mix_er_graphs_wide_configs(pkg, O, n, p, seed, P, knobs):
+    """Random ER topologies decomposed by the host path: 12-64 slots exercise the NS 16 / 32 / 64
+    kernels -- the row-per-wave kernel (default) and the LDS-column kernel with both edge-step
+    forms (per-row lookups, one read + v_readlane); MATCHA-like random flags, 4 rounds, ragged,
+    sub-tile and whole-tile widths, bit-exact."""
     import random as pyrandom
     saved = pkg.engine.mix_tuning()
-    pkg.engine.set_mix_tuning(readlane_min=readlane_min)
+    pkg.engine.set_mix_tuning(**knobs)
     pyrandom.seed(0)
     gp = pkg.GraphProcessor(pkg.erdos_renyi(n, p, seed), 1.0, 0, n, 4, False)
     M = len(gp.neighbors_info)

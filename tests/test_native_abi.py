@@ -95,3 +95,22 @@ def test_exchange_plan_moves_each_row_once_per_link(pkg):
         assert (len(sends), len(recvs)) == ((3, 4) if rank == 0 else (4, 3))
         assert sends == ([0, 1, 3] if rank == 0 else [4, 5, 6, 7])
         assert pkg.engine.max_incoming_remote(partner, base, nl) == len(recvs)
+
+
+def test_mix_kernel_dispatch_names(pkg):
+    """mx_mix_kernel_name mirrors mx_gossip_mix's dispatch under the knobs (host-only)."""
+    E = pkg.engine
+    saved = E.mix_tuning()
+    try:
+        assert saved["rows"] == 2
+        assert [E.mix_kernel_name(s) for s in (1, 8, 9, 16, 33, 64)] == ["mix_kernel_rows"] * 6
+        assert E.mix_kernel_name(65) == ""
+        E.set_mix_tuning(rows=1)
+        assert [E.mix_kernel_name(s) for s in (8, 16, 64)] == ["mix_kernel_reg", "mix_kernel_rows", "mix_kernel_rows"]
+        E.set_mix_tuning(rows=0, regidx=0)
+        assert [E.mix_kernel_name(s) for s in (8, 16)] == ["mix_kernel", "mix_kernel"]
+        E.set_mix_tuning(rows=2, regidx=1, unroll=4)
+        assert [E.mix_kernel_name(s) for s in (8, 16)] == ["mix_kernel_reg", "mix_kernel_rows"]
+        assert pkg.lib.mx_mix_set(b"rows", 3) != 0
+    finally:
+        E.set_mix_tuning(**saved)

@@ -31,7 +31,7 @@ def timeit(fn, reps=20, warm=3):
 
 TOTAL = int(os.environ.get("MIXWIDE_TOTAL", 8 * 25_600_000))
 if os.environ.get("MIXWIDE_TUNE"):
-    KEYS = ("blocks_per_cu", "unroll", "nontemporal", "prefetch", "regidx", "chunked", "grid", "readlane_min")
+    KEYS = ("blocks_per_cu", "unroll", "nontemporal", "prefetch", "regidx", "chunked", "grid", "readlane_min", "rows")
     pkg.engine.set_mix_tuning(**dict(zip(KEYS, (int(v) for v in os.environ["MIXWIDE_TUNE"].split(",")))))
 print(json.dumps({"tuning": pkg.engine.mix_tuning()}))
 cases = [("graph0", 8, None), ("graph2", 16, None), ("er32", 32, 0.2), ("er64", 64, 0.1)]
