@@ -21,8 +21,11 @@
 // Scheduling: by default tiles (never straddling a tensor) are strided over a persistent grid,
 // so at any moment the whole chip streams one narrow window of every row (DRAM row locality);
 // optionally (knob "chunked") a single-segment layout is split into equal contiguous ranges.
-// The default kernel for n_slots <= 8 is the register-indexed variant (mix_kernel_reg): one
-// register vector per lane indexed through s_set_gpr_idx by the wave-uniform slot, no LDS.
+// Three kernels share this contract (knob "rows" picks): the default row-per-wave kernel
+// (mix_kernel_rows: the tile is staged in LDS by the whole workgroup, then each wave walks whole
+// rows' own partner lists -- the fastest at every slot count), the register-indexed kernel for
+// <= 8 slots (mix_kernel_reg: one register vector per lane indexed through s_set_gpr_idx, no
+// LDS) and the LDS-column kernel (mix_kernel: per-lane columns, every row to the max degree).
 #include "mx_common.h"
 
 namespace {
