@@ -258,6 +258,7 @@ def main():
     hbm_bytes = []
     link_bytes = []
     pair_bytes = []
+    total_bytes = []
     for f in flags:
         deg = np.zeros(n, int)
         for g in range(len(f)):
@@ -279,6 +280,7 @@ def main():
         remote = sum(1 for p, b in moved if b == rank)
         hbm_bytes.append(2 * act * P * 4 + remote * P * 4)
         link_bytes.append(max(links.values()) if links else 0)
+        total_bytes.append(sum(links.values()))
         pair = {}
         for (a, b), v in links.items():
             key = (min(a, b), max(a, b))
@@ -334,6 +336,8 @@ def main():
                            "max_pair_bytes_both_directions": pb,
                            "achieved_both_directions": pb / round_s / 1e9,
                            "frac_both_directions": pb / round_s / XGMI_LINK_PEAK,
+                           "aggregate_bytes_per_round": float(np.mean(total_bytes)),
+                           "aggregate_achieved": float(np.mean(total_bytes)) / round_s / 1e9,
                            "round_ms": 1e3 * round_s, "round_ms_events_rank0": avg_ms,
                            "note": "busiest GPU pair: bytes that cross it per round (one direction, and "
                                    "both directions summed) / whole-job round time (exchange + mix), "
