@@ -7,7 +7,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_native", "libmatcha_gossip.so")
+# MX_GOSSIP_LIB: another build of the same library (A/B timing of kernel variants in one run)
+LIB_PATH = os.environ.get("MX_GOSSIP_LIB") or os.path.join(_HERE, "_native", "libmatcha_gossip.so")
 
 c_int, c_i64, c_u64, c_f32, c_f64 = ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, ctypes.c_float, ctypes.c_double
 c_p = ctypes.c_void_p
