@@ -82,10 +82,20 @@ def check(rc, what=""):
 
 
 def stream_ptr(stream=None):
-    """hipStream_t of a torch stream (default: torch's current stream on the current device)."""
+    """hipStream_t of a torch stream (default: torch's current stream on the current device).
+    The default is read as a raw handle (no torch.cuda.Stream object is built): a small-row round
+    is launch-bound, and building that object cost about as much as the kernel launch."""
+    if stream is not None:
+        return stream.cuda_stream
+    return _raw_stream(_cur_dev())
+
+
+def _bind_stream_getters():
     import torch
-    s = stream if stream is not None else torch.cuda.current_stream()
-    return ctypes.c_void_p(s.cuda_stream)
+    return torch._C._cuda_getCurrentRawStream, torch._C._cuda_getDevice
+
+
+_raw_stream, _cur_dev = _bind_stream_getters()
 
 
 def require_device():

@@ -412,7 +412,11 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_reg(float* const* __restrict_
 // per lane.  The LDS-column kernel instead runs every row for max-degree steps in every lane,
 // with per-row lookups and selects -- VALU-bound at 32-64 slots.  Items are dealt to the 4 waves
 // by weight (degree + 1, ranked in wave 0, snake order), two items interleaved per wave for ILP.
-template <int NS, int TW, bool NT>
+//
+// SPLIT > 1 (small rows, fewer layout tiles than the persistent grid): each layout tile of
+// TW * SPLIT columns is worked as SPLIT sub-tiles of TW columns, so a 181k-parameter round
+// spreads over every CU instead of a few dozen (layouts and tile_off stay in layout-tile units).
+template <int NS, int TW, bool NT, int SPLIT = 1>
 __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict__ seg_ptrs,
                                                         const int64_t* __restrict__ seg_len,
                                                         const int64_t* __restrict__ tile_off,
@@ -437,7 +441,8 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int64_t niter = total_tiles > blockIdx.x ? (total_tiles - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
+    const int64_t total_work = total_tiles * SPLIT;
+    const int64_t niter = total_work > blockIdx.x ? (total_work - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
     if (niter == 0) return;
 
     // tile geometry (segment, first column, limit, 16-byte-vector ok) and staging
@@ -446,7 +451,8 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict
         int64_t col0, lim;
         bool vec_ok;
     };
-    auto geo = [&](int64_t tile) {
+    auto geo = [&](int64_t work) {
+        const int64_t tile = work / SPLIT;
         int lo = 0, hi = nseg;
         while (hi - lo > 1) {
             const int mid = (lo + hi) >> 1;
@@ -454,7 +460,7 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict
         }
         Geo gq;
         gq.ptrs = seg_ptrs + (int64_t)lo * n_slots;
-        gq.col0 = (tile - tile_off[lo]) * TW;
+        gq.col0 = (tile - tile_off[lo]) * (TW * SPLIT) + (work % SPLIT) * TW;
         gq.lim = seg_len[lo];
         gq.vec_ok = seg_vec[lo] != 0;
         return gq;
@@ -598,6 +604,8 @@ struct Tune {
     int readlane_min = 32;  // LDS kernel: slot counts >= this fetch a step's slots with one read + v_readlane
     int rows = 2;        // row-per-wave kernel: 2 = every slot count (<= 8 slots with unroll 1 / 2),
                          // 1 = 9-64 slots only (<= 8: register-indexed / LDS-column), 0 = never
+    int split = 0;       // row kernel sub-tiles per layout tile: 0 = auto (enough work items for
+                         // the persistent grid), 1 / 2 / 4 = forced (capped by the geometry)
 };
 Tune g_tune;
 
@@ -620,10 +628,23 @@ int cu_count() {
 
 // grid: CUs x blocks_per_cu persistent workgroups, never more than there are tiles; a single
 // segment is split into equal contiguous chunks (chunked = 1)
+inline int64_t grid_target() {
+    return g_tune.grid > 0 ? (int64_t)g_tune.grid : (int64_t)cu_count() * g_tune.blocks_per_cu;
+}
 inline int64_t grid_for(int64_t total_tiles) {
-    int64_t grid = g_tune.grid > 0 ? (int64_t)g_tune.grid : (int64_t)cu_count() * g_tune.blocks_per_cu;
+    int64_t grid = grid_target();
     if (grid > total_tiles) grid = total_tiles;
     return grid < 1 ? 1 : grid;
+}
+
+// row kernel sub-tiles per layout tile: a sub-tile keeps >= 256 columns (one wave pass), and
+// auto picks the smallest split that gives every persistent workgroup a work item
+int row_split(int ns, int64_t total_tiles) {
+    const int cap = ns == 64 ? 1 : (ns == 32 ? 2 : 4);
+    if (g_tune.split > 0) return g_tune.split < cap ? g_tune.split : cap;
+    int s = 1;
+    while (s < cap && total_tiles * s < grid_target()) s *= 2;
+    return s;
 }
 
 template <int VEC, int NS, int U, bool NT, bool PF>
@@ -638,11 +659,11 @@ int launch(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_o
     return MX_OK;
 }
 
-template <int NS, int TW, bool NT>
+template <int NS, int TW, bool NT, int SPLIT = 1>
 int launch_rows(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_off,
                 const uint8_t* seg_vec, int nseg, int n_slots, const int32_t* plan, int64_t iter,
                 int n_local, int M, float alpha, int64_t total_tiles, hipStream_t st) {
-    hipLaunchKernelGGL((mix_kernel_rows<NS, TW, NT>), dim3((unsigned)grid_for(total_tiles)), dim3(kTPB),
+    hipLaunchKernelGGL((mix_kernel_rows<NS, TW, NT, SPLIT>), dim3((unsigned)grid_for(total_tiles * SPLIT)), dim3(kTPB),
                        0, st, seg_ptrs, seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan,
                        iter, n_local, M, alpha);
     MX_LAUNCH_CHECK();
@@ -697,6 +718,9 @@ extern "C" int mx_mix_set(const char* key, int value) {
     } else if (!strcmp(key, "rows")) {
         MX_CHECK(value >= 0 && value <= 2, "mx_mix_set: rows %d", value);
         slot = &g_tune.rows;
+    } else if (!strcmp(key, "split")) {
+        MX_CHECK(value == 0 || value == 1 || value == 2 || value == 4, "mx_mix_set: split %d", value);
+        slot = &g_tune.split;
     }
     MX_CHECK(slot, "mx_mix_set: unknown key '%s'", key);
     *slot = value;
@@ -714,6 +738,7 @@ extern "C" int mx_mix_get(const char* key) {
     if (!strcmp(key, "grid")) return g_tune.grid;
     if (!strcmp(key, "readlane_min")) return g_tune.readlane_min;
     if (!strcmp(key, "rows")) return g_tune.rows;
+    if (!strcmp(key, "split")) return g_tune.split;
     mx::set_error("mx_mix_get: unknown key '%s'", key);
     return MX_ERR_INVALID;
 }
@@ -774,10 +799,13 @@ extern "C" int mx_gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_
         const bool nt = g_tune.nontemporal != 0;
         if (c.ns == 8 && unroll_for(8) == 2)
             return nt ? launch_rows<8, 2048, true>(MX_ARGS) : launch_rows<8, 2048, false>(MX_ARGS);
-        if (c.ns == 8) return nt ? launch_rows<8, 1024, true>(MX_ARGS) : launch_rows<8, 1024, false>(MX_ARGS);
-        if (c.ns == 16) return nt ? launch_rows<16, 1024, true>(MX_ARGS) : launch_rows<16, 1024, false>(MX_ARGS);
-        if (c.ns == 32) return nt ? launch_rows<32, 512, true>(MX_ARGS) : launch_rows<32, 512, false>(MX_ARGS);
-        return nt ? launch_rows<64, 256, true>(MX_ARGS) : launch_rows<64, 256, false>(MX_ARGS);
+        const int sp = row_split(c.ns, total_tiles);
+#define MX_ROWS(N, TW, S) (nt ? launch_rows<N, TW, true, S>(MX_ARGS) : launch_rows<N, TW, false, S>(MX_ARGS))
+        if (c.ns == 8) return sp == 4 ? MX_ROWS(8, 256, 4) : sp == 2 ? MX_ROWS(8, 512, 2) : MX_ROWS(8, 1024, 1);
+        if (c.ns == 16) return sp == 4 ? MX_ROWS(16, 256, 4) : sp == 2 ? MX_ROWS(16, 512, 2) : MX_ROWS(16, 1024, 1);
+        if (c.ns == 32) return sp == 2 ? MX_ROWS(32, 256, 2) : MX_ROWS(32, 512, 1);
+        return MX_ROWS(64, 256, 1);
+#undef MX_ROWS
     }
     if (g_tune.regidx && c.ns == 8) {
         if (unroll_for(8) == 4) { MX_DISPATCH_REG(8, 4) }

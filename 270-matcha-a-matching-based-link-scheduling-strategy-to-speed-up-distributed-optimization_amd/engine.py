@@ -23,7 +23,7 @@ from ._lib import MXError, check, lib, require_device, stream_ptr
 ROW_ALIGN = 64  # arena rows padded to 256 B
 
 TUNE_KEYS = ("blocks_per_cu", "unroll", "nontemporal", "prefetch", "regidx", "chunked", "grid", "readlane_min",
-             "rows")
+             "rows", "split")
 
 
 def mix_tuning():
@@ -36,7 +36,11 @@ def mix_kernel_name(n_slots):
     return lib.mx_mix_kernel_name(int(n_slots)).decode()
 
 
+_TUNE_GEN = [0]     # bumped on every knob change: layouts re-check their tile size only then
+
+
 def set_mix_tuning(**knobs):
+    _TUNE_GEN[0] += 1
     for k, v in knobs.items():
         check(lib.mx_mix_set(k.encode(), int(v)), "mx_mix_set")
 
@@ -159,6 +163,9 @@ class Layout:
         self.seg_len = torch.from_numpy(seg_len).to("cuda")
         self.tile_off = torch.from_numpy(tile_off).to("cuda")
         self.seg_vec = torch.from_numpy(vec).to("cuda")
+        self.tune_gen = _TUNE_GEN[0]
+        self._args = (self.seg_ptrs.data_ptr(), self.seg_len.data_ptr(), self.tile_off.data_ptr(),
+                      self.seg_vec.data_ptr(), nseg, self.total_tiles, n_slots)
 
 
 class GossipEngine:
@@ -201,7 +208,8 @@ class GossipEngine:
         check(lib.mx_plan_build(self.flags_dev.data_ptr(), self.T, self.M, self.partner_dev.data_ptr(),
                                 self.n, None, self.rank, self.row_base, self.n_local, self.alpha,
                                 self.plan.data_ptr(), stream_ptr()), "mx_plan_build")
-        self.any_active = self.flags_host.any(axis=1)
+        self.any_active = self.flags_host.any(axis=1).tolist()
+        self._plan_ptr = self.plan.data_ptr()
 
     # ------------------------------------------------------------------ per round
     def exchange_plan(self, it):
@@ -237,13 +245,15 @@ class GossipEngine:
         return nrem.value
 
     def mix(self, it, layout, stream=None):
-        if layout.tile != lib.mx_mix_tile(layout.n_slots):
-            raise MXError("layout built for another mixing tile size (the unroll knob changed it)")
-        check(lib.mx_gossip_mix(layout.seg_ptrs.data_ptr(), layout.seg_len.data_ptr(),
-                                layout.tile_off.data_ptr(), layout.seg_vec.data_ptr(), layout.nseg,
-                                layout.total_tiles, layout.n_slots, self.plan.data_ptr(), int(it),
-                                self.n_local, self.M, self.alpha32, stream_ptr(stream)),
-              "mx_gossip_mix")
+        if layout.tune_gen != _TUNE_GEN[0]:
+            if layout.tile != lib.mx_mix_tile(layout.n_slots):
+                raise MXError("layout built for another mixing tile size (the unroll knob changed it)")
+            layout.tune_gen = _TUNE_GEN[0]
+        # one ctypes call per round with pre-resolved pointers (small rows are launch-bound)
+        rc = lib.mx_gossip_mix(*layout._args, self._plan_ptr, int(it), self.n_local, self.M, self.alpha32,
+                               stream_ptr(stream))
+        if rc:
+            check(rc, "mx_gossip_mix")
 
 
 def _params(model):

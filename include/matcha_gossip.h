@@ -105,6 +105,9 @@ int mx_mix_tile(int n_slots);
  *   rows           row-per-wave kernel (tile staged in LDS, each wave walks whole rows' own
  *                  partner lists): 2 = every slot count (default; <= 8 slots needs unroll 1 or 2),
  *                  1 = 9-64 slots only, 0 = never
+ *   split          row kernel: sub-tiles of 256+ columns per layout tile, so short rows still
+ *                  give every persistent workgroup work: 0 = auto (default), 1 / 2 / 4 = forced
+ *                  (capped at 4 for 8/16 slots, 2 for 32, 1 for 64); layouts are unaffected
  * "unroll" changes the tile size: rebuild layouts (mx_mix_layout) after setting it.
  * mx_mix_get returns the current value (negative on an unknown key).
  * mx_mix_kernel_name: the kernel mx_gossip_mix launches for n_slots under the current knobs

@@ -296,13 +296,15 @@ def test_mix_every_tuning_variant(pkg, O, bpc, u, nt, pf, rg, ch):
         pkg.engine.set_mix_tuning(**saved)
 
 
-@pytest.mark.parametrize("bpc,nt,u", [(1, 0, 1), (2, 1, 1), (5, 1, 1), (4, 0, 1), (2, 1, 2), (1, 0, 2)])
-def test_mix_row_kernel_for_eight_slots(pkg, O, bpc, nt, u):
+@pytest.mark.parametrize("bpc,nt,u,sp", [(1, 0, 1, 0), (2, 1, 1, 0), (5, 1, 1, 0), (4, 0, 1, 0), (2, 1, 2, 0),
+                                         (1, 0, 2, 0), (2, 1, 1, 1), (2, 1, 1, 2), (2, 1, 1, 4), (1, 0, 1, 4)])
+def test_mix_row_kernel_for_eight_slots(pkg, O, bpc, nt, u, sp):
     """rows = 2 routes <= 8 slots through the row-per-wave kernel too: bit-exact on the same
-    layouts (flat, ragged multi-segment, unaligned) as every other variant."""
+    layouts (flat, ragged multi-segment, unaligned) as every other variant, with the layout tile
+    worked whole or as 2 / 4 sub-tiles (split)."""
     saved = pkg.engine.mix_tuning()
     try:
-        pkg.engine.set_mix_tuning(blocks_per_cu=bpc, nontemporal=nt, rows=2, unroll=u)
+        pkg.engine.set_mix_tuning(blocks_per_cu=bpc, nontemporal=nt, rows=2, unroll=u, split=sp)
         _layouts_bit_exact(pkg, O)
     finally:
         pkg.engine.set_mix_tuning(**saved)
@@ -337,8 +339,10 @@ def _layouts_bit_exact(pkg, O):
 
 
 @pytest.mark.parametrize("knobs", [{"rows": 1}, {"rows": 0, "readlane_min": 32}, {"rows": 0, "readlane_min": 16},
-                                   {"rows": 0, "readlane_min": 128}, {"rows": 1, "nontemporal": 0, "blocks_per_cu": 1}],
-                         ids=["rows", "lds-rl32", "lds-rl16", "lds-rl128", "rows-t-bpc1"])
+                                   {"rows": 0, "readlane_min": 128}, {"rows": 1, "nontemporal": 0, "blocks_per_cu": 1},
+                                   {"rows": 1, "split": 1}, {"rows": 1, "split": 2}, {"rows": 1, "split": 4}],
+                         ids=["rows", "lds-rl32", "lds-rl16", "lds-rl128", "rows-t-bpc1", "rows-s1", "rows-s2",
+                              "rows-s4"])
 @pytest.mark.parametrize("n,p,seed,P", [(32, 0.2, 7, 70_001), (64, 0.1, 1234, 50_003), (24, 0.3, 3, 9_999),
                                         (16, 0.4, 5, 1024 * 7), (64, 0.1, 1234, 256 * 9), (48, 0.15, 11, 333),
                                         (12, 0.5, 2, 100_003)])

@@ -36,7 +36,7 @@ def timeit(fn, reps=40, warm=5):
     return float(np.median(ms)), float(ms.min())
 
 
-KEYS = ("blocks_per_cu", "unroll", "nontemporal", "prefetch", "regidx", "chunked", "grid", "readlane_min", "rows")
+KEYS = ("blocks_per_cu", "unroll", "nontemporal", "prefetch", "regidx", "chunked", "grid", "readlane_min", "rows", "split")
 configs = []
 for spec in sys.argv[1:] or ["sweep"]:
     if spec == "sweep":
@@ -47,7 +47,7 @@ for spec in sys.argv[1:] or ["sweep"]:
     else:
         cfg = tuple(int(x) for x in spec.split(","))
         configs.append(cfg)
-DEFAULT_TAIL = (0, 32, 1)      # grid, readlane_min, rows
+DEFAULT_TAIL = (0, 32, 1, 0)   # grid, readlane_min, rows, split
 configs = [c + DEFAULT_TAIL[len(c) - len(KEYS):] if len(c) < len(KEYS) else c for c in configs]
 src = torch.empty((n, P), device="cuda")
 dst = torch.empty_like(src)
@@ -59,7 +59,7 @@ for cfg in configs:
     pkg.engine.set_mix_tuning(**dict(zip(KEYS, cfg)))
     lay = pkg.Layout([P], [[grp.arena[r].data_ptr()] for r in range(n)], grp.engine.n_slots)
     med, mn = timeit(lambda: grp.engine.mix(0, lay))
-    res.append({"cfg": "bpc=%d U=%d NT=%d PF=%d REG=%d CH=%d GRID=%d RL=%d ROWS=%d" % cfg, "med_us": med * 1e3, "min_us": mn * 1e3,
+    res.append({"cfg": "bpc=%d U=%d NT=%d PF=%d REG=%d CH=%d GRID=%d RL=%d ROWS=%d SPLIT=%d" % cfg, "med_us": med * 1e3, "min_us": mn * 1e3,
                 "TBps": BYTES / med / 1e9, "frac": BYTES / med / 1e9 / 8.0})
     print(json.dumps(res[-1]), flush=True)
 med, mn = timeit(lambda: dst.copy_(src))
