@@ -692,7 +692,8 @@ unsigned clamp_grid(int64_t n, int64_t per, int64_t cap) {
 }  // namespace
 
 int g_sample_stride = 0;   // 0 = auto (about kSampleTarget sampled elements per row)
-int g_compact_blocks = 2048;  // persistent compaction blocks over all rows
+int g_compact_blocks = 1024;  // persistent compaction blocks over all rows (tools/per_gpu.py sweep)
+int g_sample_pieces = 1;      // sampled 1024-element pieces per wave (sample_kernel grid)
 
 int64_t sample_stride(int64_t P) {
     const int64_t nc = n_chunks(P);
@@ -719,12 +720,18 @@ extern "C" int mx_topk_set(const char* key, int64_t value) {
         g_compact_blocks = (int)value;
         return MX_OK;
     }
+    if (!strcmp(key, "sample_pieces")) {
+        MX_CHECK(value >= 1 && value <= 1024, "mx_topk_set: sample_pieces %lld", (long long)value);
+        g_sample_pieces = (int)value;
+        return MX_OK;
+    }
     MX_CHECK(false, "mx_topk_set: unknown key '%s'", key);
 }
 
 extern "C" int64_t mx_topk_get(const char* key) {
     if (key && !strcmp(key, "sample_stride")) return g_sample_stride;
     if (key && !strcmp(key, "compact_blocks")) return g_compact_blocks;
+    if (key && !strcmp(key, "sample_pieces")) return g_sample_pieces;
     mx::set_error("mx_topk_get: unknown key '%s'", key ? key : "(null)");
     return MX_ERR_INVALID;
 }
@@ -755,7 +762,7 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
     MX_CHECK(nc <= 0x7fffffff, "mx_topk_abs_diff_rows: P too large");
     const unsigned bgrid = clamp_grid(nc, 1, (g_compact_blocks + nrows - 1) / nrows);   // persistent
     const unsigned wgrid = (unsigned)((nc + kWaves - 1) / kWaves);          // one wave per chunk
-    const unsigned sgrid = clamp_grid(nsamp, 4 * kWaves, (1024 + nrows - 1) / nrows);
+    const unsigned sgrid = clamp_grid(nsamp, (int64_t)g_sample_pieces * kWaves, (1024 + nrows - 1) / nrows);
     const unsigned cgrid = clamp_grid(wgrid, 2, (2048 + nrows - 1) / nrows);
     const dim3 one(1, nrows);
 #define MX_L(kern, grid, tpb, ...)                                                 \

@@ -638,12 +638,13 @@ inline int64_t grid_for(int64_t total_tiles) {
 }
 
 // row kernel sub-tiles per layout tile: a sub-tile keeps >= 256 columns (one wave pass), and
-// auto picks the smallest split that gives every persistent workgroup a work item
+// auto picks the smallest split giving the persistent grid 1.5 work items per workgroup
+// (measured, 8 slots: 651 tiles run 11 % faster as 1302 sub-tiles, 977 tiles 5 % slower as 1954)
 int row_split(int ns, int64_t total_tiles) {
     const int cap = ns == 64 ? 1 : (ns == 32 ? 2 : 4);
     if (g_tune.split > 0) return g_tune.split < cap ? g_tune.split : cap;
     int s = 1;
-    while (s < cap && total_tiles * s < grid_target()) s *= 2;
+    while (s < cap && 2 * total_tiles * s < 3 * grid_target()) s *= 2;
     return s;
 }
 

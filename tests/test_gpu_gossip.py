@@ -246,19 +246,26 @@ def _topk_case(O, P, pattern):
     return x
 
 
-@pytest.mark.parametrize("stride", [0, 1, 16])
+@pytest.mark.parametrize("stride,pieces,blocks", [(0, 1, 1024), (1, 1, 1024), (16, 1, 1024), (0, 4, 2048),
+                                                  (16, 3, 77), (0, 2, 4096)])
 @pytest.mark.parametrize("pattern", ["layers", "sampled_large", "constant", "ties"])
-def test_topk_sampled_floor_exact(pkg, O, stride, pattern):
-    """The sampled candidate floor (and its device-side fallback) never changes the result."""
+def test_topk_sampled_floor_exact(pkg, O, stride, pieces, blocks, pattern):
+    """The sampled candidate floor (and its device-side fallback) never changes the result, for any
+    sampling grid (pieces per wave) or persistent compaction grid."""
     P, ratio = 2_000_001, 0.99
     x = _topk_case(O, P, pattern)
     k = O.topk_k(P, ratio)
     ov, oi = O.topk_abs(x, k)
+    saved = {key: int(pkg.lib.mx_topk_get(key)) for key in (b"sample_pieces", b"compact_blocks")}
     pkg._lib.check(pkg.lib.mx_topk_set(b"sample_stride", stride))
+    pkg._lib.check(pkg.lib.mx_topk_set(b"sample_pieces", pieces))
+    pkg._lib.check(pkg.lib.mx_topk_set(b"compact_blocks", blocks))
     try:
         v, i = pkg.get_top_k(torch.from_numpy(x).cuda(), ratio)
     finally:
         pkg.lib.mx_topk_set(b"sample_stride", 0)
+        for key, val in saved.items():
+            pkg.lib.mx_topk_set(key, val)
     assert np.array_equal(i.cpu().numpy(), oi)
     assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32))
 
