@@ -694,6 +694,8 @@ unsigned clamp_grid(int64_t n, int64_t per, int64_t cap) {
 int g_sample_stride = 0;   // 0 = auto (about kSampleTarget sampled elements per row)
 int g_compact_blocks = 1024;  // persistent compaction blocks over all rows (tools/per_gpu.py sweep)
 int g_sample_pieces = 1;      // sampled 1024-element pieces per wave (sample_kernel grid)
+int g_cand_chunks = 2;        // chunk regions per wave of cand_hist / cand_mark (fewer blocks =
+                              // fewer global histogram flushes onto the same 1024 / 512 bins)
 
 int64_t sample_stride(int64_t P) {
     const int64_t nc = n_chunks(P);
@@ -720,6 +722,11 @@ extern "C" int mx_topk_set(const char* key, int64_t value) {
         g_compact_blocks = (int)value;
         return MX_OK;
     }
+    if (!strcmp(key, "cand_chunks")) {
+        MX_CHECK(value >= 1 && value <= 4096, "mx_topk_set: cand_chunks %lld", (long long)value);
+        g_cand_chunks = (int)value;
+        return MX_OK;
+    }
     if (!strcmp(key, "sample_pieces")) {
         MX_CHECK(value >= 1 && value <= 1024, "mx_topk_set: sample_pieces %lld", (long long)value);
         g_sample_pieces = (int)value;
@@ -732,6 +739,7 @@ extern "C" int64_t mx_topk_get(const char* key) {
     if (key && !strcmp(key, "sample_stride")) return g_sample_stride;
     if (key && !strcmp(key, "compact_blocks")) return g_compact_blocks;
     if (key && !strcmp(key, "sample_pieces")) return g_sample_pieces;
+    if (key && !strcmp(key, "cand_chunks")) return g_cand_chunks;
     mx::set_error("mx_topk_get: unknown key '%s'", key ? key : "(null)");
     return MX_ERR_INVALID;
 }
@@ -763,7 +771,7 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
     const unsigned bgrid = clamp_grid(nc, 1, (g_compact_blocks + nrows - 1) / nrows);   // persistent
     const unsigned wgrid = (unsigned)((nc + kWaves - 1) / kWaves);          // one wave per chunk
     const unsigned sgrid = clamp_grid(nsamp, (int64_t)g_sample_pieces * kWaves, (1024 + nrows - 1) / nrows);
-    const unsigned cgrid = clamp_grid(wgrid, 2, (2048 + nrows - 1) / nrows);
+    const unsigned cgrid = clamp_grid(nc, (int64_t)g_cand_chunks * kWaves, (2048 + nrows - 1) / nrows);
     const dim3 one(1, nrows);
 #define MX_L(kern, grid, tpb, ...)                                                 \
     hipLaunchKernelGGL(kern, grid, dim3(tpb), 0, st, R, ##__VA_ARGS__);            \

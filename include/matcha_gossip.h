@@ -148,7 +148,8 @@ size_t mx_topk_work_bytes(int64_t P);
 /* Top-k knobs: "sample_stride" = sample every S-th 1024-element chunk for the candidate floor
  * (0 = auto, about 2^18 sampled elements per row; 1 = exact full histogram, no sampling);
  * "compact_blocks" = persistent workgroups of the full pass, over all rows (default 1024);
- * "sample_pieces" = sampled 1024-element pieces per wave of the sampling pass (default 1). */
+ * "sample_pieces" = sampled 1024-element pieces per wave of the sampling pass (default 1);
+ * "cand_chunks" = candidate regions per wave of the candidate-histogram / mark passes (default 2). */
 int mx_topk_set(const char* key, int64_t value);
 int64_t mx_topk_get(const char* key);
 int mx_topk_abs_diff(const float* x, const float* x_hat, int64_t P, int64_t k, float* vals,
