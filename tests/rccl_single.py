@@ -1,0 +1,58 @@
+"""One rank, real RCCL (torchrun --nproc-per-node 1, backend nccl): the library's own RCCL
+communicator is created through RcclComm (unique id broadcast over torch.distributed), runs
+mx_allreduce_mean, an exchange round with nothing to move, and a full VirtualWorkerGroup /
+ChocoWorkerGroup round with the RCCL comm attached, then is destroyed.  This is the linkage check of
+the N > 1 transport (the library binds to the RCCL torch already loaded); cross-GPU traffic itself
+needs one GPU per rank."""
+import importlib
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+PKG = "270-matcha-a-matching-based-link-scheduling-strategy-to-speed-up-distributed-optimization_amd"
+
+
+def main():
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    pkg = importlib.import_module(PKG)
+    import oracle as O
+    comm = pkg.engine.RcclComm()
+    out = {"rank": comm.rank, "nranks": comm.nranks}
+    # all-reduce mean over one rank: sum / 1 leaves every value as it was
+    x = torch.from_numpy(O.synth(5, 1_000_003)).cuda()
+    y = x.clone()
+    pkg._lib.check(pkg.lib.mx_allreduce_mean(comm.handle, y.data_ptr(), y.numel(), 1, pkg._lib.stream_ptr()))
+    torch.cuda.synchronize()
+    out["allreduce_identity"] = bool(torch.equal(x, y))
+    # gossip rounds with the RCCL communicator attached (one rank: no cross-GPU edge, so the
+    # exchange posts nothing) -- bit-exact vs the oracle
+    n, P = 8, 50_001
+    np.random.seed(1234)
+    GP = pkg.MatchaProcessor(pkg.select_graph(0), 0.5, 0, n, 6, True)
+    grp = pkg.VirtualWorkerGroup(GP, numel=P, rank=0, nranks=1, comm=comm)
+    X = np.stack([O.synth(1234 + i, P) for i in range(n)])
+    grp.rows.copy_(torch.from_numpy(X))
+    partner = np.asarray(GP.neighbors_info, np.int32)
+    for it in range(6):
+        nrem = grp.engine.exchange(it, grp._row_ptrs, None, grp.ld * 4, P * 4)
+        assert nrem == 0
+        grp.step(it)
+        X = O.decen_round(X, partner, np.asarray(GP.active_flags[it], np.uint8), GP.neighbor_weight)
+    torch.cuda.synchronize()
+    out["decen_bit_exact"] = bool(np.array_equal(grp.rows.cpu().numpy().view(np.uint32), X.view(np.uint32)))
+    comm.close()
+    dist.destroy_process_group()
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -63,3 +63,13 @@ def test_dropin_communicators_one_process_per_worker():
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     res = json.loads(line)
     assert res["world"] == 8 and all(v for k, v in res.items() if k != "world"), res
+
+
+def test_rccl_single_rank_linkage():
+    """The library's own RCCL communicator (unique id over torch.distributed, ncclCommInitRank,
+    all-reduce mean, an exchange round with nothing to move, destroy) under torchrun with the nccl
+    backend -- the N > 1 transport's linkage against the RCCL torch loaded."""
+    r = _torchrun(1, [os.path.join(HERE, "rccl_single.py")], timeout=150)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out == {"rank": 0, "nranks": 1, "allreduce_identity": True, "decen_bit_exact": True}, out
