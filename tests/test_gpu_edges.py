@@ -1,0 +1,74 @@
+"""GPU edge shapes: rows far shorter than a tile (1 .. 4097 params; every sub-tile split), top-k
+at k = 1 (the reference's torch.max path, compressors.py:12-14) and k = P, and Choco rounds on
+tiny rows -- bit-exact vs the oracle."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import Topo
+
+pytestmark = pytest.mark.gpu
+
+SIZES = [1, 2, 3, 4, 5, 63, 64, 65, 255, 256, 257, 1023, 1025, 4097]
+
+
+@pytest.mark.parametrize("split", [0, 4])
+@pytest.mark.parametrize("gid", [0, 2])
+def test_mix_tiny_rows(pkg, O, gid, split):
+    saved = pkg.engine.mix_tuning()
+    pkg.engine.set_mix_tuning(split=split)
+    try:
+        n = pkg.GRAPH_SIZES[gid]
+        gp = pkg.GraphProcessor(pkg.select_graph(gid), 1.0, 0, n, 4, True)
+        M = len(gp.neighbors_info)
+        rng = np.random.RandomState(gid + 7)
+        flags = (rng.uniform(size=(3, M)) < 0.6).astype(np.uint8)
+        flags[0] = 1
+        topo = Topo(gp.neighbors_info, 0.19, flags)
+        for P in SIZES:
+            grp = pkg.VirtualWorkerGroup(topo, numel=P)
+            X = np.stack([O.synth(P * 31 + i, P) for i in range(n)])
+            grp.rows.copy_(torch.from_numpy(X))
+            for f in flags:
+                grp.communicate()
+                X = O.decen_round(X, topo.neighbors_info, f, 0.19)
+            got = grp.rows.cpu().numpy()
+            assert np.array_equal(got.view(np.uint32), X.view(np.uint32)), f"P={P}"
+    finally:
+        pkg.engine.set_mix_tuning(**saved)
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 7, 100, 4096, 4097])
+@pytest.mark.parametrize("ratio", [0.0, 0.5, 0.999999])
+def test_topk_extreme_k(pkg, O, P, ratio):
+    x = O.synth(P + 11, P)
+    k = O.topk_k(P, ratio)
+    assert 1 <= k <= P
+    ov, oi = O.topk_abs(x, k)
+    v, i = pkg.get_top_k(torch.from_numpy(x).cuda(), ratio)
+    assert i.numel() == k
+    assert np.array_equal(i.cpu().numpy(), oi)
+    assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32))
+
+
+@pytest.mark.parametrize("P", [1, 5, 257, 4099])
+@pytest.mark.parametrize("ratio", [0.0, 0.5, 0.99])
+def test_choco_tiny_rows(pkg, O, P, ratio):
+    n = 8
+    gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, n, 4, True)
+    flags = np.array([[1, 1, 1, 1, 1], [1, 0, 1, 0, 1], [0, 1, 1, 1, 0]], np.uint8)
+    topo = Topo(gp.neighbors_info, 2 / 7, flags)
+    grp = pkg.ChocoWorkerGroup(topo, numel=P, ratio=ratio, consensus_lr=0.2)
+    X = np.stack([O.synth(70 + i, P) for i in range(n)])
+    XH, S = np.zeros_like(X), np.zeros_like(X)
+    grp.rows.copy_(torch.from_numpy(X))
+    k = O.topk_k(P, ratio)
+    for t, f in enumerate(flags):
+        if t:
+            D = np.stack([np.float32(0.05) * O.synth(600 + 13 * t + i, P) for i in range(n)])
+            X += D
+            grp.rows.add_(torch.from_numpy(D).cuda())
+        grp.communicate()
+        O.choco_round(X, XH, S, topo.neighbors_info, f, 2 / 7, k, 0.2)
+        got = grp.rows.cpu().numpy()
+        assert np.array_equal(got.view(np.uint32), X.view(np.uint32)), f"round {t}"
