@@ -245,12 +245,15 @@ class GossipEngine:
         return nrem.value
 
     def mix(self, it, layout, stream=None):
+        it = int(it)
+        if not 0 <= it < self.T:                 # the kernel indexes the plan table by `it`
+            raise IndexError(f"iteration {it} outside the schedule's {self.T} rows")
         if layout.tune_gen != _TUNE_GEN[0]:
             if layout.tile != lib.mx_mix_tile(layout.n_slots):
                 raise MXError("layout built for another mixing tile size (the unroll knob changed it)")
             layout.tune_gen = _TUNE_GEN[0]
         # one ctypes call per round with pre-resolved pointers (small rows are launch-bound)
-        rc = lib.mx_gossip_mix(*layout._args, self._plan_ptr, int(it), self.n_local, self.M, self.alpha32,
+        rc = lib.mx_gossip_mix(*layout._args, self._plan_ptr, it, self.n_local, self.M, self.alpha32,
                                stream_ptr(stream))
         if rc:
             check(rc, "mx_gossip_mix")

@@ -72,3 +72,17 @@ def test_choco_tiny_rows(pkg, O, P, ratio):
         O.choco_round(X, XH, S, topo.neighbors_info, f, 2 / 7, k, 0.2)
         got = grp.rows.cpu().numpy()
         assert np.array_equal(got.view(np.uint32), X.view(np.uint32)), f"round {t}"
+
+
+def test_iteration_outside_schedule_raises(pkg):
+    """The kernels index the plan table by iteration: the host refuses one outside the schedule
+    instead of launching a read past the table."""
+    gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, 8, 4, True)
+    topo = Topo(gp.neighbors_info, 0.2, np.ones((3, 5), np.uint8))
+    grp = pkg.VirtualWorkerGroup(topo, numel=1000)
+    for bad in (3, 4, -1):
+        with pytest.raises(IndexError):
+            grp.engine.mix(bad, grp.layout)
+    ch = pkg.ChocoWorkerGroup(topo, numel=1000, ratio=0.9, consensus_lr=0.1)
+    with pytest.raises(IndexError):
+        ch.average(3)
