@@ -100,6 +100,55 @@ def max_over_ranks(x, world, dev):
     return float(t.item())
 
 
+def exchange_only(group, first, K, world, dev):
+    """N > 1 diagnostic: the RCCL exchange of K rounds alone (no mixing; rows do not change),
+    max over ranks of the back-to-back wall time per round."""
+    import torch.distributed as dist
+    eng = group.engine
+    slab = group.slab.data_ptr() if group.slab is not None else None
+    torch.cuda.synchronize()
+    dist.barrier()
+    t = time.perf_counter()
+    for j in range(K):
+        eng.exchange(first + j, group._row_ptrs, slab, group.ld * 4, group.numel * 4)
+    torch.cuda.synchronize()
+    dist.barrier()
+    return max_over_ranks((time.perf_counter() - t) / K, world, dev)
+
+
+def p2p_probe(rank, world, nbytes, dev, reps=5):
+    """N > 1: one xGMI link through RCCL (torch.distributed send/recv on the nccl group), ranks 0
+    and 1 only: unidirectional 0 -> 1 and bidirectional 0 <-> 1, seconds per transfer (max over
+    the two ranks)."""
+    import torch.distributed as dist
+    buf = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+    rbuf = torch.empty_like(buf)
+    res = {}
+    for mode in ("uni", "bi"):
+        for rep in range(reps + 1):                 # first transfer: connection setup, untimed
+            torch.cuda.synchronize()
+            dist.barrier()
+            t = time.perf_counter()
+            if rank in (0, 1):
+                peer = 1 - rank
+                ops = []
+                if mode == "bi" or rank == 0:
+                    ops.append(dist.P2POp(dist.isend, buf, peer))
+                if mode == "bi" or rank == 1:
+                    ops.append(dist.P2POp(dist.irecv, rbuf, peer))
+                for w in dist.batch_isend_irecv(ops):
+                    w.wait()
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t
+            if rep == 1:
+                res[mode] = []
+            if rep >= 1:
+                res[mode].append(el if rank in (0, 1) else 0.0)
+        res[mode] = max_over_ranks(float(np.median(res[mode])), world, dev)
+    del buf, rbuf
+    return res
+
+
 def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99, gamma=0.1, placement=None):
     """Secondary figure: ChocoSGD rounds (BASELINE config: VGG-16 size, top-1 %, graph 0, every
     matching active) on the same GPUs -- top-k compress + [N > 1] message exchange + fused apply."""
@@ -287,6 +336,10 @@ def main():
             pair[key] = pair.get(key, 0) + v
         pair_bytes.append(max(pair.values()) if pair else 0)
     avg_ms = float(step_ms.mean())
+    exch_s = probe = None
+    if world > 1:             # (with --transport gloo: the same code over host staging, tests only)
+        exch_s = exchange_only(group, W + K, K, world, dev)
+        probe = p2p_probe(rank, world, P * 4, dev)
     mix_avg_ms = float(mix_ms.mean())
     mix_bytes = float(np.mean(hbm_bytes))
     achieved = mix_bytes / (mix_avg_ms * 1e-3)
@@ -339,6 +392,15 @@ def main():
                            "aggregate_bytes_per_round": float(np.mean(total_bytes)),
                            "aggregate_achieved": float(np.mean(total_bytes)) / round_s / 1e9,
                            "round_ms": 1e3 * round_s, "round_ms_events_rank0": avg_ms,
+                           "exchange_only_ms": 1e3 * exch_s if exch_s else None,
+                           "exchange_only_busiest_link_GBps": lb / exch_s / 1e9 if exch_s else None,
+                           "exchange_only_busiest_pair_both_directions_GBps": pb / exch_s / 1e9 if exch_s else None,
+                           "p2p_probe": ({"bytes": P * 4, "uni_ms": 1e3 * probe["uni"],
+                                          "uni_GBps": P * 4 / probe["uni"] / 1e9, "bi_ms": 1e3 * probe["bi"],
+                                          "bi_GBps_both_directions": 2 * P * 4 / probe["bi"] / 1e9,
+                                          "how": "torch.distributed batch_isend_irecv (RCCL), ranks 0 and 1, "
+                                                 "median of 5 after one untimed transfer"}
+                                         if probe else None),
                            "note": "busiest GPU pair: bytes that cross it per round (one direction, and "
                                    "both directions summed) / whole-job round time (exchange + mix), "
                                    "against the 153 GB/s per-link figure of SURVEY.md §8d"}

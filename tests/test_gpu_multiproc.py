@@ -51,6 +51,7 @@ def test_bench_multiprocess_path():
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     out = json.loads(line)
     assert out["n_gpus"] == 2 and out["value"] > 0 and out["xgmi"]["max_link_bytes_per_round"] > 0
+    assert out["xgmi"]["exchange_only_ms"] > 0 and out["xgmi"]["p2p_probe"]["uni_GBps"] > 0
     assert out["choco"]["rounds_per_s"] > 0 and out["cpu_baseline"] is None
 
 
