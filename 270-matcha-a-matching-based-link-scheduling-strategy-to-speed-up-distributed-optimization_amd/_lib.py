@@ -42,6 +42,7 @@ SIGNATURES = {
     "mx_rccl_init": (c_int, [c_p, c_int, c_int, c_p]),
     "mx_rccl_destroy": (c_int, [c_p]),
     "mx_exchange_plan": (c_int, [c_p, c_int, c_p, c_int, c_p, c_int, c_int, c_int, c_p, c_int, c_p]),
+    "mx_exchange_post": (c_int, [c_p, c_p, c_int, c_p, c_int, c_p, c_i64, c_i64, c_p]),
     "mx_exchange_round": (c_int, [c_p, c_p, c_int, c_p, c_int, c_p, c_int, c_int, c_int, c_p, c_p, c_i64,
                                   c_i64, c_p, c_p]),
     "mx_allreduce_mean": (c_int, [c_p, c_p, c_i64, c_int, c_p]),

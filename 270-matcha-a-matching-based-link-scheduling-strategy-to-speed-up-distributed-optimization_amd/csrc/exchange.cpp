@@ -103,32 +103,27 @@ extern "C" int mx_exchange_plan(const uint8_t* flags_row, int M, const int32_t* 
     return MX_OK;
 }
 
-extern "C" int mx_exchange_round(void* comm_v, const uint8_t* flags_row, int M,
-                                 const int32_t* partner, int n_global, const int32_t* owner,
-                                 int my_rank, int row_base, int n_local, void* const* rows,
-                                 void* slab, int64_t slab_ld_bytes, int64_t row_bytes,
-                                 int* n_remote_out, void* stream) {
-    MX_CHECK(comm_v && rows, "mx_exchange_round: null pointer");
-    MX_CHECK(row_bytes > 0 && row_bytes % 4 == 0, "mx_exchange_round: row_bytes %lld", (long long)row_bytes);
-    int nops = 0;
-    int rc = mx_exchange_plan(flags_row, M, partner, n_global, owner, my_rank, row_base, n_local,
-                              nullptr, 0, &nops);
-    if (rc != MX_OK) return rc;
-    std::vector<int32_t> ops(4 * (size_t)(nops > 0 ? nops : 1));
-    rc = mx_exchange_plan(flags_row, M, partner, n_global, owner, my_rank, row_base, n_local,
-                          ops.data(), nops, &nops);
-    if (rc != MX_OK) return rc;
-    int remote = 0;
-    for (int i = 0; i < nops; ++i) remote += ops[4 * i] == 1;
-    if (n_remote_out) *n_remote_out = remote;
-    if (nops == 0) return MX_OK;
-    MX_CHECK(remote == 0 || slab, "mx_exchange_round: receive slab required");
+extern "C" int mx_exchange_post(void* comm_v, const int32_t* ops, int n_ops, void* const* rows, int n_rows,
+                                void* slab, int64_t slab_ld_bytes, int64_t row_bytes, void* stream) {
+    MX_CHECK(comm_v && (ops || n_ops == 0) && n_ops >= 0, "mx_exchange_post: bad arguments");
+    MX_CHECK(row_bytes > 0 && row_bytes % 4 == 0, "mx_exchange_post: row_bytes %lld", (long long)row_bytes);
+    if (n_ops == 0) return MX_OK;
+    for (int i = 0; i < n_ops; ++i) {                     // validate everything before posting
+        const int32_t* o = ops + 4 * i;
+        MX_CHECK(o[0] == 0 || o[0] == 1, "mx_exchange_post: op %d kind %d", i, o[0]);
+        MX_CHECK(o[1] >= 0, "mx_exchange_post: op %d peer %d", i, o[1]);
+        if (o[0] == 0)
+            MX_CHECK(rows && o[2] >= 0 && o[2] < n_rows && rows[o[2]], "mx_exchange_post: op %d row %d of %d", i,
+                     o[2], n_rows);
+        else
+            MX_CHECK(slab && o[2] >= 0 && slab_ld_bytes >= row_bytes, "mx_exchange_post: op %d slab slot %d", i, o[2]);
+    }
     ncclComm_t comm = reinterpret_cast<ncclComm_t>(comm_v);
     hipStream_t st = mx::as_stream(stream);
     const size_t count = (size_t)(row_bytes / 4);
     MX_NCCL(ncclGroupStart());
-    for (int i = 0; i < nops; ++i) {
-        const int32_t* o = &ops[4 * i];
+    for (int i = 0; i < n_ops; ++i) {
+        const int32_t* o = ops + 4 * i;
         ncclResult_t r;
         if (o[0] == 0) {
             r = ncclSend(rows[o[2]], count, ncclFloat32, o[1], comm, st);
@@ -144,6 +139,26 @@ extern "C" int mx_exchange_round(void* comm_v, const uint8_t* flags_row, int M,
     }
     MX_NCCL(ncclGroupEnd());
     return MX_OK;
+}
+
+extern "C" int mx_exchange_round(void* comm_v, const uint8_t* flags_row, int M,
+                                 const int32_t* partner, int n_global, const int32_t* owner,
+                                 int my_rank, int row_base, int n_local, void* const* rows,
+                                 void* slab, int64_t slab_ld_bytes, int64_t row_bytes,
+                                 int* n_remote_out, void* stream) {
+    MX_CHECK(comm_v && rows, "mx_exchange_round: null pointer");
+    int nops = 0;
+    int rc = mx_exchange_plan(flags_row, M, partner, n_global, owner, my_rank, row_base, n_local,
+                              nullptr, 0, &nops);
+    if (rc != MX_OK) return rc;
+    std::vector<int32_t> ops(4 * (size_t)(nops > 0 ? nops : 1));
+    rc = mx_exchange_plan(flags_row, M, partner, n_global, owner, my_rank, row_base, n_local,
+                          ops.data(), nops, &nops);
+    if (rc != MX_OK) return rc;
+    int remote = 0;
+    for (int i = 0; i < nops; ++i) remote += ops[4 * i] == 1;
+    if (n_remote_out) *n_remote_out = remote;
+    return mx_exchange_post(comm_v, ops.data(), nops, rows, n_local, slab, slab_ld_bytes, row_bytes, stream);
 }
 
 namespace {

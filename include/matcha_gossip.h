@@ -206,6 +206,12 @@ int mx_rccl_destroy(void* comm);
 int mx_exchange_plan(const uint8_t* flags_row, int M, const int32_t* partner, int n_global,
                      const int32_t* owner, int my_rank, int row_base, int n_local, int32_t* ops,
                      int cap, int* n_ops);
+/* Posts an explicit operation list (mx_exchange_plan's layout) inside one ncclGroupStart/End:
+ * kind 0 = ncclSend of rows[op[2]] to op[1], kind 1 = ncclRecv from op[1] into slab slot op[2];
+ * row_bytes per operation.  Sends to / receives from one peer pair up in list order.  Every op is
+ * validated before anything is posted.  mx_exchange_round = mx_exchange_plan + this. */
+int mx_exchange_post(void* comm, const int32_t* ops, int n_ops, void* const* rows, int n_rows, void* slab,
+                     int64_t slab_ld_bytes, int64_t row_bytes, void* stream);
 int mx_exchange_round(void* comm, const uint8_t* flags_row, int M, const int32_t* partner,
                       int n_global, const int32_t* owner, int my_rank, int row_base, int n_local,
                       void* const* rows, void* slab, int64_t slab_ld_bytes, int64_t row_bytes,

@@ -49,6 +49,28 @@ def main():
         X = O.decen_round(X, partner, np.asarray(GP.active_flags[it], np.uint8), GP.neighbor_weight)
     torch.cuda.synchronize()
     out["decen_bit_exact"] = bool(np.array_equal(grp.rows.cpu().numpy().view(np.uint32), X.view(np.uint32)))
+    # real ncclSend / ncclRecv through mx_exchange_post: a one-rank communicator sends to itself
+    # (sends and receives to one peer pair up in posting order), so slab slot 2 gets row 0, slot 0
+    # gets row 2 and slot 1 row 1 -- the slab addressing, counts and grouping of the N > 1 path
+    import ctypes
+    P2 = 300_007
+    rows = torch.from_numpy(np.stack([O.synth(900 + i, P2) for i in range(3)])).cuda()
+    ld = P2 + 57
+    slab = torch.full((3, ld), -7.0, device="cuda")
+    ops = np.array([[0, 0, 0, 0], [1, 0, 2, 0], [0, 0, 2, 2], [1, 0, 0, 2], [0, 0, 1, 1], [1, 0, 1, 1]],
+                   np.int32)
+    ptrs = (ctypes.c_void_p * 3)(*[rows[i].data_ptr() for i in range(3)])
+    pkg._lib.check(pkg.lib.mx_exchange_post(comm.handle, ops.ctypes.data, len(ops), ptrs, 3, slab.data_ptr(),
+                                            ld * 4, P2 * 4, pkg._lib.stream_ptr()))
+    torch.cuda.synchronize()
+    out["post_self_exchange"] = bool(torch.equal(slab[2, :P2], rows[0]) and torch.equal(slab[0, :P2], rows[2])
+                                     and torch.equal(slab[1, :P2], rows[1])
+                                     and bool((slab[:, P2:] == -7.0).all()))
+    bad = ops.copy()
+    bad[0, 2] = 5                                    # row index out of range: refused before posting
+    rc = pkg.lib.mx_exchange_post(comm.handle, bad.ctypes.data, len(bad), ptrs, 3, slab.data_ptr(), ld * 4,
+                                  P2 * 4, pkg._lib.stream_ptr())
+    out["post_validates"] = rc != 0
     comm.close()
     dist.destroy_process_group()
     print(json.dumps(out), flush=True)

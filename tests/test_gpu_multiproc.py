@@ -73,4 +73,5 @@ def test_rccl_single_rank_linkage():
     r = _torchrun(1, [os.path.join(HERE, "rccl_single.py")], timeout=150)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
-    assert out == {"rank": 0, "nranks": 1, "allreduce_identity": True, "decen_bit_exact": True}, out
+    assert out == {"rank": 0, "nranks": 1, "allreduce_identity": True, "decen_bit_exact": True,
+                   "post_self_exchange": True, "post_validates": True}, out
