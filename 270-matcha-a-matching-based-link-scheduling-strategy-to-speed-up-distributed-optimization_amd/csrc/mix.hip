@@ -74,9 +74,18 @@ struct PlanLds {
     int32_t w[mx::kPlanHeader + 2 * NS + NS * kMaxM];
 };
 
+// The round to mix: `iter`, or with iter_dev (graph-replayable launches) the device counter
+// *iter_dev, `iter` then being the schedule length; outside [0, length) the launch is a no-op.
+__device__ __forceinline__ int64_t round_of(int64_t iter, const int64_t* iter_dev) {
+    if (!iter_dev) return iter;
+    const int64_t v = *iter_dev;
+    return (v >= 0 && v < iter) ? v : -1;
+}
+
 template <int NS>
 __device__ __forceinline__ uint64_t load_plan(PlanLds<NS>& sp, const int32_t* plan, int64_t iter,
                                               int n_local, int M) {
+    if (iter < 0) return 0;                      // block-uniform: no barrier is skipped unevenly
     const int64_t W = mx::plan_words(n_local, M);
     const int32_t* rec = plan + iter * W;
     for (int i = threadIdx.x; i < W; i += kTPB) sp.w[i] = rec[i];
@@ -175,13 +184,13 @@ __global__ __launch_bounds__(kTPB) void mix_kernel(float* const* __restrict__ se
                                                    const int64_t* __restrict__ tile_off,
                                                    const uint8_t* __restrict__ seg_vec, int nseg,
                                                    int64_t total_tiles, int n_slots,
-                                                   const int32_t* __restrict__ plan, int64_t iter,
+                                                   const int32_t* __restrict__ plan, int64_t iter, const int64_t* __restrict__ iter_dev,
                                                    int n_local, int M, float alpha, int chunked) {
     using F = typename VT<VEC>::type;
     __shared__ F lds[NS][U][kTPB];
     __shared__ PlanLds<NS> sp;
     const int tid = threadIdx.x;
-    const uint64_t need = load_plan<NS>(sp, plan, iter, n_local, M);
+    const uint64_t need = load_plan<NS>(sp, plan, round_of(iter, iter_dev), n_local, M);
     if (need == 0) return;                    // all flags zero: the reference does no I/O
     const int32_t* deg = sp.w + mx::kPlanHeader;
     const float* sw = reinterpret_cast<const float*>(deg + n_local);
@@ -314,11 +323,11 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_reg(float* const* __restrict_
                                                        const int64_t* __restrict__ tile_off,
                                                        const uint8_t* __restrict__ seg_vec, int nseg,
                                                        int64_t total_tiles, int n_slots,
-                                                       const int32_t* __restrict__ plan, int64_t iter,
+                                                       const int32_t* __restrict__ plan, int64_t iter, const int64_t* __restrict__ iter_dev,
                                                        int n_local, int M, float alpha, int chunked) {
     using F = typename VT<4>::type;
     __shared__ PlanLds<NS> sp;
-    const uint64_t need = load_plan<NS>(sp, plan, iter, n_local, M);
+    const uint64_t need = load_plan<NS>(sp, plan, round_of(iter, iter_dev), n_local, M);
     if (need == 0) return;
     const int32_t* deg = sp.w + mx::kPlanHeader;
     const float* sw = reinterpret_cast<const float*>(deg + n_local);
@@ -422,7 +431,7 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict
                                                         const int64_t* __restrict__ tile_off,
                                                         const uint8_t* __restrict__ seg_vec, int nseg,
                                                         int64_t total_tiles, int n_slots,
-                                                        const int32_t* __restrict__ plan, int64_t iter,
+                                                        const int32_t* __restrict__ plan, int64_t iter, const int64_t* __restrict__ iter_dev,
                                                         int n_local, int M, float alpha) {
     using F = typename VT<4>::type;
     constexpr int C4 = TW / 4;            // float4 per slot per tile
@@ -433,7 +442,7 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict
     __shared__ F lds[NS * C4];
     __shared__ PlanLds<NS> sp;
     __shared__ int32_t wl[4][NI / 4];
-    const uint64_t need = load_plan<NS>(sp, plan, iter, n_local, M);
+    const uint64_t need = load_plan<NS>(sp, plan, round_of(iter, iter_dev), n_local, M);
     if (need == 0) return;
     const int32_t* deg = sp.w + mx::kPlanHeader;
     const float* sw = reinterpret_cast<const float*>(deg + n_local);
@@ -650,34 +659,34 @@ int row_split(int ns, int64_t total_tiles) {
 
 template <int VEC, int NS, int U, bool NT, bool PF>
 int launch(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_off,
-           const uint8_t* seg_vec, int nseg, int n_slots, const int32_t* plan, int64_t iter,
+           const uint8_t* seg_vec, int nseg, int n_slots, const int32_t* plan, int64_t iter, const int64_t* iter_dev,
            int n_local, int M, float alpha, int64_t total_tiles, hipStream_t st) {
     const int mode = ((nseg == 1 && g_tune.chunked) ? 1 : 0) | (NS >= g_tune.readlane_min ? 2 : 0);
     hipLaunchKernelGGL((mix_kernel<VEC, NS, U, NT, PF>), dim3((unsigned)grid_for(total_tiles)), dim3(kTPB),
                        0, st, seg_ptrs, seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan,
-                       iter, n_local, M, alpha, mode);
+                       iter, iter_dev, n_local, M, alpha, mode);
     MX_LAUNCH_CHECK();
     return MX_OK;
 }
 
 template <int NS, int TW, bool NT, int SPLIT = 1>
 int launch_rows(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_off,
-                const uint8_t* seg_vec, int nseg, int n_slots, const int32_t* plan, int64_t iter,
+                const uint8_t* seg_vec, int nseg, int n_slots, const int32_t* plan, int64_t iter, const int64_t* iter_dev,
                 int n_local, int M, float alpha, int64_t total_tiles, hipStream_t st) {
     hipLaunchKernelGGL((mix_kernel_rows<NS, TW, NT, SPLIT>), dim3((unsigned)grid_for(total_tiles * SPLIT)), dim3(kTPB),
                        0, st, seg_ptrs, seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan,
-                       iter, n_local, M, alpha);
+                       iter, iter_dev, n_local, M, alpha);
     MX_LAUNCH_CHECK();
     return MX_OK;
 }
 
 template <int NS, int U, bool NT, bool PF>
 int launch_reg(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_off,
-               const uint8_t* seg_vec, int nseg, int n_slots, const int32_t* plan, int64_t iter,
+               const uint8_t* seg_vec, int nseg, int n_slots, const int32_t* plan, int64_t iter, const int64_t* iter_dev,
                int n_local, int M, float alpha, int64_t total_tiles, hipStream_t st) {
     hipLaunchKernelGGL((mix_kernel_reg<NS, U, NT, PF>), dim3((unsigned)grid_for(total_tiles)), dim3(kTPB),
                        0, st, seg_ptrs, seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan,
-                       iter, n_local, M, alpha, (nseg == 1 && g_tune.chunked) ? 1 : 0);
+                       iter, iter_dev, n_local, M, alpha, (nseg == 1 && g_tune.chunked) ? 1 : 0);
     MX_LAUNCH_CHECK();
     return MX_OK;
 }
@@ -765,10 +774,47 @@ extern "C" int mx_mix_layout(const int64_t* seg_len_host, int nseg, int n_slots,
     return MX_OK;
 }
 
+namespace {
+int gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev, const int64_t* tile_off_dev,
+               const uint8_t* seg_vec_dev, int nseg, int64_t total_tiles, int n_slots, const int32_t* plan_dev,
+               int64_t iter, const int64_t* iter_dev, int n_local, int M, float alpha, void* stream);
+}
+
 extern "C" int mx_gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev,
                              const int64_t* tile_off_dev, const uint8_t* seg_vec_dev, int nseg,
                              int64_t total_tiles, int n_slots, const int32_t* plan_dev,
                              int64_t iter, int n_local, int M, float alpha, void* stream) {
+    return gossip_mix(seg_ptrs_dev, seg_len_dev, tile_off_dev, seg_vec_dev, nseg, total_tiles, n_slots, plan_dev,
+                      iter, nullptr, n_local, M, alpha, stream);
+}
+
+extern "C" int mx_gossip_mix_at(float* const* seg_ptrs_dev, const int64_t* seg_len_dev,
+                                const int64_t* tile_off_dev, const uint8_t* seg_vec_dev, int nseg,
+                                int64_t total_tiles, int n_slots, const int32_t* plan_dev,
+                                const int64_t* iter_dev, int64_t n_iters, int n_local, int M, float alpha,
+                                void* stream) {
+    MX_CHECK(iter_dev, "mx_gossip_mix_at: null iteration counter");
+    return gossip_mix(seg_ptrs_dev, seg_len_dev, tile_off_dev, seg_vec_dev, nseg, total_tiles, n_slots, plan_dev,
+                      n_iters, iter_dev, n_local, M, alpha, stream);
+}
+
+namespace {
+__global__ void advance_kernel(int64_t* it, int64_t by) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) it[0] += by;
+}
+}  // namespace
+
+extern "C" int mx_iter_advance(int64_t* iter_dev, int64_t by, void* stream) {
+    MX_CHECK(iter_dev, "mx_iter_advance: null counter");
+    hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(64), 0, mx::as_stream(stream), iter_dev, by);
+    MX_LAUNCH_CHECK();
+    return MX_OK;
+}
+
+namespace {
+int gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev, const int64_t* tile_off_dev,
+               const uint8_t* seg_vec_dev, int nseg, int64_t total_tiles, int n_slots, const int32_t* plan_dev,
+               int64_t iter, const int64_t* iter_dev, int n_local, int M, float alpha, void* stream) {
     MX_CHECK(seg_ptrs_dev && seg_len_dev && tile_off_dev && seg_vec_dev && plan_dev,
              "mx_gossip_mix: null pointer");
     MX_CHECK(nseg >= 1 && n_local >= 1 && n_slots >= n_local, "mx_gossip_mix: nseg=%d n_local=%d n_slots=%d",
@@ -781,7 +827,7 @@ extern "C" int mx_gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_
     if (total_tiles <= 0) return MX_OK;
     const int key = (g_tune.nontemporal ? 1 : 0) | (g_tune.prefetch ? 2 : 0);
 #define MX_ARGS seg_ptrs_dev, seg_len_dev, tile_off_dev, seg_vec_dev, nseg, n_slots, plan_dev, iter, \
-                n_local, M, alpha, total_tiles, st
+                iter_dev, n_local, M, alpha, total_tiles, st
 #define MX_DISPATCH(V, N, U)                                                  \
     switch (key) {                                                            \
         case 0: return launch<V, N, U, false, false>(MX_ARGS);                \
@@ -828,3 +874,4 @@ extern "C" int mx_gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_
 #undef MX_DISPATCH_REG
 #undef MX_ARGS
 }
+}  // namespace

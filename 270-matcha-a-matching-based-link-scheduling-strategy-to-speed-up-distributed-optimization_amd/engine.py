@@ -259,6 +259,23 @@ class GossipEngine:
             check(rc, "mx_gossip_mix")
 
 
+    def mix_at(self, iter_dev, layout, stream=None):
+        """Graph-replayable round: the kernel reads the iteration from the int64 device tensor
+        `iter_dev` when it runs (mx_gossip_mix_at) and the counter is advanced by one on the same
+        stream, so a captured launch pair serves every iteration (a counter past the schedule
+        makes the launch a no-op)."""
+        if layout.tune_gen != _TUNE_GEN[0]:
+            if layout.tile != lib.mx_mix_tile(layout.n_slots):
+                raise MXError("layout built for another mixing tile size (the unroll knob changed it)")
+            layout.tune_gen = _TUNE_GEN[0]
+        if iter_dev.dtype != torch.int64 or iter_dev.device.type != "cuda" or iter_dev.numel() != 1:
+            raise TypeError("iter_dev must be a one-element int64 CUDA tensor")
+        s = stream_ptr(stream)
+        check(lib.mx_gossip_mix_at(*layout._args, self._plan_ptr, iter_dev.data_ptr(), self.T, self.n_local,
+                                   self.M, self.alpha32, s), "mx_gossip_mix_at")
+        check(lib.mx_iter_advance(iter_dev.data_ptr(), 1, s), "mx_iter_advance")
+
+
 def _params(model):
     return [p for p in model.parameters()]
 
@@ -293,6 +310,7 @@ class VirtualWorkerGroup:
                                    owner=owner_table(n, nranks))
         self.topology = topology
         self.iter = 0
+        self.iter_dev = torch.zeros(1, dtype=torch.int64, device="cuda")   # device_round's counter
         if models is not None:
             if len(models) != self.n_local:
                 raise ValueError(f"{len(models)} models for {self.n_local} local workers")
@@ -385,6 +403,18 @@ class VirtualWorkerGroup:
             mixed[b] = torch.cuda.Event()
             mixed[b].record(cur)
         return True
+
+    def device_round(self, stream=None):
+        """Enqueue the round at the device-side counter `self.iter_dev` and advance it (no host
+        work depends on the round, so the pair can be captured once in a HIP graph --
+        torch.cuda.graph -- and replayed every iteration).  One GPU only: a cross-GPU exchange's
+        operation list depends on the round's flags on the host.  Set the counter with
+        `self.iter_dev.fill_(it)`; `self.iter` (the host counter of communicate()) is not touched."""
+        if self.engine.comm is not None:
+            raise MXError("device_round: graph-replayable rounds need all partners on this GPU (nranks = 1)")
+        if self.chunked:
+            raise MXError("device_round: not with chunk_cols")
+        self.engine.mix_at(self.iter_dev, self.layout, stream)
 
     def state_dict(self):
         """Checkpoint: the workers' rows and the iteration counter (resume on the same schedule)."""

@@ -183,7 +183,13 @@ class VirtualTrainer:
     element-wise op sequence of torch.optim.SGD) runs once over the stacked views -- a training
     step for all workers is a handful of batched launches plus the gossip kernel."""
 
-    def __init__(self, args, model_fn, n_batches, device="cuda", batched=False):
+    def __init__(self, args, model_fn, n_batches, device="cuda", batched=False, graph=False):
+        """graph=True (with batched=True, decentralized gossip, one GPU): once the learning rate
+        is constant within an epoch, the whole training iteration -- vmap'd forward / backward,
+        SGD update and the gossip round at a device-side iteration counter (device_round) -- is
+        captured once per learning rate in a HIP graph and replayed, so an iteration costs one
+        graph launch plus the batch copies instead of dozens of host launches.  Results are
+        identical to batched=True (same kernels, same order)."""
         self.args = args
         size = args.size
         np.random.seed(args.randomSeed)                          # train_mpi.py:62
@@ -209,6 +215,11 @@ class VirtualTrainer:
         self.recorders = [Recorder(args, r) for r in range(size)] if args.save else None
         self.epoch = 0
         self.batched = bool(batched)
+        self.graph = bool(graph)
+        if self.graph and (not self.batched or args.compress):
+            raise ValueError("graph mode needs batched=True and decentralized (non-Choco) gossip")
+        self._graphs = {}
+        self._dev_iter_synced = False
         if self.batched:
             self._setup_batched()
 
@@ -222,10 +233,12 @@ class VirtualTrainer:
         rows = self.group.rows
         n = rows.shape[0]
         self._stack = {}
+        self._stack_off = []
         off = 0
         for name, p in m0.named_parameters():          # the arena's adoption order
             k = p.numel()
             self._stack[name] = rows[:, off:off + k].view((n,) + tuple(p.shape))
+            self._stack_off.append(off)
             off += k
         self._mom = {}
 
@@ -240,8 +253,11 @@ class VirtualTrainer:
 
     def _batched_step(self, b, lr):
         """Every worker's forward / backward / SGD step for batch b; per-worker (loss, acc)."""
-        args = self.args
         X, Y = self._data_stacked[b]
+        return self._batched_update(X, Y, lr)
+
+    def _batched_update(self, X, Y, lr):
+        args = self.args
         grads, (loss, out) = self._grad_fn(self._stack, X, Y)
         wd, mom = 5e-4, args.momentum
         with torch.no_grad():
@@ -258,6 +274,56 @@ class VirtualTrainer:
             acc = (out.argmax(-1) == Y).float().mean(-1) * 100.0
         return loss.detach(), acc
 
+    # ------------------------------------------------------------------ HIP-graph iterations
+    def _lr_stable(self, epoch):
+        """update_learning_rate's value is constant within this epoch (no per-iteration warmup)"""
+        return not (self.args.warmup and epoch < 5 and self.args.lr > 0.1)
+
+    def _graph_for(self, lr):
+        """(graph, loss, acc) of one whole iteration at learning rate lr, captured on first use:
+        forward / backward / SGD on the static batch buffers, then the gossip round at the device
+        counter.  Capturing runs nothing."""
+        hit = self._graphs.get(lr)
+        if hit is not None:
+            return hit
+        if not hasattr(self, "_Xs"):
+            X0, Y0 = self._data_stacked[0]
+            self._Xs, self._Ys = X0.clone(), Y0.clone()      # valid labels: the warm-up runs on them
+            self._cap_stream = torch.cuda.Stream()
+        # warm the BLAS libraries for these GEMM shapes on the capture stream first (they set up
+        # handles / workspaces / heuristics lazily, which a capturing stream does not permit),
+        # on a scratch copy of the arena laid out like the live one: no worker state changes
+        cs = self._cap_stream
+        cs.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(cs):
+            scratch = self.group.arena.clone()
+            n = scratch.shape[0]
+            views = {name: scratch[:, off:off + v.shape[1:].numel()].view(v.shape)
+                     for (name, v), off in zip(self._stack.items(), self._stack_off)}
+            self._grad_fn(views, self._Xs, self._Ys)
+        torch.cuda.current_stream().wait_stream(cs)
+        torch.cuda.synchronize()
+        del scratch, views
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=cs):
+            loss, acc = self._batched_update(self._Xs, self._Ys, lr)
+            self.group.device_round()
+        self._graphs[lr] = (g, loss, acc)
+        return self._graphs[lr]
+
+    def _graph_iteration(self, b, lr):
+        """One training iteration + gossip round by graph replay; (loss, acc) device tensors."""
+        g, loss, acc = self._graph_for(lr)
+        X, Y = self._data_stacked[b]
+        self._Xs.copy_(X)
+        self._Ys.copy_(Y)
+        if not self._dev_iter_synced:
+            self.group.iter_dev.fill_(self.group.iter)
+            self._dev_iter_synced = True
+        g.replay()
+        self.group.iter += 1
+        return loss, acc
+
     def train_epoch(self, on_round=None):
         """One epoch of train_mpi.py:109-168 for every worker; returns per-worker stats."""
         args = self.args
@@ -270,7 +336,27 @@ class VirtualTrainer:
         tic = time.time()
         for m in self.models:
             m.train()
-        for b in range(self.n_batches):
+        use_graph = self.graph and self._lr_stable(epoch) and (self.args.momentum == 0 or self._mom)
+        if use_graph:
+            if on_round is not None:
+                raise ValueError("graph mode runs the step and the gossip round as one replay: no round hooks")
+            t0 = time.time()
+            stat = torch.empty((self.n_batches, 2, size), dtype=torch.float32, device="cuda")
+            for b in range(self.n_batches):
+                lr = update_learning_rate(self.optimizers[0], epoch, args, itr=b, itr_per_epoch=self.n_batches)
+                loss_b, acc_b = self._graph_iteration(b, lr)
+                stat[b, 0].copy_(loss_b)
+                stat[b, 1].copy_(acc_b)
+            st = stat.cpu().numpy()                            # one host sync per epoch
+            dt = (time.time() - t0) / size
+            bs = self._data_stacked[0][1].shape[1]
+            for b in range(self.n_batches):
+                for r in range(size):
+                    losses[r].update(float(st[b, 0, r]), bs)
+                    top1[r].update(float(st[b, 1, r]), bs)
+            for r in range(size):
+                comp[r] += dt                                  # gossip included (one replay per iteration)
+        for b in range(0 if not use_graph else self.n_batches, self.n_batches):
             if self.batched:
                 t0 = time.time()
                 lr = update_learning_rate(self.optimizers[0], epoch, args, itr=b, itr_per_epoch=self.n_batches)
@@ -299,6 +385,7 @@ class VirtualTrainer:
             if on_round is not None:
                 on_round("before", self)
             comm_time += self.communicate()                  # train_mpi.py:142, all workers at once
+            self._dev_iter_synced = False
             if on_round is not None:
                 on_round("after", self)
         record_time = time.time() - tic

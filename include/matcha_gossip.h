@@ -120,6 +120,15 @@ int mx_gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev,
                   const int64_t* tile_off_dev, const uint8_t* seg_vec_dev, int nseg,
                   int64_t total_tiles, int n_slots, const int32_t* plan_dev, int64_t iter,
                   int n_local, int M, float alpha, void* stream);
+/* Graph-replayable form: the round is read on the device from *iter_dev (int64) when the kernel
+ * runs, so one captured launch (hipStreamBeginCapture / torch.cuda.graph) serves every
+ * iteration; a counter outside [0, n_iters) makes the launch a no-op.  mx_iter_advance adds `by`
+ * to the counter on the stream (capture it after the mix). */
+int mx_gossip_mix_at(float* const* seg_ptrs_dev, const int64_t* seg_len_dev,
+                     const int64_t* tile_off_dev, const uint8_t* seg_vec_dev, int nseg,
+                     int64_t total_tiles, int n_slots, const int32_t* plan_dev, const int64_t* iter_dev,
+                     int64_t n_iters, int n_local, int M, float alpha, void* stream);
+int mx_iter_advance(int64_t* iter_dev, int64_t by, void* stream);
 
 /* ---------------------------------------------------------------- flatten / unflatten
  * mx_gather replaces flatten_tensors (comm_helpers.py:12-30): flat[off[s] + i] = src[s][i].

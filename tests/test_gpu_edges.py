@@ -86,3 +86,42 @@ def test_iteration_outside_schedule_raises(pkg):
     ch = pkg.ChocoWorkerGroup(topo, numel=1000, ratio=0.9, consensus_lr=0.1)
     with pytest.raises(IndexError):
         ch.average(3)
+
+
+@pytest.mark.parametrize("P,split", [(181_668, 0), (50_003, 1), (1_000_000, 0)])
+def test_device_round_graph_replay(pkg, O, P, split):
+    """device_round (mx_gossip_mix_at + mx_iter_advance) captured once in a HIP graph
+    (torch.cuda.graph) and replayed: every replay is the next MATCHA round of the schedule --
+    skipped rounds included -- bit-exact vs the oracle; past the schedule's end a replay is a no-op."""
+    saved = pkg.engine.mix_tuning()
+    pkg.engine.set_mix_tuning(split=split)
+    try:
+        n, T = 8, 12
+        np.random.seed(77)
+        GP = pkg.MatchaProcessor(pkg.select_graph(0), 0.4, 0, n, T, True)
+        grp = pkg.VirtualWorkerGroup(GP, numel=P)
+        X = np.stack([O.synth(4000 + i, P) for i in range(n)])
+        grp.rows.copy_(torch.from_numpy(X))
+        partner = np.asarray(GP.neighbors_info, np.int32)
+        grp.iter_dev.fill_(0)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g):
+                grp.device_round()
+                grp.device_round()                   # two rounds per replay
+        torch.cuda.synchronize()
+        assert int(grp.iter_dev.item()) == 0 and np.array_equal(grp.rows.cpu().numpy(), X)  # capture ran nothing
+        rows = len(GP.active_flags)                 # T + 1 rows (graph_manager.py:298-309)
+        for it in range(0, rows + 4, 2):             # the last replays run past the schedule
+            g.replay()
+            for j in (it, it + 1):
+                if j < rows:
+                    X = O.decen_round(X, partner, np.asarray(GP.active_flags[j], np.uint8), GP.neighbor_weight)
+            torch.cuda.synchronize()
+            got = grp.rows.cpu().numpy()
+            assert np.array_equal(got.view(np.uint32), X.view(np.uint32)), f"rounds {it}, {it + 1}"
+        assert int(grp.iter_dev.item()) == len(range(0, rows + 4, 2)) * 2
+    finally:
+        pkg.engine.set_mix_tuning(**saved)

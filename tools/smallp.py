@@ -18,7 +18,7 @@ from conftest import Topo  # noqa: E402
 
 n = 8
 gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, n, 4, True)
-topo = Topo(gp.neighbors_info, 2 / 7, np.ones((4, 5), np.uint8))
+topo = Topo(gp.neighbors_info, 2 / 7, np.ones((64, 5), np.uint8))
 
 
 def events(fn, reps=200, warm=20):
@@ -66,8 +66,25 @@ for P in sizes:
         k_us = events(lambda: grp.engine.mix(0, grp.layout))
         r_us = back_to_back(lambda: grp.step(0))
         h_us = host_only(lambda: grp.step(0))
+        # HIP graph of R device_round()s (no host work per round): GPU-side round time
+        R = 50
+        g = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream()
+        grp.iter_dev.fill_(0)
+        torch.cuda.synchronize()
+        with torch.cuda.stream(side):
+            with torch.cuda.graph(g):
+                for _ in range(R):
+                    grp.device_round()
+
+        def replay():
+            grp.iter_dev.fill_(0)
+            g.replay()
+        g_us = events(replay, reps=20, warm=3) / R
         print(json.dumps({"P": P, "split": sp, "kernel_us": round(k_us, 2), "TBps": round(B / k_us / 1e6, 3),
-                          "round_us_back_to_back": round(r_us, 2), "host_us_per_step": round(h_us, 2)}), flush=True)
+                          "round_us_back_to_back": round(r_us, 2), "host_us_per_step": round(h_us, 2),
+                          "round_us_graph": round(g_us, 2), "TBps_graph": round(B / g_us / 1e6, 3)}), flush=True)
+        del g
     pkg.engine.set_mix_tuning(split=0)
     del grp
     torch.cuda.empty_cache()

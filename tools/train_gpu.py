@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--checkpoint", default=None)
     ap.add_argument("--resume", default=None)
     ap.add_argument("--batched", action="store_true", help="one vmap'd step for all virtual workers")
+    ap.add_argument("--graph", action="store_true", help="with --batched: replay each iteration (step + "
+                    "gossip round) as one captured HIP graph once the learning rate is constant")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -55,7 +57,7 @@ def main():
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
         tr = H.RankTrainer(args, H.model_factory(args), a.batches, rank, world)
     else:
-        tr = H.VirtualTrainer(args, H.model_factory(args), a.batches, batched=a.batched)
+        tr = H.VirtualTrainer(args, H.model_factory(args), a.batches, batched=a.batched or a.graph, graph=a.graph)
         if a.resume:
             tr.load(a.resume)
     import time
