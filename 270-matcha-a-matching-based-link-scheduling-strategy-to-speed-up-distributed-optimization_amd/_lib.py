@@ -41,6 +41,8 @@ SIGNATURES = {
     "mx_choco_apply_work_bytes": (ctypes.c_size_t, [c_i64, c_int]),
     "mx_choco_apply": (c_int, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_int, c_p, c_i64, c_int,
                                c_int, c_f32, c_f32, c_p, c_p]),
+    "mx_choco_apply_at": (c_int, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_int, c_p, c_p, c_i64, c_int,
+                                  c_int, c_f32, c_f32, c_p, c_p]),
     "mx_rccl_unique_id": (c_int, [c_p]),
     "mx_rccl_init": (c_int, [c_p, c_int, c_int, c_p]),
     "mx_rccl_destroy": (c_int, [c_p]),

@@ -72,6 +72,7 @@ class ChocoWorkerGroup:
         self.apply_work = torch.empty(int(lib.mx_choco_apply_work_bytes(P, self.engine.n_slots)),
                                       dtype=torch.uint8, device="cuda")
         self.gamma32 = float(np.float32(consensus_lr))
+        self.iter_dev = torch.zeros(1, dtype=torch.int64, device="cuda")   # device_round's counter
 
     @property
     def rows(self):
@@ -108,6 +109,22 @@ class ChocoWorkerGroup:
                                  self.engine.plan.data_ptr(), int(it), self.n_local, self.engine.M,
                                  self.engine.alpha32, self.gamma32, self.apply_work.data_ptr(),
                                  stream_ptr(stream)), "mx_choco_apply")
+
+    def device_round(self, stream=None):
+        """Graph-replayable round at the device counter `self.iter_dev` (then advanced): top-k of
+        every row, then mx_choco_apply_at, which reads the round on the device and leaves the state
+        untouched for a round without active matchings (the reference skips those,
+        communicator.py:249-250; the messages written meanwhile are scratch).  One GPU only."""
+        if self.engine.comm is not None:
+            raise RuntimeError("device_round: graph-replayable rounds need all partners on this GPU (nranks = 1)")
+        self.compress(0, stream)
+        sp = stream_ptr(stream)
+        check(lib.mx_choco_apply_at(self.x.data_ptr(), self.x_hat.data_ptr(), self.s.data_ptr(), self.ld,
+                                    self.numel, self.k, self.msgs.data_ptr(), self.msg_ld, self.engine.n_slots,
+                                    self.engine.plan.data_ptr(), self.iter_dev.data_ptr(), self.engine.T,
+                                    self.n_local, self.engine.M, self.engine.alpha32, self.gamma32,
+                                    self.apply_work.data_ptr(), sp), "mx_choco_apply_at")
+        check(lib.mx_iter_advance(self.iter_dev.data_ptr(), 1, sp), "mx_iter_advance")
 
     def step(self, it, stream=None):
         """One round at iteration `it`; False (nothing done) for an all-zero flags row."""

@@ -580,10 +580,26 @@ __device__ __forceinline__ int64_t tile_of(int64_t i, int64_t ntiles) {
     return t < ntiles ? t : ntiles;
 }
 
+// The plan record of this round: `rec` itself, or with iter_dev (graph-replayable launches) the
+// record of round *iter_dev of the plan table at `rec`; null (launch is a no-op) when that round
+// is outside [0, n_iters) or has no active matching -- communicator.py:249-250 skips such rounds.
+__device__ __forceinline__ const int32_t* round_rec(const int32_t* rec, const int64_t* iter_dev, int64_t n_iters,
+                                                   int64_t words) {
+    if (!iter_dev) return rec;
+    const int64_t v = *iter_dev;
+    if (v < 0 || v >= n_iters) return nullptr;
+    const int32_t* r = rec + v * words;
+    return r[0] ? r : nullptr;
+}
+
 __global__ __launch_bounds__(kTPB) void bounds_kernel(const char* __restrict__ msgs, int64_t msg_ld,
                                                       int64_t kpad, int64_t k, int64_t ntiles,
-                                                      const int32_t* __restrict__ rec, int n_local,
+                                                      const int32_t* __restrict__ rec_in,
+                                                      const int64_t* __restrict__ iter_dev, int64_t n_iters,
+                                                      int64_t words, int n_local,
                                                       int32_t* __restrict__ bnd) {
+    const int32_t* rec = round_rec(rec_in, iter_dev, n_iters, words);
+    if (!rec) return;
     const int slot = blockIdx.y;
     if (slot >= n_local + rec[1]) return;
     const Msg m = msg_at(msgs, msg_ld, kpad, slot);
@@ -600,8 +616,12 @@ __global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, floa
                                                      const char* __restrict__ msgs, int64_t msg_ld,
                                                      int64_t kpad, int64_t ntiles,
                                                      const int32_t* __restrict__ bnd,
-                                                     const int32_t* __restrict__ rec, int n_local, int M,
+                                                     const int32_t* __restrict__ rec_in,
+                                                     const int64_t* __restrict__ iter_dev, int64_t n_iters,
+                                                     int64_t words, int n_local, int M,
                                                      float alpha, float g) {
+    const int32_t* rec = round_rec(rec_in, iter_dev, n_iters, words);
+    if (!rec) return;
     __shared__ float ls[kTile], lh[kTile];
     __shared__ uint8_t ds[kTile / kGran], dh[kTile / kGran];
     const int r = blockIdx.y;
@@ -803,10 +823,34 @@ extern "C" size_t mx_choco_apply_work_bytes(int64_t P, int n_slots) {
     return sizeof(int32_t) * (size_t)(n_tiles(P < 1 ? 1 : P) + 1) * (size_t)(n_slots < 1 ? 1 : n_slots);
 }
 
+namespace {
+int choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t k, const void* msgs,
+                int64_t msg_ld_bytes, int n_slots, const int32_t* plan_dev, int64_t iter, const int64_t* iter_dev,
+                int n_local, int M, float alpha, float gamma, void* work, void* stream);
+}
+
 extern "C" int mx_choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t k,
                               const void* msgs, int64_t msg_ld_bytes, int n_slots, const int32_t* plan_dev,
                               int64_t iter, int n_local, int M, float alpha, float gamma, void* work,
                               void* stream) {
+    MX_CHECK(iter >= 0, "mx_choco_apply: iter < 0");
+    return choco_apply(x, xhat, s, ld, P, k, msgs, msg_ld_bytes, n_slots, plan_dev, iter, nullptr, n_local, M,
+                       alpha, gamma, work, stream);
+}
+
+extern "C" int mx_choco_apply_at(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t k,
+                                 const void* msgs, int64_t msg_ld_bytes, int n_slots, const int32_t* plan_dev,
+                                 const int64_t* iter_dev, int64_t n_iters, int n_local, int M, float alpha,
+                                 float gamma, void* work, void* stream) {
+    MX_CHECK(iter_dev && n_iters >= 0, "mx_choco_apply_at: bad iteration counter");
+    return choco_apply(x, xhat, s, ld, P, k, msgs, msg_ld_bytes, n_slots, plan_dev, n_iters, iter_dev, n_local, M,
+                       alpha, gamma, work, stream);
+}
+
+namespace {
+int choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t k, const void* msgs,
+                int64_t msg_ld_bytes, int n_slots, const int32_t* plan_dev, int64_t iter, const int64_t* iter_dev,
+                int n_local, int M, float alpha, float gamma, void* work, void* stream) {
     MX_CHECK(x && xhat && s && msgs && plan_dev && work, "mx_choco_apply: null pointer");
     MX_CHECK(P >= 1 && k >= 1 && k <= P && ld >= P && k < (int64_t)1 << 31, "mx_choco_apply: P=%lld k=%lld ld=%lld",
              (long long)P, (long long)k, (long long)ld);
@@ -816,16 +860,19 @@ extern "C" int mx_choco_apply(float* x, float* xhat, float* s, int64_t ld, int64
     MX_CHECK(msg_ld_bytes >= 4 * kpad + 8 * k && msg_ld_bytes % 8 == 0, "mx_choco_apply: msg_ld %lld",
              (long long)msg_ld_bytes);
     hipStream_t st = mx::as_stream(stream);
-    const int32_t* rec = plan_dev + iter * mx::plan_words(n_local, M);
+    const int64_t words = mx::plan_words(n_local, M);
+    const int32_t* rec = iter_dev ? plan_dev : plan_dev + iter * words;   // with iter_dev: iter = n_iters
     const int64_t nt = n_tiles(P);
     int32_t* bnd = static_cast<int32_t*>(work);
     const char* m = static_cast<const char*>(msgs);
     hipLaunchKernelGGL(bounds_kernel, dim3(clamp_grid(k + 1, kTPB * 4, 1024), n_slots), dim3(kTPB), 0, st, m,
-                       msg_ld_bytes, kpad, k, nt, rec, n_local, bnd);
+                       msg_ld_bytes, kpad, k, nt, rec, iter_dev, iter, words, n_local, bnd);
     MX_LAUNCH_CHECK();
     MX_CHECK(nt <= 0x7fffffff, "mx_choco_apply: P too large");
     hipLaunchKernelGGL(apply_kernel, dim3((unsigned)nt, n_local), dim3(kTPB), 0, st, x, xhat, s, ld, P, m,
-                       msg_ld_bytes, kpad, nt, (const int32_t*)bnd, rec, n_local, M, alpha, gamma);
+                       msg_ld_bytes, kpad, nt, (const int32_t*)bnd, rec, iter_dev, iter, words, n_local, M, alpha,
+                       gamma);
     MX_LAUNCH_CHECK();
     return MX_OK;
 }
+}  // namespace

@@ -216,8 +216,8 @@ class VirtualTrainer:
         self.epoch = 0
         self.batched = bool(batched)
         self.graph = bool(graph)
-        if self.graph and (not self.batched or args.compress):
-            raise ValueError("graph mode needs batched=True and decentralized (non-Choco) gossip")
+        if self.graph and not self.batched:
+            raise ValueError("graph mode needs batched=True")
         self._graphs = {}
         self._dev_iter_synced = False
         if self.batched:
@@ -296,7 +296,8 @@ class VirtualTrainer:
         cs = self._cap_stream
         cs.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(cs):
-            scratch = self.group.arena.clone()
+            base = self.group.x if hasattr(self.group, "x_hat") else self.group.arena
+            scratch = base.clone()
             n = scratch.shape[0]
             views = {name: scratch[:, off:off + v.shape[1:].numel()].view(v.shape)
                      for (name, v), off in zip(self._stack.items(), self._stack_off)}

@@ -192,6 +192,11 @@ int mx_choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64
                    const void* msgs, int64_t msg_ld_bytes, int n_slots, const int32_t* plan_dev,
                    int64_t iter, int n_local, int M, float alpha, float gamma, void* work,
                    void* stream);
+/* Graph-replayable form (as mx_gossip_mix_at): the round is *iter_dev, read on the device; a
+ * round outside [0, n_iters) or with no active matching leaves x, x_hat and s untouched. */
+int mx_choco_apply_at(float* x, float* x_hat, float* s, int64_t ld, int64_t P, int64_t k, const void* msgs,
+                      int64_t msg_ld_bytes, int n_slots, const int32_t* plan_dev, const int64_t* iter_dev,
+                      int64_t n_iters, int n_local, int M, float alpha, float gamma, void* work, void* stream);
 
 /* ---------------------------------------------------------------- cross-GPU exchange (RCCL)
  * One process per GPU; workers partitioned by owner[].  mx_exchange_round posts, inside one

@@ -124,19 +124,24 @@ def test_batched_step_matches_per_worker_sgd(pkg, momentum, nesterov):
         float((seq.group.rows - bat.group.rows).abs().max())
 
 
-@pytest.mark.parametrize("momentum,nesterov,matcha", [(0.0, False, True), (0.9, False, True), (0.9, True, False)])
-def test_graph_mode_identical_to_batched(pkg, momentum, nesterov, matcha):
+@pytest.mark.parametrize("momentum,nesterov,matcha,compress", [(0.0, False, True, False), (0.9, False, True, False),
+                                                               (0.9, True, False, False), (0.0, False, True, True),
+                                                               (0.9, False, True, True)])
+def test_graph_mode_identical_to_batched(pkg, momentum, nesterov, matcha, compress):
     """graph=True replays one captured HIP graph per learning rate (forward / backward / SGD +
     the gossip round at the device counter): rows, per-worker losses / accuracies and the
     iteration counter equal the eager batched trainer's exactly."""
     H = pkg.harness
-    args = _args(pkg, momentum=momentum, nesterov=nesterov, epoch=3, lr=0.05, matcha=matcha)
+    args = _args(pkg, momentum=momentum, nesterov=nesterov, epoch=3, lr=0.05, matcha=matcha, compress=compress,
+                 ratio=0.9, budget=0.3 if compress else 0.5)
     eag = H.VirtualTrainer(args, H.model_factory(args), n_batches=4, batched=True)
     gra = H.VirtualTrainer(args, H.model_factory(args), n_batches=4, batched=True, graph=True)
     for e in range(3):
         se = eag.train_epoch()
         sg = gra.train_epoch()
         assert torch.equal(eag.group.rows, gra.group.rows), f"epoch {e}"
+        if compress:
+            assert torch.equal(eag.group.x_hat, gra.group.x_hat) and torch.equal(eag.group.s, gra.group.s)
         assert [s["loss"] for s in se] == [s["loss"] for s in sg]
         assert [s["train_acc"] for s in se] == [s["train_acc"] for s in sg]
     assert eag.group.iter == gra.group.iter == 12
