@@ -43,6 +43,11 @@ def parse():
                     help="N > 1 partner exchange: rccl (the product path, one GPU per rank) or gloo "
                          "(tests/gloo_transport.py: host staging, lets N ranks share one GPU to test "
                          "the multi-process path; never a performance number)")
+    ap.add_argument("--overlap", choices=("auto", "on", "off"), default="auto",
+                    help="N > 1: column-pipelined exchange (RCCL on a side stream overlapped with mixing; "
+                         "VirtualWorkerGroup chunk_cols) -- auto: time both forms over a few untimed rounds and "
+                         "use the faster for the timed region; on / off: force")
+    ap.add_argument("--chunk-cols", type=int, default=0, help="pipelined chunk width (0: a quarter of the row)")
     ap.add_argument("--placement", choices=("auto", "contiguous"), default="auto",
                     help="N > 1: which workers share a GPU -- auto (placement.best_placement, fewest rows "
                          "over the busiest xGMI pair) or contiguous id blocks")
@@ -217,8 +222,10 @@ def main():
 
     n, P = args.workers, args.params
     K, W = args.steps, args.warmup
+    R = 4                                        # N > 1: untimed calibration rounds per exchange form
     np.random.seed(1234)
-    GP = pkg.MatchaProcessor(pkg.select_graph(args.graph), args.budget, rank, n, W + 2 * K, True)
+    GP = pkg.MatchaProcessor(pkg.select_graph(args.graph), args.budget, rank, n,
+                             W + 2 * K + (R + 1 if world > 1 else 0), True)
     group = pkg.VirtualWorkerGroup(GP, numel=P, rank=rank, nranks=world, comm=comm, placement=args.placement)
     for r in range(group.n_local):
         pkg._lib.check(pkg.lib.mx_synth_fill(group.rows[r].data_ptr(), P, 1234 + group.workers[r], None))
@@ -227,12 +234,48 @@ def main():
     for it in range(W):
         group.step(it)
     torch.cuda.synchronize()
+    timed, overlap = group, None
+    any_remote = world > 1 and max_over_ranks(float(group.engine.max_remote), world, dev) > 0   # collective
+    if any_remote and args.overlap != "off":
+        # column pipelining: chunk c+1 of every exchanged row travels on a side stream while chunk c
+        # is mixed (bit-identical results).  Whether it pays depends on the link rate vs the extra
+        # RCCL groups per round, so with "auto" both forms run R untimed rounds and the faster one
+        # (max over ranks, so every rank picks the same) is the one timed.
+        C = args.chunk_cols or ((P + 3) // 4 + 63) // 64 * 64
+        gchunk = pkg.VirtualWorkerGroup(GP, numel=P, rank=rank, nranks=world, comm=comm, placement=args.placement,
+                                        chunk_cols=C)
+        for r in range(gchunk.n_local):
+            pkg._lib.check(pkg.lib.mx_synth_fill(gchunk.rows[r].data_ptr(), P, 1234 + gchunk.workers[r], None))
+        base_it = W + 2 * K
+
+        def calib(g, first):
+            torch.cuda.synchronize()
+            dist.barrier()
+            t = time.perf_counter()
+            for j in range(R):
+                g.step(first + j)
+            torch.cuda.synchronize()
+            dist.barrier()
+            return max_over_ranks((time.perf_counter() - t) / R, world, dev)
+
+        gchunk.step(base_it)                     # first chunked round (side stream, events) untimed
+        t_plain = calib(group, base_it) if args.overlap == "auto" else None
+        t_chunk = calib(gchunk, base_it + 1)
+        use_chunk = args.overlap == "on" or t_chunk < t_plain
+        overlap = {"mode": args.overlap, "chunk_cols": C, "chunks": len(getattr(gchunk, "chunks", [None])),
+                   "calib_ms_unchunked": 1e3 * t_plain if t_plain else None, "calib_ms_chunked": 1e3 * t_chunk,
+                   "chosen": "chunked" if use_chunk else "unchunked",
+                   "note": f"{R} untimed rounds per form before the timed region, max over ranks"}
+        if use_chunk:
+            timed = gchunk
+        else:
+            del gchunk
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for j in range(K):                           # the timed rounds: back to back, nothing else
-        group.step(W + j)
+        timed.step(W + j)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -363,7 +406,8 @@ def main():
                                    f"budget {args.budget} ({'every matching active' if args.budget >= 1 else 'MATCHA schedule'})",
                        "workers": n, "params_per_worker": P, "graph": args.graph, "budget": args.budget,
                        "parallelism": f"{n} workers over {world} GPU(s)" +
-                                      (f", placement {args.placement}" if world > 1 else ""),
+                                      (f", placement {args.placement}" if world > 1 else "") +
+                                      (", column-pipelined exchange" if timed is not group else ""),
                        "placement": group.placement if world > 1 else None,
                        "transport": args.transport if world > 1 else None},
             "roofline": {"bound": "hbm", "kernel": f"{pkg.engine.mix_kernel_name(eng.n_slots)} (mx_gossip_mix)",
@@ -377,6 +421,7 @@ def main():
                          "note": "achieved = algorithmic bytes (2 x active rows x P x 4 [+ slab rows]) / "
                                  "mean per-launch duration, HIP events on the launch stream"},
             "matcha_schedule": matcha,
+            "overlap": overlap,
             "choco": choco,
         }
         if world > 1:

@@ -52,7 +52,24 @@ def test_bench_multiprocess_path():
     out = json.loads(line)
     assert out["n_gpus"] == 2 and out["value"] > 0 and out["xgmi"]["max_link_bytes_per_round"] > 0
     assert out["xgmi"]["exchange_only_ms"] > 0 and out["xgmi"]["p2p_probe"]["uni_GBps"] > 0
+    ov = out["overlap"]
+    assert ov["mode"] == "auto" and ov["chunks"] == 4 and ov["chosen"] in ("chunked", "unchunked")
+    assert ov["calib_ms_unchunked"] > 0 and ov["calib_ms_chunked"] > 0
     assert out["choco"]["rounds_per_s"] > 0 and out["cpu_baseline"] is None
+
+
+@pytest.mark.parametrize("nproc,overlap", [(2, "on"), (4, "off")])
+def test_bench_multiprocess_overlap_forms(nproc, overlap):
+    """bench.py's N > 1 branch with the exchange form forced (column-pipelined / plain)."""
+    r = _torchrun(nproc, ["bench.py", "--gpus", str(nproc), "--transport", "gloo", "--steps", "3", "--warmup", "1",
+                          "--params", "100000", "--choco", "0", "--cpu-seconds", "0", "--overlap", overlap])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["value"] > 0
+    if overlap == "on":
+        assert out["overlap"]["chosen"] == "chunked" and "column-pipelined" in out["config"]["parallelism"]
+    else:
+        assert out["overlap"] is None
 
 
 def test_dropin_communicators_one_process_per_worker():
