@@ -43,6 +43,8 @@ def parse():
                     help="N > 1 partner exchange: rccl (the product path, one GPU per rank) or gloo "
                          "(tests/gloo_transport.py: host staging, lets N ranks share one GPU to test "
                          "the multi-process path; never a performance number)")
+    ap.add_argument("--allreduce", type=int, default=1, help="also time all-reduce averaging (the paper's "
+                    "centralized baseline) on the same rows")
     ap.add_argument("--overlap", choices=("auto", "on", "off"), default="auto",
                     help="N > 1: column-pipelined exchange (RCCL on a side stream overlapped with mixing; "
                          "VirtualWorkerGroup chunk_cols) -- auto: time both forms over a few untimed rounds and "
@@ -152,6 +154,41 @@ def p2p_probe(rank, world, nbytes, dev, reps=5):
         res[mode] = max_over_ranks(float(np.median(res[mode])), world, dev)
     del buf, rbuf
     return res
+
+
+def allreduce_figure(group, n, world, dev, K, W):
+    """Context figure: the all-reduce averaging the paper compares gossip against
+    (centralizedCommunicator, communicator.py:46-76 / sync_allreduce): every worker's row becomes
+    the mean of all workers' rows -- local row sum, torch.distributed all_reduce (RCCL at N > 1),
+    / n, written back to every local row.  torch ops, not the product path; rounds/s like `value`."""
+    import torch.distributed as dist
+    rows = group.rows
+
+    def one():
+        acc = rows.sum(0)
+        if world > 1:
+            if dev == "cpu":                     # gloo test transport: host staging
+                h = acc.cpu()
+                dist.all_reduce(h)
+                acc.copy_(h)
+            else:
+                dist.all_reduce(acc)
+        rows.copy_((acc / n).expand_as(rows))
+
+    for _ in range(W):
+        one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t = time.perf_counter()
+    for _ in range(K):
+        one()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = max_over_ranks(time.perf_counter() - t, world, dev)
+    return {"rounds_per_s": K / el, "ms_per_round": 1e3 * el / K,
+            "how": "row sum + torch.distributed all_reduce (RCCL at N > 1) + / n + copy back; torch ops"}
 
 
 def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99, gamma=0.1, placement=None):
@@ -337,6 +374,8 @@ def main():
                   "skipped_rounds": int((fl.sum(1) == 0).sum())}
         del gm
 
+    allreduce = allreduce_figure(group, n, world, dev, max(5, K // 5), 2) if args.allreduce else None
+
     choco = (choco_figure(pkg, GP, rank, world, max(5, K // 5), 3, comm, dev, P=args.choco_params,
                           placement=args.placement)
              if args.choco else None)
@@ -421,6 +460,7 @@ def main():
                          "note": "achieved = algorithmic bytes (2 x active rows x P x 4 [+ slab rows]) / "
                                  "mean per-launch duration, HIP events on the launch stream"},
             "matcha_schedule": matcha,
+            "allreduce_baseline": allreduce,
             "overlap": overlap,
             "choco": choco,
         }

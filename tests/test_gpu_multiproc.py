@@ -56,6 +56,7 @@ def test_bench_multiprocess_path():
     assert ov["mode"] == "auto" and ov["chunks"] == 4 and ov["chosen"] in ("chunked", "unchunked")
     assert ov["calib_ms_unchunked"] > 0 and ov["calib_ms_chunked"] > 0
     assert out["choco"]["rounds_per_s"] > 0 and out["cpu_baseline"] is None
+    assert out["allreduce_baseline"]["rounds_per_s"] > 0
 
 
 @pytest.mark.parametrize("nproc,overlap", [(2, "on"), (4, "off")])
