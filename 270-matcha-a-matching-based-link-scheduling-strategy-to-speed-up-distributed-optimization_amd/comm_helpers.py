@@ -23,9 +23,12 @@ def flatten_tensors(tensors):
     tensors = list(tensors)
     if not tensors:
         raise ValueError("flatten_tensors needs at least one tensor")
+    dev = tensors[0].device
     for t in tensors:
-        if t.device.type != "cuda" or t.dtype != torch.float32:
-            raise TypeError("flatten_tensors runs on the GPU: float32 CUDA tensors required")
+        if t.dtype != torch.float32 or t.device != dev:
+            raise TypeError("flatten_tensors: float32 tensors on one device required")
+    if dev.type != "cuda":    # the reference's CPU tensors: gathered on the GPU, returned on the CPU
+        return flatten_tensors([t.to("cuda") for t in tensors]).to(dev)
     src = [t.contiguous() for t in tensors]
     off = _offsets(src)
     total = int(off[-1])

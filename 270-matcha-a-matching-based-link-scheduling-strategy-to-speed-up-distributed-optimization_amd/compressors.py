@@ -9,10 +9,14 @@ def get_top_k(x, ratio):
     """Top (1 - ratio) fraction of x by magnitude: k = max(1, int(len * (1 - ratio))).
     Returns (x[indices], indices int64).  Indices come back in ascending order; among equal
     magnitudes at the k-th threshold the lowest indices are kept (the reference's
-    torch.topk(sorted=False) / torch.max leave both unspecified)."""
-    x_data = x.view(-1)
-    if x_data.device.type != "cuda" or x_data.dtype != torch.float32:
-        raise TypeError("get_top_k runs on the GPU: a float32 CUDA tensor is required")
+    torch.topk(sorted=False) / torch.max leave both unspecified).  CPU input (the reference's
+    default) is staged to the GPU and the result returned on the input's device."""
+    x_data = x.reshape(-1)
+    if x_data.dtype != torch.float32:
+        raise TypeError("get_top_k: a float32 tensor is required")
+    host = x_data.device.type != "cuda"
+    if host:                  # the reference's CPU tensors: staged to the GPU, selected there, returned
+        x_data = x_data.to("cuda")
     x_data = x_data.contiguous()
     P = x_data.numel()
     k = topk_count(P, ratio)
@@ -21,4 +25,6 @@ def get_top_k(x, ratio):
     work = torch.empty(int(lib.mx_topk_work_bytes(P)), dtype=torch.uint8, device=x_data.device)
     check(lib.mx_topk_abs_diff(x_data.data_ptr(), None, P, k, vals.data_ptr(), idx.data_ptr(),
                                work.data_ptr(), stream_ptr()), "mx_topk_abs_diff")
+    if host:
+        return vals.to(x.device), idx.to(x.device)
     return vals, idx

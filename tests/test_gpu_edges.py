@@ -125,3 +125,19 @@ def test_device_round_graph_replay(pkg, O, P, split):
         assert int(grp.iter_dev.item()) == len(range(0, rows + 4, 2)) * 2
     finally:
         pkg.engine.set_mix_tuning(**saved)
+
+
+def test_cpu_inputs_staged_through_the_gpu(pkg, O):
+    """The reference keeps models on the CPU (train_mpi.py:92 has .cuda() commented out):
+    flatten_tensors / get_top_k take CPU tensors, compute on the GPU and answer on the CPU."""
+    ts = [torch.from_numpy(O.synth(60 + i, n)).reshape(shape) for i, (n, shape) in
+          enumerate(((15, (3, 5)), (7, (7,)), (2112, (64, 33))))]
+    flat = pkg.flatten_tensors(ts)
+    assert flat.device.type == "cpu" and torch.equal(flat, torch.cat([t.reshape(-1) for t in ts]))
+    x = O.synth(91, 50_001)
+    v, i = pkg.get_top_k(torch.from_numpy(x), 0.99)
+    ov, oi = O.topk_abs(x, O.topk_k(50_001, 0.99))
+    assert v.device.type == "cpu" and i.device.type == "cpu" and i.dtype == torch.int64
+    assert np.array_equal(i.numpy(), oi) and np.array_equal(v.numpy().view(np.uint32), ov.view(np.uint32))
+    with pytest.raises(TypeError):
+        pkg.flatten_tensors([ts[0], ts[1].cuda()])
