@@ -36,8 +36,8 @@ SIGNATURES = {
     "mx_topk_set": (c_int, [ctypes.c_char_p, c_i64]),
     "mx_topk_get": (c_i64, [ctypes.c_char_p]),
     "mx_topk_abs_diff": (c_int, [c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p]),
-    "mx_topk_abs_diff_rows": (c_int, [c_p, c_p, c_i64, c_int, c_i64, c_i64, c_p, c_i64, c_i64, c_p, c_i64, c_p]),
-    "mx_choco_msg_bytes": (c_i64, [c_i64]),
+    "mx_topk_abs_diff_rows": (c_int, [c_p, c_p, c_i64, c_int, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_p]),
+    "mx_choco_msg_bytes": (c_i64, [c_i64, c_i64]),
     "mx_choco_apply_work_bytes": (ctypes.c_size_t, [c_i64, c_int]),
     "mx_choco_apply": (c_int, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_int, c_p, c_i64, c_int,
                                c_int, c_f32, c_f32, c_p, c_p]),

@@ -64,11 +64,13 @@ class ChocoWorkerGroup:
                     off += k
         self.k = topk_count(P, ratio)
         self.kpad = (self.k + 1) // 2 * 2
-        self.msg_bytes = int(lib.mx_choco_msg_bytes(self.k))
+        # vals f32[kpad] | idx int64[k] | tile bounds int32[ceil(P/4096) + 1] (written by the top-k)
+        self.msg_bytes = int(lib.mx_choco_msg_bytes(P, self.k))
+        self.bnd_off = 4 * self.kpad + 8 * self.k
         self.msg_ld = (self.msg_bytes + 255) // 256 * 256
         self.msgs = torch.empty(self.engine.n_slots * self.msg_ld, dtype=torch.uint8, device="cuda")
         self.work_ld = int(lib.mx_topk_work_bytes(P))
-        self.work = torch.empty(self.n_local * self.work_ld, dtype=torch.uint8, device="cuda")
+        self.work = torch.zeros(self.n_local * self.work_ld, dtype=torch.uint8, device="cuda")  # zero on first use
         self.apply_work = torch.empty(int(lib.mx_choco_apply_work_bytes(P, self.engine.n_slots)),
                                       dtype=torch.uint8, device="cuda")
         self.gamma32 = float(np.float32(consensus_lr))
@@ -90,7 +92,7 @@ class ChocoWorkerGroup:
         x - x_hat into its message slot."""
         check(lib.mx_topk_abs_diff_rows(self.x.data_ptr(), self.x_hat.data_ptr(), self.ld, self.n_local,
                                         self.numel, self.k, self.msgs.data_ptr(), self.msg_ld, 4 * self.kpad,
-                                        self.work.data_ptr(), self.work_ld, stream_ptr(stream)),
+                                        self.bnd_off, self.work.data_ptr(), self.work_ld, stream_ptr(stream)),
               "mx_topk_abs_diff_rows")
 
     def average(self, it, stream=None):

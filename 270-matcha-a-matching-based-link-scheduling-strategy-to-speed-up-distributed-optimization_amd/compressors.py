@@ -22,7 +22,7 @@ def get_top_k(x, ratio):
     k = topk_count(P, ratio)
     vals = torch.empty(k, dtype=torch.float32, device=x_data.device)
     idx = torch.empty(k, dtype=torch.int64, device=x_data.device)
-    work = torch.empty(int(lib.mx_topk_work_bytes(P)), dtype=torch.uint8, device=x_data.device)
+    work = torch.zeros(int(lib.mx_topk_work_bytes(P)), dtype=torch.uint8, device=x_data.device)  # zero on first use
     check(lib.mx_topk_abs_diff(x_data.data_ptr(), None, P, k, vals.data_ptr(), idx.data_ptr(),
                                work.data_ptr(), stream_ptr()), "mx_topk_abs_diff")
     if host:

@@ -13,18 +13,27 @@
 //                      to the sample with a 25 % + 4 sigma margin), then, one 4096-element chunk
 //                      per block iteration, stores every key whose digit is >= b_lo as (value,
 //                      chunk-local index) into the chunk's own region in index order (wave scans
-//                      + one barrier) and counts its top digit into the 12-bit candidate histogram;
-//      count_kernel    candidates per row; compact_kernel(fallback) re-runs with b_lo = 0 in the
-//                      (sample-dependent, rare) case that fewer than k were kept -- the result is
-//                      exact either way;
+//                      + one barrier), counts its top digit into the 12-bit candidate histogram
+//                      and adds the block's kept count to the row's candidate total;
+//                      compact_kernel(fallback) re-runs with b_lo = 0 (into a histogram of its
+//                      own) in the (sample-dependent, rare) case that fewer than k were kept --
+//                      the result is exact either way;
 //   C  cand_hist<10>, cand_hist<9>: the 10- and 9-bit digits of the candidates matching the
 //      prefix resolved so far; every block of a pass re-resolves the previous histograms itself
 //      (find_bin, read-only), so no one-block select launches sit between the passes;
 //      cand_mark resolves the exact threshold key T and the number of its ties to take, and
-//      counts > T / == T per chunk; scan_kernel turns them into output offsets; write_cand emits
-//      the selected candidates in index order (values = x - x_hat, int64 indices).
+//      counts > T / == T per chunk; scan_kernel turns them into output offsets (a kernel boundary,
+//      not a last-block tail: a device-scope fence per block writes back and invalidates the XCD's
+//      L2 and measured slower); write_cand emits the selected candidates in index order
+//      (values = x - x_hat, int64 indices) and, optionally, the message's per-4096-element tile
+//      bounds that mx_choco_apply reads (the output offset of every chunk), and re-zeroes the
+//      histograms / counters for the next call.
 // Everything stays on the device; no host round trip.  All local workers' rows are processed by
-// the same launches (blockIdx.y = row): 10 launches per round for any number of rows.
+// the same launches (blockIdx.y = row): 7 launches per call for any number of rows (8 with the
+// fallback pass that sampling needs).
+//
+// Work invariant: the histograms and the candidate total are zero on entry (the
+// caller zero-fills the scratch once; every call leaves it that way), so no zeroing launch runs.
 #include "mx_common.h"
 
 namespace {
@@ -35,18 +44,18 @@ constexpr int kSubQuads = kSub / 4;
 constexpr int kChunk = kWaves * kSub;        // elements per chunk = one block (candidate region)
 constexpr int kTopBits = 12, kTopShift = 19;
 constexpr int kTopBins = 1 << kTopBits;
+constexpr int kScanTPB = 1024;
 constexpr int kMidBits = 10, kMidShift = 9;  // bits 9..18
 constexpr int kLowBits = 9;                  // bits 0..8
-constexpr int kScanTPB = 1024;
 constexpr int64_t kSampleTarget = 1 << 18;   // sampled elements per row (auto stride)
 
-constexpr int kHistWords = 2 * kTopBins + (1 << kMidBits) + (1 << kLowBits);   // hs, h12, h10, h9
+constexpr int kHistWords = 3 * kTopBins + (1 << kMidBits) + (1 << kLowBits);   // hs, h12, h12f, h10, h9
 
 struct SelState {
     uint32_t b0;          // lowest top digit kept as a candidate (b_lo)
     uint32_t T;           // exact threshold key (cand_mark)
     int64_t need;         // ties of T to take (cand_mark)
-    int64_t cand_n;       // candidates kept by compact_kernel
+    unsigned long long cand_n;   // candidates kept by the first compact_kernel pass (zero on entry)
 };
 
 struct WorkLayout {
@@ -80,6 +89,7 @@ struct Rows {
     char* work;
     int64_t work_ld;
     int64_t P, k;
+    int64_t bnd_off;      // int32 tile bounds at out + r*out_ld + bnd_off (< 0: not written)
 };
 
 struct RowView {
@@ -87,6 +97,7 @@ struct RowView {
     const float* xh;
     uint32_t* hs;         // sampled top digits
     uint32_t* h12;        // candidates' top digits
+    uint32_t* h12f;       // the same, of the fallback pass (keeps every key)
     uint32_t* h10;        // next 10 bits of the candidates in the threshold bin
     uint32_t* h9;         // last 9 bits
     SelState* st;
@@ -107,7 +118,8 @@ __device__ __forceinline__ RowView row_view(const Rows& R) {
     v.xh = R.xh ? R.xh + (int64_t)r * R.ld : nullptr;
     v.hs = reinterpret_cast<uint32_t*>(wb + w.hist);
     v.h12 = v.hs + kTopBins;
-    v.h10 = v.h12 + kTopBins;
+    v.h12f = v.h12 + kTopBins;
+    v.h10 = v.h12f + kTopBins;
     v.h9 = v.h10 + (1 << kMidBits);
     v.st = reinterpret_cast<SelState*>(wb + w.state);
     v.cnt = reinterpret_cast<int64_t*>(wb + w.cnt);
@@ -172,12 +184,6 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
     return v;
-}
-
-// zero every row's histograms (sample, 12 / 10 / 9-bit candidate digits): one launch per batch
-__global__ __launch_bounds__(kTPB) void zero_hist(Rows R) {
-    const RowView v = row_view(R);
-    for (int i = threadIdx.x; i < kHistWords; i += kTPB) v.hs[i] = 0;
 }
 
 // ---- S: top-digit histogram over every S-th 1024-element piece, one wave per sampled piece
@@ -267,7 +273,8 @@ __device__ Resolved resolve(const RowView& v, int64_t k, int stages) {
     Resolved z{0u, 0u, k};
     int b;
     int64_t rem, tot;
-    find_bin<kTopBins>(v.h12, z.need, &b, &rem, &tot);
+    const bool fb = v.st->cand_n < (unsigned long long)k;   // the fallback pass ran for this row
+    find_bin<kTopBins>(fb ? v.h12f : v.h12, z.need, &b, &rem, &tot);
     z.prefix = (uint32_t)b << kTopShift;
     z.mask = 0xfffu << kTopShift;
     z.need = rem;
@@ -298,7 +305,7 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double
     const RowView v = row_view(R);
     uint32_t b_lo = 0;
     if (fallback) {
-        if (v.st->cand_n >= R.k) return;
+        if (v.st->cand_n >= (unsigned long long)R.k) return;
     } else {
         int64_t want = R.k;
         if (S > 1) {
@@ -330,6 +337,7 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double
         }
     };
     int64_t c = blockIdx.x;
+    uint32_t kept = 0;                             // this block's candidates (thread 0)
     if (c < nc && whole(c)) issue(c);
     __syncthreads();                               // h zeroed
     for (int par = 0; c < nc; c += gridDim.x, par ^= 1) {
@@ -391,34 +399,14 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double
         if (threadIdx.x == 0) {
             v.cnt[4 * c + 0] = 0;
             v.cnt[4 * c + 3] = all;
+            kept += all;
         }
     }
     __syncthreads();
+    uint32_t* out = fallback ? v.h12f : v.h12;
     for (int i = threadIdx.x; i < kTopBins; i += kTPB)
-        if (h[i]) atomicAdd(&v.h12[i], h[i]);
-}
-
-// one block per row: total candidates; if they are fewer than k the fallback pass will run, so
-// its 12-bit histogram starts from zero again
-__global__ __launch_bounds__(kScanTPB) void count_kernel(Rows R) {
-    const RowView v = row_view(R);
-    const int64_t nc = n_chunks(R.P);
-    __shared__ int64_t ws[kScanTPB / 64];
-    __shared__ int64_t s_tot;
-    int64_t s = 0;
-    for (int64_t c = threadIdx.x; c < nc; c += kScanTPB) s += v.cnt[4 * c + 3];
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = s;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int64_t t = 0;
-        for (int w = 0; w < kScanTPB / 64; ++w) t += ws[w];
-        v.st->cand_n = t;
-        s_tot = t;
-    }
-    __syncthreads();
-    if (s_tot < R.k)
-        for (int i = threadIdx.x; i < kTopBins; i += kScanTPB) v.h12[i] = 0;
+        if (h[i]) atomicAdd(&out[i], h[i]);
+    if (!fallback && threadIdx.x == 0 && kept) atomicAdd(&v.st->cand_n, (unsigned long long)kept);
 }
 
 // candidate histogram of the next digit (10 bits at 9, or 9 bits at 0) among candidates matching
@@ -522,11 +510,21 @@ __global__ __launch_bounds__(kTPB) void write_cand(Rows R) {
     const RowView v = row_view(R);
     const uint32_t T = v.st->T;
     const int64_t need_eq = v.st->need;
+    // nothing reads the histograms or the candidate total any more: re-zero them for the next call
+    for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < kHistWords; i += (int64_t)gridDim.x * kTPB)
+        v.hs[i] = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) v.st->cand_n = 0;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t c = (int64_t)blockIdx.x * kWaves + wave;
-    if (c >= n_chunks(R.P)) return;
+    const int64_t nchunks = n_chunks(R.P);
+    if (c >= nchunks) return;
     const int64_t nc = v.cnt[4 * c + 3];
     int64_t run_out = v.off[2 * c], run_eq = v.off[2 * c + 1];
+    if (R.bnd_off >= 0 && lane == 0) {             // chunk c is apply tile c: its first entry
+        int32_t* bnd = reinterpret_cast<int32_t*>(R.out + (int64_t)blockIdx.y * R.out_ld + R.bnd_off);
+        bnd[c] = (int32_t)run_out;
+        if (c == nchunks - 1) bnd[nchunks] = (int32_t)R.k;
+    }
     for (int64_t i0 = 0; i0 < nc; i0 += 64) {
         const int64_t i = i0 + lane;
         const bool in = i < nc;
@@ -556,28 +554,26 @@ __global__ __launch_bounds__(kTPB) void write_cand(Rows R) {
 // x_hat read once, their dirty granules written, and the messages read once.
 //
 // Messages are index-sorted, so the entries of message `slot` inside tile t are the range
-// [bnd[slot][t], bnd[slot][t+1]) (bounds_kernel: a linear pass over the index arrays).
+// [bnd[t], bnd[t+1]) of the bounds the sender's write_cand stored after the message's indices
+// (tile t = top-k chunk t: bnd[t] is that chunk's output offset).
 constexpr int kTile = 4096;                    // elements per apply tile (16 KB of s + 16 KB of x_hat)
 constexpr int kGran = 16;                      // floats per dirty granule (64 B)
 
 __host__ __device__ inline int64_t n_tiles(int64_t P) { return (P + kTile - 1) / kTile; }
 
+static_assert(kTile == kChunk, "apply tiles are the top-k chunks (the message bounds are chunk offsets)");
+
 struct Msg {
     const float* v;
     const int64_t* ix;
+    const int32_t* bnd;
 };
 
-__device__ __forceinline__ Msg msg_at(const char* msgs, int64_t msg_ld, int64_t kpad, int slot) {
+// message layout (mx_choco_msg_bytes): vals f32[kpad] | idx int64[k] | bnd int32[ntiles + 1]
+__device__ __forceinline__ Msg msg_at(const char* msgs, int64_t msg_ld, int64_t kpad, int64_t k, int slot) {
     const char* b = msgs + (int64_t)slot * msg_ld;
-    return Msg{reinterpret_cast<const float*>(b), reinterpret_cast<const int64_t*>(b + 4 * kpad)};
-}
-
-// bnd[slot][t] = first entry of message `slot` with index >= t * kTile, for t in [0, ntiles];
-// only the slots this round uses (local rows + its received messages; others may hold stale
-// bytes -- the tile numbers are clamped anyway so nothing is written out of range)
-__device__ __forceinline__ int64_t tile_of(int64_t i, int64_t ntiles) {
-    const int64_t t = i < 0 ? -1 : i / kTile;
-    return t < ntiles ? t : ntiles;
+    return Msg{reinterpret_cast<const float*>(b), reinterpret_cast<const int64_t*>(b + 4 * kpad),
+               reinterpret_cast<const int32_t*>(b + 4 * kpad + 8 * k)};
 }
 
 // The plan record of this round: `rec` itself, or with iter_dev (graph-replayable launches) the
@@ -592,30 +588,10 @@ __device__ __forceinline__ const int32_t* round_rec(const int32_t* rec, const in
     return r[0] ? r : nullptr;
 }
 
-__global__ __launch_bounds__(kTPB) void bounds_kernel(const char* __restrict__ msgs, int64_t msg_ld,
-                                                      int64_t kpad, int64_t k, int64_t ntiles,
-                                                      const int32_t* __restrict__ rec_in,
-                                                      const int64_t* __restrict__ iter_dev, int64_t n_iters,
-                                                      int64_t words, int n_local,
-                                                      int32_t* __restrict__ bnd) {
-    const int32_t* rec = round_rec(rec_in, iter_dev, n_iters, words);
-    if (!rec) return;
-    const int slot = blockIdx.y;
-    if (slot >= n_local + rec[1]) return;
-    const Msg m = msg_at(msgs, msg_ld, kpad, slot);
-    int32_t* b = bnd + (int64_t)slot * (ntiles + 1);
-    for (int64_t q = (int64_t)blockIdx.x * kTPB + threadIdx.x; q <= k; q += (int64_t)gridDim.x * kTPB) {
-        const int64_t prev = q == 0 ? -1 : tile_of(m.ix[q - 1], ntiles);
-        const int64_t cur = q == k ? ntiles : tile_of(m.ix[q], ntiles);
-        for (int64_t t = prev + 1; t <= cur; ++t) b[t] = (int32_t)q;
-    }
-}
-
 __global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, float* __restrict__ xh,
                                                      float* __restrict__ s, int64_t ld, int64_t P,
                                                      const char* __restrict__ msgs, int64_t msg_ld,
-                                                     int64_t kpad, int64_t ntiles,
-                                                     const int32_t* __restrict__ bnd,
+                                                     int64_t kpad, int64_t k,
                                                      const int32_t* __restrict__ rec_in,
                                                      const int64_t* __restrict__ iter_dev, int64_t n_iters,
                                                      int64_t words, int n_local, int M,
@@ -655,10 +631,8 @@ __global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, floa
     const int d = deg[r];
     const int32_t* src = deg + 2 * n_local + r * M;
     for (int e = 0; e < d; ++e) {              // partners, ascending matching order
-        const int slot = src[e];
-        const Msg m = msg_at(msgs, msg_ld, kpad, slot);
-        const int32_t* b = bnd + (int64_t)slot * (ntiles + 1);
-        const int lo = b[t], hi = b[t + 1];
+        const Msg m = msg_at(msgs, msg_ld, kpad, k, src[e]);
+        const int lo = m.bnd[t], hi = m.bnd[t + 1];
         for (int q = lo + tid; q < hi; q += kTPB) {
             const int c = (int)(m.ix[q] - t0);
             ls[c] = __fadd_rn(ls[c], __fmul_rn(alpha, m.v[q]));
@@ -668,9 +642,8 @@ __global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, floa
     }
     {                                          // own message
         const float sw = __int_as_float(deg[n_local + r]);
-        const Msg m = msg_at(msgs, msg_ld, kpad, r);
-        const int32_t* b = bnd + (int64_t)r * (ntiles + 1);
-        const int lo = b[t], hi = b[t + 1];
+        const Msg m = msg_at(msgs, msg_ld, kpad, k, r);
+        const int lo = m.bnd[t], hi = m.bnd[t + 1];
         for (int q = lo + tid; q < hi; q += kTPB) {
             const int c = (int)(m.ix[q] - t0);
             const float vq = m.v[q];
@@ -728,7 +701,10 @@ int64_t sample_stride(int64_t P) {
 
 extern "C" size_t mx_topk_work_bytes(int64_t P) { return layout(P < 1 ? 1 : P).total; }
 
-extern "C" int64_t mx_choco_msg_bytes(int64_t k) { return 4 * ((k + 1) / 2 * 2) + 8 * k; }
+extern "C" int64_t mx_choco_msg_bytes(int64_t P, int64_t k) {
+    if (P < 1 || k < 1) return 0;
+    return 4 * ((k + 1) / 2 * 2) + 8 * k + 4 * (n_chunks(P) + 1);
+}
 
 extern "C" int mx_topk_set(const char* key, int64_t value) {
     MX_CHECK(key, "mx_topk_set: null key");
@@ -766,18 +742,21 @@ extern "C" int64_t mx_topk_get(const char* key) {
 
 extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t ld, int nrows, int64_t P,
                                      int64_t k, void* out, int64_t out_ld_bytes, int64_t idx_off_bytes,
-                                     void* work, int64_t work_ld_bytes, void* stream) {
+                                     int64_t bnd_off_bytes, void* work, int64_t work_ld_bytes, void* stream) {
     MX_CHECK(x && out && work, "mx_topk_abs_diff_rows: null pointer");
     MX_CHECK(P >= 1 && k >= 1 && k <= P && nrows >= 1 && nrows <= 65535 && (nrows == 1 || ld >= P),
              "mx_topk_abs_diff_rows: P=%lld k=%lld nrows=%d ld=%lld", (long long)P, (long long)k, nrows, (long long)ld);
     MX_CHECK(((uintptr_t)(static_cast<char*>(out) + idx_off_bytes)) % 8 == 0 && (nrows == 1 || out_ld_bytes % 8 == 0),
              "mx_topk_abs_diff_rows: int64 index output must be 8-byte aligned");
+    MX_CHECK(bnd_off_bytes < 0 || (((uintptr_t)(static_cast<char*>(out) + bnd_off_bytes)) % 4 == 0 &&
+                                   (nrows == 1 || out_ld_bytes % 4 == 0) && k < (int64_t)1 << 31),
+             "mx_topk_abs_diff_rows: tile bounds must be 4-byte aligned (and k < 2^31)");
     MX_CHECK(work_ld_bytes >= (int64_t)layout(P).total || nrows == 1, "mx_topk_abs_diff_rows: work_ld too small");
     MX_CHECK(((uintptr_t)work) % 256 == 0 && (nrows == 1 || work_ld_bytes % 256 == 0),
              "mx_topk_abs_diff_rows: work must be 256-byte aligned");
     hipStream_t st = mx::as_stream(stream);
     Rows R{x, x_hat, ld, static_cast<char*>(out), out_ld_bytes, idx_off_bytes, static_cast<char*>(work),
-           work_ld_bytes, P, k};
+           work_ld_bytes, P, k, bnd_off_bytes};
     const int64_t nc = n_chunks(P);
     const int64_t S = sample_stride(P);
     const int64_t nsamp = (n_subs(P) + S - 1) / S;
@@ -792,21 +771,16 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
     const unsigned wgrid = (unsigned)((nc + kWaves - 1) / kWaves);          // one wave per chunk
     const unsigned sgrid = clamp_grid(nsamp, (int64_t)g_sample_pieces * kWaves, (1024 + nrows - 1) / nrows);
     const unsigned cgrid = clamp_grid(nc, (int64_t)g_cand_chunks * kWaves, (2048 + nrows - 1) / nrows);
-    const dim3 one(1, nrows);
 #define MX_L(kern, grid, tpb, ...)                                                 \
     hipLaunchKernelGGL(kern, grid, dim3(tpb), 0, st, R, ##__VA_ARGS__);            \
     MX_LAUNCH_CHECK()
-    MX_L(zero_hist, one, kTPB);
     MX_L(sample_kernel, dim3(sgrid, nrows), kTPB, S);
     MX_L(compact_kernel, dim3(bgrid, nrows), kTPB, S, frac, 0);
-    if (S > 1) {
-        MX_L(count_kernel, one, kScanTPB);
-        MX_L(compact_kernel, dim3(bgrid, nrows), kTPB, S, frac, 1);
-    }
+    if (S > 1) MX_L(compact_kernel, dim3(bgrid, nrows), kTPB, S, frac, 1);
     MX_L(cand_hist<kMidBits>, dim3(cgrid, nrows), kTPB);
     MX_L(cand_hist<kLowBits>, dim3(cgrid, nrows), kTPB);
     MX_L(cand_mark, dim3(cgrid, nrows), kTPB);
-    MX_L(scan_kernel, one, kScanTPB);
+    MX_L(scan_kernel, dim3(1, nrows), kScanTPB);
     MX_L(write_cand, dim3(wgrid, nrows), kTPB);
 #undef MX_L
     return MX_OK;
@@ -816,12 +790,11 @@ extern "C" int mx_topk_abs_diff(const float* x, const float* x_hat, int64_t P, i
                                 int64_t* idx, void* work, void* stream) {
     MX_CHECK(vals && idx, "mx_topk_abs_diff: null pointer");
     const int64_t idx_off = reinterpret_cast<char*>(idx) - reinterpret_cast<char*>(vals);
-    return mx_topk_abs_diff_rows(x, x_hat, P, 1, P, k, vals, 0, idx_off, work, 0, stream);
+    return mx_topk_abs_diff_rows(x, x_hat, P, 1, P, k, vals, 0, idx_off, -1, work, 0, stream);
 }
 
-extern "C" size_t mx_choco_apply_work_bytes(int64_t P, int n_slots) {
-    return sizeof(int32_t) * (size_t)(n_tiles(P < 1 ? 1 : P) + 1) * (size_t)(n_slots < 1 ? 1 : n_slots);
-}
+// The tile bounds travel inside the messages; mx_choco_apply needs no scratch (kept in the ABI).
+extern "C" size_t mx_choco_apply_work_bytes(int64_t, int) { return 0; }
 
 namespace {
 int choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t k, const void* msgs,
@@ -851,27 +824,23 @@ namespace {
 int choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t k, const void* msgs,
                 int64_t msg_ld_bytes, int n_slots, const int32_t* plan_dev, int64_t iter, const int64_t* iter_dev,
                 int n_local, int M, float alpha, float gamma, void* work, void* stream) {
-    MX_CHECK(x && xhat && s && msgs && plan_dev && work, "mx_choco_apply: null pointer");
+    (void)work;
+    MX_CHECK(x && xhat && s && msgs && plan_dev, "mx_choco_apply: null pointer");
     MX_CHECK(P >= 1 && k >= 1 && k <= P && ld >= P && k < (int64_t)1 << 31, "mx_choco_apply: P=%lld k=%lld ld=%lld",
              (long long)P, (long long)k, (long long)ld);
     MX_CHECK(n_local >= 1 && n_local <= 65535 && n_slots >= n_local && n_slots <= 65535 && M >= 1,
              "mx_choco_apply: n_local=%d n_slots=%d M=%d", n_local, n_slots, M);
     const int64_t kpad = (k + 1) / 2 * 2;
-    MX_CHECK(msg_ld_bytes >= 4 * kpad + 8 * k && msg_ld_bytes % 8 == 0, "mx_choco_apply: msg_ld %lld",
+    MX_CHECK(msg_ld_bytes >= mx_choco_msg_bytes(P, k) && msg_ld_bytes % 8 == 0, "mx_choco_apply: msg_ld %lld",
              (long long)msg_ld_bytes);
     hipStream_t st = mx::as_stream(stream);
     const int64_t words = mx::plan_words(n_local, M);
     const int32_t* rec = iter_dev ? plan_dev : plan_dev + iter * words;   // with iter_dev: iter = n_iters
     const int64_t nt = n_tiles(P);
-    int32_t* bnd = static_cast<int32_t*>(work);
     const char* m = static_cast<const char*>(msgs);
-    hipLaunchKernelGGL(bounds_kernel, dim3(clamp_grid(k + 1, kTPB * 4, 1024), n_slots), dim3(kTPB), 0, st, m,
-                       msg_ld_bytes, kpad, k, nt, rec, iter_dev, iter, words, n_local, bnd);
-    MX_LAUNCH_CHECK();
     MX_CHECK(nt <= 0x7fffffff, "mx_choco_apply: P too large");
     hipLaunchKernelGGL(apply_kernel, dim3((unsigned)nt, n_local), dim3(kTPB), 0, st, x, xhat, s, ld, P, m,
-                       msg_ld_bytes, kpad, nt, (const int32_t*)bnd, rec, iter_dev, iter, words, n_local, M, alpha,
-                       gamma);
+                       msg_ld_bytes, kpad, k, rec, iter_dev, iter, words, n_local, M, alpha, gamma);
     MX_LAUNCH_CHECK();
     return MX_OK;
 }

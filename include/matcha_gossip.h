@@ -147,7 +147,9 @@ int mx_scatter(float* const* ptrs_dev, const int64_t* off_dev, int nseg, int64_t
  * Writes vals[k] = (x - x_hat)[idx] and idx[k] (int64) sorted by index.  Among equal
  * magnitudes at the k-th threshold the lowest indices are taken (torch.topk(sorted=False)
  * leaves that unspecified).  x_hat may be NULL (treated as zeros: get_top_k on x itself).
- * `work` is a 256-byte aligned device scratch of mx_topk_work_bytes(P) bytes.
+ * `work` is a 256-byte aligned device scratch of mx_topk_work_bytes(P) bytes, ZERO-FILLED before
+ * its first use (hipMemset); every call leaves its histograms and counters zero again, so no
+ * zeroing launch runs per call.  One scratch may serve calls of any P.
  * One full pass over x / x_hat: a sampled top-digit histogram picks a candidate floor, one
  * streaming pass keeps the keys above it, and the exact radix select runs on those only (a
  * too-high floor is detected on the device and the pass re-run keeping every key: the result
@@ -166,10 +168,12 @@ int mx_topk_abs_diff(const float* x, const float* x_hat, int64_t P, int64_t k, f
 /* Batched form (one set of launches for every local worker): row r reads x + r*ld (and
  * x_hat + r*ld), writes its values at out + r*out_ld_bytes and its int64 indices at
  * out + r*out_ld_bytes + idx_off_bytes, and uses work + r*work_ld_bytes
- * (work_ld_bytes >= mx_topk_work_bytes(P)). */
+ * (work_ld_bytes >= mx_topk_work_bytes(P)).  bnd_off_bytes >= 0: also writes the message's
+ * int32 tile bounds there (bnd[t] = first output entry with index >= 4096 t, t = 0..ceil(P/4096);
+ * the layout mx_choco_apply reads); < 0: not written. */
 int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t ld, int nrows, int64_t P,
                           int64_t k, void* out, int64_t out_ld_bytes, int64_t idx_off_bytes,
-                          void* work, int64_t work_ld_bytes, void* stream);
+                          int64_t bnd_off_bytes, void* work, int64_t work_ld_bytes, void* stream);
 
 /* ChocoCommunicator.averaging (communicator.py:200-230) for one round of n_local workers,
  * in place on the state rows (a round whose flags are all zero must not be applied):
@@ -177,16 +181,18 @@ int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t ld, int nr
  *   s_r[idx_r] += f32(1-d*alpha) * v_r ; x_hat_r[idx_r] += v_r
  *   x_r = fma(gamma, s_r, x_r) ; x_r = fma(-gamma, x_hat_r, x_r)
  *   x/xhat/s  float [n_local][P] rows with stride ld (floats)
- *   msgs      compressed messages, one per plan slot, msg_ld_bytes apart: slot k holds
- *             vals float[k] at +0 and idx int64[k] at +4*round_up(k, 2) (mx_choco_msg_bytes);
- *             slots [0, n_local) are the local rows' own messages, the rest received ones
- *   work      device scratch of mx_choco_apply_work_bytes(P, n_slots) bytes
+ *   msgs      compressed messages, one per plan slot, msg_ld_bytes apart: a slot holds
+ *             vals float[k] at +0, idx int64[k] at +4*round_up(k, 2) and the tile bounds int32
+ *             [ceil(P/4096) + 1] right after the indices (mx_choco_msg_bytes(P, k) bytes, written
+ *             by mx_topk_abs_diff_rows with bnd_off_bytes = 4*round_up(k, 2) + 8*k); slots
+ *             [0, n_local) are the local rows' own messages, the rest received ones
+ *   work      unused (the tile bounds travel in the messages); may be NULL
  * One fused pass: per 4096-element tile of a row, s and x_hat are staged in LDS, every message
  * entry in the tile is applied there in the order above, x is updated, and only the touched
  * 64-byte granules of s / x_hat are written back.
  */
-int64_t mx_choco_msg_bytes(int64_t k);
-/* Scratch of mx_choco_apply (per-tile ranges of every message slot). */
+int64_t mx_choco_msg_bytes(int64_t P, int64_t k);
+/* Scratch of mx_choco_apply: 0 bytes (kept for ABI stability). */
 size_t mx_choco_apply_work_bytes(int64_t P, int n_slots);
 int mx_choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t k,
                    const void* msgs, int64_t msg_ld_bytes, int n_slots, const int32_t* plan_dev,

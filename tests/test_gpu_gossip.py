@@ -270,6 +270,49 @@ def test_topk_sampled_floor_exact(pkg, O, stride, pieces, blocks, pattern):
     assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32))
 
 
+def test_topk_work_reuse_and_tile_bounds(pkg, O):
+    """One zero-filled scratch serves a sequence of calls of different P / k / patterns (incl. the
+    fallback pass): each call leaves its histograms and counters zero (no zeroing launch runs),
+    results stay exact, and the tile bounds the message carries are the index-range starts of
+    every 4096-element tile (what mx_choco_apply reads)."""
+    L = pkg.lib
+    big = max(int(L.mx_topk_work_bytes(P)) for P in (2_000_001, 4097, 300_000))
+    work = torch.zeros(big, dtype=torch.uint8, device="cuda")
+    hist_bytes = 4 * (3 * 4096 + 1024 + 512)
+    pkg._lib.check(L.mx_topk_set(b"sample_stride", 16))      # sampled_large then needs the fallback pass
+    try:
+        _reuse_calls(pkg, O, work, hist_bytes)
+    finally:
+        L.mx_topk_set(b"sample_stride", 0)
+
+
+def _reuse_calls(pkg, O, work, hist_bytes):
+    L = pkg.lib
+    for P, ratio, pattern in [(2_000_001, 0.99, "sampled_large"), (4097, 0.5, "ties"), (300_000, 0.9, "layers"),
+                              (2_000_001, 0.99, "constant"), (2_000_001, 0.99, "sampled_large")]:
+        x = _topk_case(O, P, pattern)
+        k = O.topk_k(P, ratio)
+        ov, oi = O.topk_abs(x, k)
+        kpad = (k + 1) // 2 * 2
+        nb = int(L.mx_choco_msg_bytes(P, k))
+        out = torch.zeros(nb, dtype=torch.uint8, device="cuda")
+        xd = torch.from_numpy(x).cuda()
+        pkg._lib.check(L.mx_topk_abs_diff_rows(xd.data_ptr(), None, P, 1, P, k, out.data_ptr(), 0, 4 * kpad,
+                                               4 * kpad + 8 * k, work.data_ptr(), 0, None), "topk rows")
+        torch.cuda.synchronize()
+        o = out.cpu().numpy()
+        assert np.array_equal(o[:4 * k].view(np.float32).view(np.uint32), ov.view(np.uint32)), (P, pattern)
+        idx = o[4 * kpad:4 * kpad + 8 * k].view(np.int64)
+        assert np.array_equal(idx, oi), (P, pattern)
+        nt = (P + 4095) // 4096
+        bnd = o[4 * kpad + 8 * k:nb].view(np.int32)
+        assert np.array_equal(bnd, np.searchsorted(oi, np.arange(nt + 1) * 4096).astype(np.int32)), (P, pattern)
+        w = work.cpu().numpy()
+        assert not w[:hist_bytes].any(), "histograms not re-zeroed"
+        state = w[hist_bytes:hist_bytes + 24].view(np.uint64)     # b0|T, need, cand_n
+        assert state[2] == 0, "candidate total not reset"
+
+
 # ------------------------------------------------------------------------------------ helpers
 def test_flatten_unflatten_scatter(pkg):
     ts = [torch.randn(s, device="cuda") for s in ((3, 5), (7,), (0,), (64, 33), (1,))]
