@@ -22,14 +22,15 @@
 //      prefix resolved so far; every block of a pass re-resolves the previous histograms itself
 //      (find_bin, read-only), so no one-block select launches sit between the passes;
 //      cand_mark resolves the exact threshold key T and the number of its ties to take, and
-//      counts > T / == T per chunk; scan_kernel turns them into output offsets (a kernel boundary,
-//      not a last-block tail: a device-scope fence per block writes back and invalidates the XCD's
-//      L2 and measured slower); write_cand emits the selected candidates in index order
+//      counts > T / == T per chunk and per block (contiguous chunk ranges); write_cand places each
+//      chunk's output from those (block totals before it + a few chunk counts, no scan launch;
+//      a last-block scan tail was tried and dropped: the device-scope fence every block then needs
+//      writes back and invalidates the XCD's L2) and emits the selected candidates in index order
 //      (values = x - x_hat, int64 indices) and, optionally, the message's per-4096-element tile
 //      bounds that mx_choco_apply reads (the output offset of every chunk), and re-zeroes the
 //      histograms / counters for the next call.
 // Everything stays on the device; no host round trip.  All local workers' rows are processed by
-// the same launches (blockIdx.y = row): 7 launches per call for any number of rows (8 with the
+// the same launches (blockIdx.y = row): 6 launches per call for any number of rows (7 with the
 // fallback pass that sampling needs).
 //
 // Work invariant: the histograms and the candidate total are zero on entry (the
@@ -44,7 +45,6 @@ constexpr int kSubQuads = kSub / 4;
 constexpr int kChunk = kWaves * kSub;        // elements per chunk = one block (candidate region)
 constexpr int kTopBits = 12, kTopShift = 19;
 constexpr int kTopBins = 1 << kTopBits;
-constexpr int kScanTPB = 1024;
 constexpr int kMidBits = 10, kMidShift = 9;  // bits 9..18
 constexpr int kLowBits = 9;                  // bits 0..8
 constexpr int64_t kSampleTarget = 1 << 18;   // sampled elements per row (auto stride)
@@ -102,7 +102,7 @@ struct RowView {
     uint32_t* h9;         // last 9 bits
     SelState* st;
     int64_t* cnt;
-    int64_t* off;
+    int64_t* bt;          // cand_mark block totals (keys > T, keys == T)
     float* cval;
     uint16_t* cloc;
     float* vals;
@@ -123,7 +123,7 @@ __device__ __forceinline__ RowView row_view(const Rows& R) {
     v.h9 = v.h10 + (1 << kMidBits);
     v.st = reinterpret_cast<SelState*>(wb + w.state);
     v.cnt = reinterpret_cast<int64_t*>(wb + w.cnt);
-    v.off = reinterpret_cast<int64_t*>(wb + w.off);
+    v.bt = reinterpret_cast<int64_t*>(wb + w.off);
     v.cval = reinterpret_cast<float*>(wb + w.cval);
     v.cloc = reinterpret_cast<uint16_t*>(wb + w.cloc);
     v.vals = reinterpret_cast<float*>(R.out + (int64_t)r * R.out_ld);
@@ -215,51 +215,64 @@ __global__ __launch_bounds__(kTPB) void sample_kernel(Rows R, int64_t S) {
 // Block-wide: the bin holding the need-th largest key of a finished histogram, scanning bins from
 // the top; *rem = rank of that key inside its bin.  bin 0 / rem = need - total when the histogram
 // holds fewer than `need` keys.  Read-only (every block of a kernel resolves the same answer),
-// so no separate one-block select launch sits between the passes.
+// so no separate one-block select launch sits between the passes.  Each thread loads its kPer
+// bins once (vector loads, kept in registers: the boundary search walks registers, not dependent
+// global loads), wave scans by shuffles, one barrier to combine the waves, one to publish.
 template <int NBINS>
 __device__ void find_bin(const uint32_t* __restrict__ hist, int64_t need, int* bin, int64_t* rem,
                          int64_t* total) {
     constexpr int kPer = NBINS / kTPB;
-    __shared__ int64_t part[kTPB];
+    __shared__ int64_t wsum[kWaves];
     __shared__ int s_bin;
-    __shared__ int64_t s_rem, s_total;
-    const int t = threadIdx.x;
+    __shared__ int64_t s_rem;
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+    uint32_t cnt[kPer];                                  // bins NBINS-1-(t*kPer+j), top first
     int64_t mine = 0;
-    for (int j = 0; j < kPer; ++j) mine += hist[NBINS - 1 - (t * kPer + j)];
-    part[t] = mine;
-    if (t == 0) {
-        s_bin = 0;
-        s_rem = need;
+#pragma unroll
+    for (int j = 0; j < kPer; ++j) {
+        cnt[j] = hist[NBINS - 1 - (t * kPer + j)];
+        mine += cnt[j];
     }
+    int64_t incl = mine;                                 // inclusive scan over the wave
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t x = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += x;
+    }
+    if (lane == 63) wsum[wave] = incl;
     __syncthreads();
-    for (int off = 1; off < kTPB; off <<= 1) {          // inclusive scan from the top bins down
-        const int64_t x = t >= off ? part[t - off] : 0;
-        __syncthreads();
-        part[t] += x;
-        __syncthreads();
+    int64_t base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+        base += w < wave ? wsum[w] : 0;
+        tot += wsum[w];
     }
-    const int64_t before = part[t] - mine;
-    if (t == kTPB - 1) {
-        s_total = part[t];
-        if (part[t] < need) s_rem = need - part[t];
-    }
-    if (before < need && part[t] >= need) {
+    incl += base;
+    const int64_t before = incl - mine;
+    if (tot >= need && before < need && incl >= need) {  // exactly one thread holds the boundary
         int64_t acc = before;
+        int b = -1;
+        int64_t r = 0;
+#pragma unroll
         for (int j = 0; j < kPer; ++j) {
-            const int b = NBINS - 1 - (t * kPer + j);
-            const int64_t c = hist[b];
-            if (acc + c >= need) {
-                s_bin = b;
-                s_rem = need - acc;
-                break;
+            if (b < 0 && acc + cnt[j] >= need) {
+                b = NBINS - 1 - (t * kPer + j);
+                r = need - acc;
             }
-            acc += c;
+            acc += cnt[j];
         }
+        s_bin = b;
+        s_rem = r;
     }
     __syncthreads();
-    *bin = s_bin;
-    *rem = s_rem;
-    *total = s_total;
+    *total = tot;
+    if (tot < need || need <= 0) {
+        *bin = 0;
+        *rem = need <= 0 ? need : need - tot;
+    } else {
+        *bin = s_bin;
+        *rem = s_rem;
+    }
     __syncthreads();                                     // the shared answer may be reused
 }
 
@@ -303,24 +316,9 @@ __device__ Resolved resolve(const RowView& v, int64_t k, int stages) {
 // fallback = 1: runs only if fewer than k candidates were kept, then keeps every key.
 __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double frac, int fallback) {
     const RowView v = row_view(R);
-    uint32_t b_lo = 0;
-    if (fallback) {
-        if (v.st->cand_n >= (unsigned long long)R.k) return;
-    } else {
-        int64_t want = R.k;
-        if (S > 1) {
-            const double e = (double)R.k * frac;
-            want = (int64_t)ceil(1.25 * e + 4.0 * sqrt(e) + 16.0);
-        }
-        int b;
-        int64_t rem, tot;
-        find_bin<kTopBins>(v.hs, want, &b, &rem, &tot);
-        b_lo = tot < want ? 0u : (uint32_t)b;               // too few sampled keys: keep everything
-        if (blockIdx.x == 0 && threadIdx.x == 0) v.st->b0 = b_lo;
-    }
+    if (fallback && v.st->cand_n >= (unsigned long long)R.k) return;
     __shared__ uint32_t wtot[2][kWaves];
     __shared__ uint32_t h[kTopBins];
-    for (int i = threadIdx.x; i < kTopBins; i += kTPB) h[i] = 0;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t nc = n_chunks(R.P);
     const bool vec = (((uintptr_t)v.x | (uintptr_t)v.xh) & 15) == 0;
@@ -337,8 +335,22 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double
         }
     };
     int64_t c = blockIdx.x;
+    if (c < nc && whole(c)) issue(c);              // the first chunk flies while b_lo is resolved
+    uint32_t b_lo = 0;
+    if (!fallback) {
+        int64_t want = R.k;
+        if (S > 1) {
+            const double e = (double)R.k * frac;
+            want = (int64_t)ceil(1.25 * e + 4.0 * sqrt(e) + 16.0);
+        }
+        int b;
+        int64_t rem, tot;
+        find_bin<kTopBins>(v.hs, want, &b, &rem, &tot);
+        b_lo = tot < want ? 0u : (uint32_t)b;               // too few sampled keys: keep everything
+        if (blockIdx.x == 0 && threadIdx.x == 0) v.st->b0 = b_lo;
+    }
+    for (int i = threadIdx.x; i < kTopBins; i += kTPB) h[i] = 0;
     uint32_t kept = 0;                             // this block's candidates (thread 0)
-    if (c < nc && whole(c)) issue(c);
     __syncthreads();                               // h zeroed
     for (int par = 0; c < nc; c += gridDim.x, par ^= 1) {
         float d[4][4];
@@ -438,7 +450,10 @@ __global__ __launch_bounds__(kTPB) void cand_hist(Rows R) {
 
 // the exact threshold key T and how many of its ties to take; per chunk region (one wave each)
 // the counts of candidates > T and == T, written without atomics
-__global__ __launch_bounds__(kTPB) void cand_mark(Rows R) {
+// Block j owns the contiguous chunks [j*G, (j+1)*G) and also writes its totals to bt[2j], bt[2j+1],
+// so write_cand can place any chunk's output from <= gridDim.x block totals plus < G chunk counts
+// (no separate scan launch).
+__global__ __launch_bounds__(kTPB) void cand_mark(Rows R, int64_t G) {
     const RowView v = row_view(R);
     const Resolved z = resolve(v, R.k, 3);
     const uint32_t T = z.prefix;
@@ -446,9 +461,12 @@ __global__ __launch_bounds__(kTPB) void cand_mark(Rows R) {
         v.st->T = T;
         v.st->need = z.need;
     }
+    __shared__ uint32_t sg[kWaves], se[kWaves];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t nchunks = n_chunks(R.P);
-    for (int64_t c = (int64_t)blockIdx.x * kWaves + wave; c < nchunks; c += (int64_t)gridDim.x * kWaves) {
+    const int64_t c0 = (int64_t)blockIdx.x * G, c1 = c0 + G < nchunks ? c0 + G : nchunks;
+    uint32_t wg = 0, we = 0;
+    for (int64_t c = c0 + wave; c < c1; c += kWaves) {
         const int64_t nc = v.cnt[4 * c + 3];
         uint32_t g = 0, e = 0;
         for (int64_t i = lane; i < nc; i += 64) {
@@ -458,55 +476,41 @@ __global__ __launch_bounds__(kTPB) void cand_mark(Rows R) {
         }
         g = wave_sum(g);
         e = wave_sum(e);
+        wg += g;
+        we += e;
         if (lane == 0) {
             v.cnt[4 * c + 1] = g;
             v.cnt[4 * c + 2] = e;
         }
     }
+    if (lane == 0) {
+        sg[wave] = wg;
+        se[wave] = we;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int64_t bg = 0, be = 0;
+        for (int w = 0; w < kWaves; ++w) {
+            bg += sg[w];
+            be += se[w];
+        }
+        v.bt[2 * blockIdx.x] = bg;
+        v.bt[2 * blockIdx.x + 1] = be;
+    }
 }
 
-// one block: per chunk the output offset and the global tie rank of its first tie
-__global__ __launch_bounds__(kScanTPB) void scan_kernel(Rows R) {
-    const RowView v = row_view(R);
-    const int64_t* cnt = v.cnt;
-    const int64_t nchunks = n_chunks(R.P);
-    const SelState* st = v.st;
-    int64_t* off = v.off;
-    __shared__ int64_t wsum_g[kScanTPB / 64], wsum_e[kScanTPB / 64];
-    __shared__ int64_t carry_g, carry_e;
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t need_eq = st->need;
-    if (threadIdx.x == 0) carry_g = carry_e = 0;
-    __syncthreads();
-    for (int64_t b0 = 0; b0 < nchunks; b0 += kScanTPB) {
-        const int64_t b = b0 + threadIdx.x;
-        const int64_t g = b < nchunks ? cnt[4 * b] + cnt[4 * b + 1] : 0;   // keys > T
-        const int64_t e = b < nchunks ? cnt[4 * b + 2] : 0;                // keys == T
-        int64_t sg = g, se = e;                                            // wave inclusive scan
-        for (int o = 1; o < 64; o <<= 1) {
-            const int64_t tg = __shfl_up(sg, o, 64), te = __shfl_up(se, o, 64);
-            if (lane >= o) { sg += tg; se += te; }
-        }
-        if (lane == 63) { wsum_g[wave] = sg; wsum_e[wave] = se; }
-        __syncthreads();
-        int64_t pg = carry_g, pe = carry_e;
-        for (int w = 0; w < wave; ++w) { pg += wsum_g[w]; pe += wsum_e[w]; }
-        if (b < nchunks) {
-            const int64_t gt_before = pg + sg - g, eq_before = pe + se - e;
-            off[2 * b] = gt_before + (eq_before < need_eq ? eq_before : need_eq);
-            off[2 * b + 1] = eq_before;
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            for (int w = 0; w < kScanTPB / 64; ++w) { carry_g += wsum_g[w]; carry_e += wsum_e[w]; }
-        }
-        __syncthreads();
-    }
+__device__ __forceinline__ int64_t wave_sum64(int64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
 }
 
 // ---- C: one wave per chunk region: the candidates are already in index order, so a wave scan
 // of the tie flags ranks the ties and a wave scan of the selection flags places the output.
-__global__ __launch_bounds__(kTPB) void write_cand(Rows R) {
+// The block's chunks start at c_first; keys > T and ties before it = the cand_mark block totals of
+// the blocks wholly before it (bt) + the chunk counts of its own cand_mark block before c_first,
+// summed by the whole block; each wave then adds the (< kWaves) chunks of this block before its own.
+__global__ __launch_bounds__(kTPB) void write_cand(Rows R, int64_t G) {
     const RowView v = row_view(R);
     const uint32_t T = v.st->T;
     const int64_t need_eq = v.st->need;
@@ -515,11 +519,41 @@ __global__ __launch_bounds__(kTPB) void write_cand(Rows R) {
         v.hs[i] = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) v.st->cand_n = 0;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t c = (int64_t)blockIdx.x * kWaves + wave;
+    const int64_t c_first = (int64_t)blockIdx.x * kWaves;
+    const int64_t J = c_first / G, nitems = J + (c_first - J * G);
+    int64_t g = 0, e = 0;
+    for (int64_t i = threadIdx.x; i < nitems; i += kTPB) {
+        if (i < J) {
+            g += v.bt[2 * i];
+            e += v.bt[2 * i + 1];
+        } else {
+            const int64_t cc = J * G + (i - J);
+            g += v.cnt[4 * cc + 1];
+            e += v.cnt[4 * cc + 2];
+        }
+    }
+    g = wave_sum64(g);
+    e = wave_sum64(e);
+    __shared__ int64_t rg[kWaves], re[kWaves];
+    if (lane == 0) {
+        rg[wave] = g;
+        re[wave] = e;
+    }
+    __syncthreads();
+    const int64_t c = c_first + wave;
     const int64_t nchunks = n_chunks(R.P);
     if (c >= nchunks) return;
+    int64_t gt = 0, eq = 0;
+    for (int w = 0; w < kWaves; ++w) {
+        gt += rg[w];
+        eq += re[w];
+    }
+    for (int64_t cc = c_first; cc < c; ++cc) {
+        gt += v.cnt[4 * cc + 1];
+        eq += v.cnt[4 * cc + 2];
+    }
     const int64_t nc = v.cnt[4 * c + 3];
-    int64_t run_out = v.off[2 * c], run_eq = v.off[2 * c + 1];
+    int64_t run_out = gt + (eq < need_eq ? eq : need_eq), run_eq = eq;
     if (R.bnd_off >= 0 && lane == 0) {             // chunk c is apply tile c: its first entry
         int32_t* bnd = reinterpret_cast<int32_t*>(R.out + (int64_t)blockIdx.y * R.out_ld + R.bnd_off);
         bnd[c] = (int32_t)run_out;
@@ -779,9 +813,9 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
     if (S > 1) MX_L(compact_kernel, dim3(bgrid, nrows), kTPB, S, frac, 1);
     MX_L(cand_hist<kMidBits>, dim3(cgrid, nrows), kTPB);
     MX_L(cand_hist<kLowBits>, dim3(cgrid, nrows), kTPB);
-    MX_L(cand_mark, dim3(cgrid, nrows), kTPB);
-    MX_L(scan_kernel, dim3(1, nrows), kScanTPB);
-    MX_L(write_cand, dim3(wgrid, nrows), kTPB);
+    const int64_t G = (nc + cgrid - 1) / cgrid;    // chunks per cand_mark block
+    MX_L(cand_mark, dim3(cgrid, nrows), kTPB, G);
+    MX_L(write_cand, dim3(wgrid, nrows), kTPB, G);
 #undef MX_L
     return MX_OK;
 }
