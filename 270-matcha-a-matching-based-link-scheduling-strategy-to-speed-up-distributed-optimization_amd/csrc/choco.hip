@@ -435,12 +435,23 @@ __global__ __launch_bounds__(kTPB) void cand_hist(Rows R) {
     __syncthreads();
     const int64_t nchunks = n_chunks(R.P);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int64_t c = (int64_t)blockIdx.x * kWaves + wave; c < nchunks; c += (int64_t)gridDim.x * kWaves) {
-        const int64_t nc = v.cnt[4 * c + 3];
-        for (int64_t i = lane; i < nc; i += 64) {
-            const uint32_t key = key_of(v.cval[c * kChunk + i]);
-            if ((key & z.mask) == z.prefix) atomicAdd(&h[(key >> shift) & (NB - 1)], 1u);
-        }
+    auto add = [&](float d) {
+        const uint32_t key = key_of(d);
+        if ((key & z.mask) == z.prefix) atomicAdd(&h[(key >> shift) & (NB - 1)], 1u);
+    };
+    // two chunk regions per step, their counts and first 64 candidates loaded together (the
+    // region is allocated whatever the count, lanes past it are ignored): one memory round trip
+    // instead of a count -> candidates chain per region -- this pass reads them cold
+    const int64_t stride = (int64_t)gridDim.x * kWaves;
+    for (int64_t c = (int64_t)blockIdx.x * kWaves + wave; c < nchunks; c += 2 * stride) {
+        const int64_t c2 = c + stride;
+        const bool two = c2 < nchunks;
+        const int64_t n1 = v.cnt[4 * c + 3], n2 = two ? v.cnt[4 * c2 + 3] : 0;
+        const float a1 = v.cval[c * kChunk + lane], a2 = two ? v.cval[c2 * kChunk + lane] : 0.0f;
+        if (lane < n1) add(a1);
+        for (int64_t i = 64 + lane; i < n1; i += 64) add(v.cval[c * kChunk + i]);
+        if (lane < n2) add(a2);
+        for (int64_t i = 64 + lane; i < n2; i += 64) add(v.cval[c2 * kChunk + i]);
     }
     __syncthreads();
     uint32_t* out = BITS == kMidBits ? v.h10 : v.h9;
@@ -466,10 +477,14 @@ __global__ __launch_bounds__(kTPB) void cand_mark(Rows R, int64_t G) {
     const int64_t nchunks = n_chunks(R.P);
     const int64_t c0 = (int64_t)blockIdx.x * G, c1 = c0 + G < nchunks ? c0 + G : nchunks;
     uint32_t wg = 0, we = 0;
-    for (int64_t c = c0 + wave; c < c1; c += kWaves) {
-        const int64_t nc = v.cnt[4 * c + 3];
+    auto count = [&](int64_t c, int64_t nc, float a) {     // a = candidate `lane` (speculative)
         uint32_t g = 0, e = 0;
-        for (int64_t i = lane; i < nc; i += 64) {
+        if (lane < nc) {
+            const uint32_t key = key_of(a);
+            g += key > T;
+            e += key == T;
+        }
+        for (int64_t i = 64 + lane; i < nc; i += 64) {
             const uint32_t key = key_of(v.cval[c * kChunk + i]);
             g += key > T;
             e += key == T;
@@ -482,6 +497,14 @@ __global__ __launch_bounds__(kTPB) void cand_mark(Rows R, int64_t G) {
             v.cnt[4 * c + 1] = g;
             v.cnt[4 * c + 2] = e;
         }
+    };
+    for (int64_t c = c0 + wave; c < c1; c += 2 * kWaves) {    // two regions per step (as cand_hist)
+        const int64_t c2 = c + kWaves;
+        const bool two = c2 < c1;
+        const int64_t n1 = v.cnt[4 * c + 3], n2 = two ? v.cnt[4 * c2 + 3] : 0;
+        const float a1 = v.cval[c * kChunk + lane], a2 = two ? v.cval[c2 * kChunk + lane] : 0.0f;
+        count(c, n1, a1);
+        if (two) count(c2, n2, a2);
     }
     if (lane == 0) {
         sg[wave] = wg;
@@ -520,6 +543,12 @@ __global__ __launch_bounds__(kTPB) void write_cand(Rows R, int64_t G) {
     if (blockIdx.x == 0 && threadIdx.x == 0) v.st->cand_n = 0;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t c_first = (int64_t)blockIdx.x * kWaves;
+    const int64_t c = c_first + wave;
+    const int64_t nchunks = n_chunks(R.P);
+    const bool live = c < nchunks;                 // this wave's region: count + first 64 candidates
+    const int64_t nc = live ? v.cnt[4 * c + 3] : 0;  // loaded up front (speculatively), in flight
+    const float a0 = live ? v.cval[c * kChunk + lane] : 0.0f;          // with the prefix loads
+    const uint32_t l0 = live ? v.cloc[c * kChunk + lane] : 0u;
     const int64_t J = c_first / G, nitems = J + (c_first - J * G);
     int64_t g = 0, e = 0;
     for (int64_t i = threadIdx.x; i < nitems; i += kTPB) {
@@ -540,9 +569,7 @@ __global__ __launch_bounds__(kTPB) void write_cand(Rows R, int64_t G) {
         re[wave] = e;
     }
     __syncthreads();
-    const int64_t c = c_first + wave;
-    const int64_t nchunks = n_chunks(R.P);
-    if (c >= nchunks) return;
+    if (!live) return;
     int64_t gt = 0, eq = 0;
     for (int w = 0; w < kWaves; ++w) {
         gt += rg[w];
@@ -552,7 +579,6 @@ __global__ __launch_bounds__(kTPB) void write_cand(Rows R, int64_t G) {
         gt += v.cnt[4 * cc + 1];
         eq += v.cnt[4 * cc + 2];
     }
-    const int64_t nc = v.cnt[4 * c + 3];
     int64_t run_out = gt + (eq < need_eq ? eq : need_eq), run_eq = eq;
     if (R.bnd_off >= 0 && lane == 0) {             // chunk c is apply tile c: its first entry
         int32_t* bnd = reinterpret_cast<int32_t*>(R.out + (int64_t)blockIdx.y * R.out_ld + R.bnd_off);
@@ -562,7 +588,7 @@ __global__ __launch_bounds__(kTPB) void write_cand(Rows R, int64_t G) {
     for (int64_t i0 = 0; i0 < nc; i0 += 64) {
         const int64_t i = i0 + lane;
         const bool in = i < nc;
-        const float d = in ? v.cval[c * kChunk + i] : 0.0f;
+        const float d = !in ? 0.0f : i0 == 0 ? a0 : v.cval[c * kChunk + i];
         const uint32_t key = key_of(d);
         const bool eq = in && key == T;
         const uint32_t einc = wave_incl_scan(eq ? 1u : 0u);
@@ -571,7 +597,7 @@ __global__ __launch_bounds__(kTPB) void write_cand(Rows R, int64_t G) {
         if (sel) {
             const int64_t pos = run_out + sinc - 1;
             v.vals[pos] = d;
-            v.idx[pos] = c * kChunk + v.cloc[c * kChunk + i];
+            v.idx[pos] = c * kChunk + (i0 == 0 ? l0 : v.cloc[c * kChunk + i]);
         }
         run_out += __shfl(sinc, 63, 64);
         run_eq += __shfl(einc, 63, 64);
