@@ -349,7 +349,9 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double
         b_lo = tot < want ? 0u : (uint32_t)b;               // too few sampled keys: keep everything
         if (blockIdx.x == 0 && threadIdx.x == 0) v.st->b0 = b_lo;
     }
-    for (int i = threadIdx.x; i < kTopBins; i += kTPB) h[i] = 0;
+    // only digits >= b_lo are ever counted: zero and flush just those bins (b_lo is near the top)
+    const int h0 = (int)(b_lo & ~(uint32_t)(kTPB - 1));
+    for (int i = h0 + threadIdx.x; i < kTopBins; i += kTPB) h[i] = 0;
     uint32_t kept = 0;                             // this block's candidates (thread 0)
     __syncthreads();                               // h zeroed
     for (int par = 0; c < nc; c += gridDim.x, par ^= 1) {
@@ -416,7 +418,7 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double
     }
     __syncthreads();
     uint32_t* out = fallback ? v.h12f : v.h12;
-    for (int i = threadIdx.x; i < kTopBins; i += kTPB)
+    for (int i = h0 + threadIdx.x; i < kTopBins; i += kTPB)
         if (h[i]) atomicAdd(&out[i], h[i]);
     if (!fallback && threadIdx.x == 0 && kept) atomicAdd(&v.st->cand_n, (unsigned long long)kept);
 }
