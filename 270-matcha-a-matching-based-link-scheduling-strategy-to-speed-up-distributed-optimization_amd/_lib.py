@@ -33,6 +33,7 @@ SIGNATURES = {
     "mx_gather": (c_int, [c_p, c_p, c_int, c_i64, c_p, c_p]),
     "mx_scatter": (c_int, [c_p, c_p, c_int, c_i64, c_p, c_p]),
     "mx_topk_work_bytes": (ctypes.c_size_t, [c_i64]),
+    "mx_iter_expand": (c_int, [c_p, c_p, c_int, c_p]),
     "mx_topk_set": (c_int, [ctypes.c_char_p, c_i64]),
     "mx_topk_get": (c_i64, [ctypes.c_char_p]),
     "mx_topk_abs_diff": (c_int, [c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p]),

@@ -804,6 +804,24 @@ __global__ void advance_kernel(int64_t* it, int64_t by) {
 }
 }  // namespace
 
+namespace {
+__global__ void expand_kernel(int64_t* it, int64_t* ctrs, int n) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const int64_t base = it[0];
+    for (int j = 0; j < n; ++j) ctrs[j] = base + j;
+    it[0] = base + n;
+}
+}  // namespace
+
+// K graph-replayable rounds for one launch of bookkeeping: ctrs[j] = *iter_dev + j, then
+// *iter_dev += n; the K mixing launches that follow read ctrs[0..K-1] (one counter each).
+extern "C" int mx_iter_expand(int64_t* iter_dev, int64_t* ctrs, int n, void* stream) {
+    MX_CHECK(iter_dev && ctrs && n >= 1, "mx_iter_expand: bad arguments");
+    hipLaunchKernelGGL(expand_kernel, dim3(1), dim3(64), 0, mx::as_stream(stream), iter_dev, ctrs, n);
+    MX_LAUNCH_CHECK();
+    return MX_OK;
+}
+
 extern "C" int mx_iter_advance(int64_t* iter_dev, int64_t by, void* stream) {
     MX_CHECK(iter_dev, "mx_iter_advance: null counter");
     hipLaunchKernelGGL(advance_kernel, dim3(1), dim3(64), 0, mx::as_stream(stream), iter_dev, by);

@@ -275,6 +275,24 @@ class GossipEngine:
                                    self.M, self.alpha32, s), "mx_gossip_mix_at")
         check(lib.mx_iter_advance(iter_dev.data_ptr(), 1, s), "mx_iter_advance")
 
+    def mix_rounds_at(self, iter_dev, ctrs, layout, stream=None):
+        """len(ctrs) graph-replayable rounds with one bookkeeping launch (mx_iter_expand: ctrs[j] =
+        *iter_dev + j, *iter_dev += K), then one mixing launch per round reading its own counter --
+        the same rounds as K mix_at calls, without the K counter bumps."""
+        if layout.tune_gen != _TUNE_GEN[0]:
+            if layout.tile != lib.mx_mix_tile(layout.n_slots):
+                raise MXError("layout built for another mixing tile size (the unroll knob changed it)")
+            layout.tune_gen = _TUNE_GEN[0]
+        for t in (iter_dev, ctrs):
+            if t.dtype != torch.int64 or t.device.type != "cuda" or not t.is_contiguous():
+                raise TypeError("iteration counters must be contiguous int64 CUDA tensors")
+        K = ctrs.numel()
+        s = stream_ptr(stream)
+        check(lib.mx_iter_expand(iter_dev.data_ptr(), ctrs.data_ptr(), K, s), "mx_iter_expand")
+        for j in range(K):
+            check(lib.mx_gossip_mix_at(*layout._args, self._plan_ptr, ctrs.data_ptr() + 8 * j, self.T,
+                                       self.n_local, self.M, self.alpha32, s), "mx_gossip_mix_at")
+
 
 def _params(model):
     return [p for p in model.parameters()]
@@ -311,6 +329,7 @@ class VirtualWorkerGroup:
         self.topology = topology
         self.iter = 0
         self.iter_dev = torch.zeros(1, dtype=torch.int64, device="cuda")   # device_round's counter
+        self._round_ctrs = {}                # device_rounds(K): per-round counters, one tensor per K
         if models is not None:
             if len(models) != self.n_local:
                 raise ValueError(f"{len(models)} models for {self.n_local} local workers")
@@ -415,6 +434,21 @@ class VirtualWorkerGroup:
         if self.chunked:
             raise MXError("device_round: not with chunk_cols")
         self.engine.mix_at(self.iter_dev, self.layout, stream)
+
+    def device_rounds(self, K, stream=None):
+        """K device_round()s in K + 1 launches instead of 2 K (for capture in one HIP graph): the
+        rounds at the counter `self.iter_dev` .. + K - 1, counter advanced by K."""
+        if self.engine.comm is not None:
+            raise MXError("device_rounds: graph-replayable rounds need all partners on this GPU (nranks = 1)")
+        if self.chunked:
+            raise MXError("device_rounds: not with chunk_cols")
+        K = int(K)
+        if K < 1:
+            raise ValueError("device_rounds: K >= 1")
+        ctrs = self._round_ctrs.get(K)
+        if ctrs is None:
+            ctrs = self._round_ctrs[K] = torch.zeros(K, dtype=torch.int64, device="cuda")
+        self.engine.mix_rounds_at(self.iter_dev, ctrs, self.layout, stream)
 
     def state_dict(self):
         """Checkpoint: the workers' rows and the iteration counter (resume on the same schedule)."""

@@ -129,6 +129,10 @@ int mx_gossip_mix_at(float* const* seg_ptrs_dev, const int64_t* seg_len_dev,
                      int64_t total_tiles, int n_slots, const int32_t* plan_dev, const int64_t* iter_dev,
                      int64_t n_iters, int n_local, int M, float alpha, void* stream);
 int mx_iter_advance(int64_t* iter_dev, int64_t by, void* stream);
+/* K rounds per replay with one bookkeeping launch: ctrs[j] = *iter_dev + j (j < n), then
+ * *iter_dev += n, all on the device; the n mx_gossip_mix_at launches captured after it read
+ * &ctrs[0] .. &ctrs[n-1].  Same rounds as n (mix_at + advance-by-1) pairs, half the launches. */
+int mx_iter_expand(int64_t* iter_dev, int64_t* ctrs, int n, void* stream);
 
 /* ---------------------------------------------------------------- flatten / unflatten
  * mx_gather replaces flatten_tensors (comm_helpers.py:12-30): flat[off[s] + i] = src[s][i].

@@ -127,6 +127,41 @@ def test_device_round_graph_replay(pkg, O, P, split):
         pkg.engine.set_mix_tuning(**saved)
 
 
+@pytest.mark.parametrize("K", [1, 5])
+def test_device_rounds_unrolled_graph(pkg, O, K):
+    """device_rounds(K) (one mx_iter_expand + K mx_gossip_mix_at launches) captured once: each
+    replay is the next K rounds of a MATCHA schedule, bit-exact vs the oracle, past the end no-ops,
+    and it mixes with device_round() on the same counter."""
+    n, T, P = 8, 13, 181_668
+    np.random.seed(91)
+    GP = pkg.MatchaProcessor(pkg.select_graph(0), 0.5, 0, n, T, True)
+    grp = pkg.VirtualWorkerGroup(GP, numel=P)
+    X = np.stack([O.synth(7000 + i, P) for i in range(n)])
+    grp.rows.copy_(torch.from_numpy(X))
+    partner = np.asarray(GP.neighbors_info, np.int32)
+    grp.iter_dev.fill_(0)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g):
+            grp.device_rounds(K)
+            grp.device_round()                       # K + 1 rounds per replay
+    torch.cuda.synchronize()
+    assert int(grp.iter_dev.item()) == 0 and np.array_equal(grp.rows.cpu().numpy(), X)
+    rows = len(GP.active_flags)
+    done = 0
+    while done < rows + K + 1:
+        g.replay()
+        for j in range(done, done + K + 1):
+            if j < rows:
+                X = O.decen_round(X, partner, np.asarray(GP.active_flags[j], np.uint8), GP.neighbor_weight)
+        done += K + 1
+        torch.cuda.synchronize()
+        assert np.array_equal(grp.rows.cpu().numpy().view(np.uint32), X.view(np.uint32)), f"after {done} rounds"
+    assert int(grp.iter_dev.item()) == done
+
+
 def test_cpu_inputs_staged_through_the_gpu(pkg, O):
     """The reference keeps models on the CPU (train_mpi.py:92 has .cuda() commented out):
     flatten_tensors / get_top_k take CPU tensors, compute on the GPU and answer on the CPU."""
