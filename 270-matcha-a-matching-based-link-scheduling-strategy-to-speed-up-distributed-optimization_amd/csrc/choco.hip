@@ -59,7 +59,7 @@ struct SelState {
 };
 
 struct WorkLayout {
-    size_t hist, state, cnt, off, cval, cloc, total;
+    size_t hist, state, cnt, bt, cval, cloc, total;
 };
 
 __host__ __device__ inline int64_t n_chunks(int64_t P) { return (P + kChunk - 1) / kChunk; }
@@ -71,8 +71,8 @@ __host__ __device__ inline WorkLayout layout(int64_t P) {
     w.hist = 0;
     w.state = w.hist + sizeof(uint32_t) * kHistWords;
     w.cnt = w.state + 64;
-    w.off = w.cnt + sizeof(int64_t) * 4 * (size_t)nc;
-    w.cval = (w.off + sizeof(int64_t) * 2 * (size_t)nc + 255) / 256 * 256;
+    w.bt = w.cnt + sizeof(int64_t) * 4 * (size_t)nc;              // cand_mark block totals (<= nc blocks)
+    w.cval = (w.bt + sizeof(int64_t) * 2 * (size_t)nc + 255) / 256 * 256;
     w.cloc = w.cval + sizeof(float) * (size_t)nc * kChunk;
     w.total = (w.cloc + sizeof(uint16_t) * (size_t)nc * kChunk + 255) / 256 * 256;
     return w;
@@ -123,7 +123,7 @@ __device__ __forceinline__ RowView row_view(const Rows& R) {
     v.h9 = v.h10 + (1 << kMidBits);
     v.st = reinterpret_cast<SelState*>(wb + w.state);
     v.cnt = reinterpret_cast<int64_t*>(wb + w.cnt);
-    v.bt = reinterpret_cast<int64_t*>(wb + w.off);
+    v.bt = reinterpret_cast<int64_t*>(wb + w.bt);
     v.cval = reinterpret_cast<float*>(wb + w.cval);
     v.cloc = reinterpret_cast<uint16_t*>(wb + w.cloc);
     v.vals = reinterpret_cast<float*>(R.out + (int64_t)r * R.out_ld);
