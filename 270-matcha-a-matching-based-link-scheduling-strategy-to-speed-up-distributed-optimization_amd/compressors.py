@@ -5,6 +5,19 @@ from ._lib import check, lib, stream_ptr
 from .choco import topk_count
 
 
+# device index -> persistent top-k scratch, zero-filled once (every call leaves it zeroed, so no
+# per-call fill of the ~6 P-byte buffer); calls are ordered on the current stream -- concurrent
+# get_top_k calls on different streams of one device would share it and are not supported
+_WORK = {}
+
+
+def _work(device, nbytes):
+    w = _WORK.get(device.index)
+    if w is None or w.numel() < nbytes:
+        w = _WORK[device.index] = torch.zeros(nbytes, dtype=torch.uint8, device=device)
+    return w
+
+
 def get_top_k(x, ratio):
     """Top (1 - ratio) fraction of x by magnitude: k = max(1, int(len * (1 - ratio))).
     Returns (x[indices], indices int64).  Indices come back in ascending order; among equal
@@ -22,7 +35,7 @@ def get_top_k(x, ratio):
     k = topk_count(P, ratio)
     vals = torch.empty(k, dtype=torch.float32, device=x_data.device)
     idx = torch.empty(k, dtype=torch.int64, device=x_data.device)
-    work = torch.zeros(int(lib.mx_topk_work_bytes(P)), dtype=torch.uint8, device=x_data.device)  # zero on first use
+    work = _work(x_data.device, int(lib.mx_topk_work_bytes(P)))
     check(lib.mx_topk_abs_diff(x_data.data_ptr(), None, P, k, vals.data_ptr(), idx.data_ptr(),
                                work.data_ptr(), stream_ptr()), "mx_topk_abs_diff")
     if host:
