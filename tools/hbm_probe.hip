@@ -243,6 +243,11 @@ int main() {
                 hipLaunchKernelGGL((k_read_rows<1>), dim3(g), dim3(256), 0, 0, A, Xh, ld4, ncc, 8, out);
             }));
         }
+        for (int g : {256, 512, 1024, 2048, 4096}) {   // one row (a VGG-16 worker per GPU): 118 MB
+            report("one_row", g, 1, 0, bytes / 8, time_ms([&] {
+                hipLaunchKernelGGL((k_read_rows<1>), dim3(g), dim3(256), 0, 0, A, Xh, ld4, ncc, 1, out);
+            }));
+        }
         (void)rowsc;
         return 0;
     }
