@@ -158,6 +158,132 @@ __global__ __launch_bounds__(256) void k_write(f4* __restrict__ d, int64_t n4) {
     }
 }
 
+// One-row Choco compaction pattern with its per-chunk work switched on piece by piece (MODE bits:
+// 1 LDS histogram atomics of kept keys, 2 the four wave scans, 4 the per-chunk barrier + cross-wave
+// offsets, 8 the candidate stores, 16 the stores staged through LDS and written from the first
+// lanes instead), same loop / prefetch structure as choco.hip's compact_kernel.
+__global__ void k_fill(float* x, int64_t n, uint32_t seed) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+        h ^= h >> 15; h *= 2246822519u; h ^= h >> 13; h *= 3266489917u; h ^= h >> 16;
+        x[i] = (float)(h >> 8) * (2.0f / 16777216.0f) - 1.0f;
+    }
+}
+
+__device__ __forceinline__ uint32_t p_scan(uint32_t v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t t = __shfl_up(v, o, 64);
+        if (lane >= o) v += t;
+    }
+    return v;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_compact_probe(const f4* __restrict__ x4, const f4* __restrict__ h4, int64_t nc,
+                                                       uint32_t b_lo, float* cval, uint16_t* cloc, int64_t* cnt) {
+    __shared__ uint32_t wtot[2][4];
+    __shared__ uint32_t h[4096];
+    __shared__ float sv[4][1024];                  // MODE 16: kept values / locations staged per wave
+    __shared__ uint16_t sl[4][1024];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int i = threadIdx.x; i < 4096; i += 256) h[i] = 0;
+    f4 ax[4], ah[4];
+    auto issue = [&](int64_t c) {
+        const int64_t q0 = c * 1024 + wave * 256 + lane;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            ax[j] = __builtin_nontemporal_load(x4 + q0 + j * 64);
+            ah[j] = __builtin_nontemporal_load(h4 + q0 + j * 64);
+        }
+    };
+    int64_t c = blockIdx.x;
+    if (c < nc) issue(c);
+    __syncthreads();
+    uint32_t sink = 0;
+    for (int par = 0; c < nc; c += gridDim.x, par ^= 1) {
+        float d[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) d[j][e] = __fsub_rn(ax[j][e], ah[j][e]);
+        const int64_t cn = c + gridDim.x;
+        if (cn < nc) issue(cn);
+        uint32_t keep = 0, incl[4], m[4], tot = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            m[j] = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t dg = (__float_as_uint(d[j][e]) & 0x7fffffffu) >> 19;
+                const bool f = dg >= b_lo;
+                keep |= (f ? 1u : 0u) << (4 * j + e);
+                m[j] += f;
+                if ((MODE & 1) && f) atomicAdd(&h[dg], 1u);
+            }
+            if (MODE & 2) {
+                incl[j] = p_scan(m[j]);
+                tot += __shfl(incl[j], 63, 64);
+            } else {
+                incl[j] = m[j];
+                tot += m[j];
+            }
+        }
+        uint32_t pos = 0;
+        if (MODE & 4) {
+            if (lane == 0) wtot[par][wave] = tot;
+            __syncthreads();
+            for (int w = 0; w < 4; ++w) pos += w < wave ? wtot[par][w] : 0;
+        }
+        if (MODE & 16) {                           // stage in LDS (wave-local positions), then
+            uint32_t q = 0;                        // contiguous stores from the first lanes
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint32_t p = q + incl[j] - m[j];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if ((keep >> (4 * j + e)) & 1u) {
+                        sv[wave][p] = d[j][e];
+                        sl[wave][p] = (uint16_t)(1024 * wave + 4 * (64 * j + lane) + e);
+                        ++p;
+                    }
+                }
+                q += __shfl(incl[j], 63, 64);
+            }
+            float* cv = cval + c * 4096 + pos;
+            uint16_t* cl = cloc + c * 4096 + pos;
+            for (uint32_t i = lane; i < tot; i += 64) {
+                cv[i & 4095] = sv[wave][i];
+                cl[i & 4095] = sl[wave][i];
+            }
+            if (threadIdx.x == 0) cnt[c] = tot;
+        } else if (MODE & 8) {
+            float* cv = cval + c * 4096;
+            uint16_t* cl = cloc + c * 4096;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint32_t p = pos + incl[j] - m[j];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if ((keep >> (4 * j + e)) & 1u) {
+                        cv[p & 4095] = d[j][e];
+                        cl[p & 4095] = (uint16_t)(1024 * wave + 4 * (64 * j + lane) + e);
+                        ++p;
+                    }
+                }
+                pos += (MODE & 2) ? __shfl(incl[j], 63, 64) : 0;
+            }
+            if (threadIdx.x == 0) cnt[c] = tot;
+        } else {
+            sink += keep + pos;
+        }
+    }
+    __syncthreads();
+    if ((MODE & 1) && h[threadIdx.x] == 12345u) cnt[0] = 1;
+    if (sink == 0xdeadbeefu) cnt[1] = 1;
+}
+
 template <typename F>
 static float time_ms(F launch, int reps = 30) {
     hipEvent_t a, b;
@@ -242,6 +368,24 @@ int main() {
             report("rows_flat", g, 1, 0, bytes, time_ms([&] {
                 hipLaunchKernelGGL((k_read_rows<1>), dim3(g), dim3(256), 0, 0, A, Xh, ld4, ncc, 8, out);
             }));
+        }
+        {   // the compaction's per-chunk work, piece by piece, one row (random x, x_hat = 0)
+            hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, (float*)A, Pc, 1234u);
+            CK(hipMemset(B, 0, Pc * 4));
+            float* cv;
+            uint16_t* cl;
+            int64_t* cn;
+            CK(hipMalloc(&cv, Pc * 4));
+            CK(hipMalloc(&cl, Pc * 2));
+            CK(hipMalloc(&cn, ncc * 8));
+            union { float f; uint32_t u; } t{0.9875f};
+            const uint32_t b_lo = (t.u & 0x7fffffffu) >> 19;
+#define CP(M)                                                                                             \
+    report("compact_mode" #M, 1024, 1, M, bytes / 8, time_ms([&] {                                    \
+        hipLaunchKernelGGL((k_compact_probe<M>), dim3(1024), dim3(256), 0, 0, A, Xh, ncc, b_lo, cv, cl, cn); \
+    }))
+            CP(0); CP(1); CP(2); CP(4); CP(8); CP(3); CP(7); CP(15); CP(14); CP(13); CP(11); CP(23);
+#undef CP
         }
         for (int g : {256, 512, 1024, 2048, 4096}) {   // one row (a VGG-16 worker per GPU): 118 MB
             report("one_row", g, 1, 0, bytes / 8, time_ms([&] {
