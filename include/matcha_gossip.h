@@ -162,7 +162,8 @@ int mx_scatter(float* const* ptrs_dev, const int64_t* off_dev, int nseg, int64_t
 size_t mx_topk_work_bytes(int64_t P);
 /* Top-k knobs: "sample_stride" = sample every S-th 1024-element chunk for the candidate floor
  * (0 = auto, about 2^18 sampled elements per row; 1 = exact full histogram, no sampling);
- * "compact_blocks" = persistent workgroups of the full pass, over all rows (default 1024);
+ * "compact_blocks" = persistent workgroups of the full pass, over all rows (0 = auto: 1024 for
+ * one row, 2048 for several);
  * "sample_pieces" = sampled 1024-element pieces per wave of the sampling pass (default 1);
  * "cand_chunks" = candidate regions per wave of the candidate-histogram / mark passes (default 2). */
 int mx_topk_set(const char* key, int64_t value);
