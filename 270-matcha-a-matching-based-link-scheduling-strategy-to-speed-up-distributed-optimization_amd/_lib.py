@@ -21,6 +21,7 @@ SIGNATURES = {
     "mx_flags_binomial_sequential": (c_int, [c_p, c_int, c_p, c_int, c_i64, c_p, c_p, c_p, c_p]),
     "mx_plan_words": (c_i64, [c_int, c_int]),
     "mx_plan_build": (c_int, [c_p, c_i64, c_int, c_p, c_int, c_p, c_int, c_int, c_int, c_f64, c_p, c_p]),
+    "mx_plan_set_idle": (c_int, [c_p, c_i64, c_int, c_int, c_int, c_p]),
     "mx_mix_tile": (c_int, [c_int]),
     "mx_mix_layout": (c_int, [c_p, c_int, c_int, c_p]),
     "mx_mix_set": (c_int, [ctypes.c_char_p, c_int]),

@@ -36,8 +36,9 @@ def flatten_tensors(tensors):
     if total:
         ptrs = torch.tensor([t.data_ptr() for t in src], dtype=torch.int64, device=flat.device)
         offd = torch.from_numpy(off).to(flat.device)
-        check(lib.mx_gather(ptrs.data_ptr(), offd.data_ptr(), len(src), total, flat.data_ptr(),
-                            stream_ptr()), "mx_gather")
+        with torch.cuda.device(flat.device):     # the stream of the tensors' own device
+            check(lib.mx_gather(ptrs.data_ptr(), offd.data_ptr(), len(src), total, flat.data_ptr(),
+                                stream_ptr()), "mx_gather")
     return flat
 
 
@@ -56,15 +57,16 @@ def scatter_tensors(flat, tensors):
     """reset_model's copy-back loop (communicator.py:124-131) as one mx_scatter launch."""
     tensors = list(tensors)
     for t in tensors:
-        if t.device.type != "cuda" or t.dtype != torch.float32 or not t.is_contiguous():
-            raise TypeError("scatter_tensors: contiguous float32 CUDA tensors required")
+        if t.device != flat.device or t.dtype != torch.float32 or not t.is_contiguous():
+            raise TypeError("scatter_tensors: contiguous float32 tensors on flat's CUDA device required")
     off = _offsets(tensors)
     total = int(off[-1])
     if total:
         ptrs = torch.tensor([t.data_ptr() for t in tensors], dtype=torch.int64, device=flat.device)
         offd = torch.from_numpy(off).to(flat.device)
-        check(lib.mx_scatter(ptrs.data_ptr(), offd.data_ptr(), len(tensors), total, flat.data_ptr(),
-                             stream_ptr()), "mx_scatter")
+        with torch.cuda.device(flat.device):
+            check(lib.mx_scatter(ptrs.data_ptr(), offd.data_ptr(), len(tensors), total, flat.data_ptr(),
+                                 stream_ptr()), "mx_scatter")
 
 
 def communicate(tensors, communication_op):

@@ -51,24 +51,57 @@ def _ensure_process_group(rank, size):
 
 
 class _Staging:
-    """Moves a model's parameters into / out of a group row (device or host models)."""
+    """Moves a model's parameters into / out of a group row.
 
-    def __init__(self, tensors, row):
-        self.tensors = tensors
+    GPU models are adopted: every parameter's storage is a view of the group row, so a round
+    mixes them in place and nothing is copied.  Host models (the reference's default) are staged:
+    copied to the row before and back after each round."""
+
+    def __init__(self, params, row):
+        self.params = params
         self.row = row
-        self.on_gpu = all(t.device.type == "cuda" for t in tensors)
+        self.on_gpu = all(p.device.type == "cuda" for p in params)
+
+    def adopted(self):
+        """True while every parameter still lives at its place in the row (a caller may have
+        reassigned p.data since, e.g. torch.nn.utils.vector_to_parameters or model.cpu())."""
+        base, off = self.row.data_ptr(), 0
+        for p in self.params:
+            if p.data.data_ptr() != base + 4 * off and p.numel():
+                return False
+            off += p.numel()
+        return True
+
+    def adopt(self):
+        """(Re-)home the parameters' current values into the row as views (identity kept)."""
+        off = 0
+        with torch.no_grad():
+            for p in self.params:
+                k = p.numel()
+                view = self.row[off:off + k].view(p.shape)
+                if p.data.data_ptr() != view.data_ptr():
+                    view.copy_(p.data)
+                    p.data = view
+                off += k
 
     def load(self):
-        if not self.on_gpu:
-            flat = torch.cat([t.reshape(-1) for t in self.tensors]) if len(self.tensors) > 1 \
-                else self.tensors[0].reshape(-1)
-            self.row.copy_(flat, non_blocking=False)
+        if self.on_gpu:
+            if not self.adopted():
+                self.on_gpu = all(p.device.type == "cuda" for p in self.params)
+                if self.on_gpu:
+                    self.adopt()
+            if self.on_gpu:
+                return
+        tensors = [p.data for p in self.params]
+        flat = torch.cat([t.reshape(-1) for t in tensors]) if len(tensors) > 1 else tensors[0].reshape(-1)
+        self.row.copy_(flat, non_blocking=False)
 
     def store(self):
         if not self.on_gpu:
             host = self.row.cpu()
+            tensors = [p.data for p in self.params]
             with torch.no_grad():
-                for f, t in zip(unflatten_tensors(host, self.tensors), self.tensors):
+                for f, t in zip(unflatten_tensors(host, tensors), tensors):
                     t.copy_(f)
 
 
@@ -100,8 +133,11 @@ class Communicator(object):
 class decenCommunicator(Communicator):
     """communicator.py:79-158 -- decentralized averaging according to the topology's schedule."""
 
-    def __init__(self, rank, size, topology, *, transport=None):
+    def __init__(self, rank, size, topology, *, transport=None, idle_rows="skip"):
+        """idle_rows="canonical": a round in which this worker has no active partner rewrites its
+        parameters as 0 + 1.0 * x, as the reference does (-0.0 -> +0.0); "skip" leaves them."""
         super(decenCommunicator, self).__init__(rank, size, transport=transport)
+        self.idle_rows = idle_rows
         self.topology = topology
         self.neighbor_weight = topology.neighbor_weight
         self.iter = 0
@@ -111,17 +147,16 @@ class decenCommunicator(Communicator):
 
     def _bind(self, model):
         params = [p for p in model.parameters()]
-        on_gpu = all(p.device.type == "cuda" for p in params)
-        comm = self._comm()
-        if on_gpu:
-            self._group = VirtualWorkerGroup(self.topology, [model], rank=self.rank, nranks=self.size,
-                                             comm=comm)
-            self._stage = _Staging([p.data for p in params], self._group.rows[0])
+        n = int(sum(p.numel() for p in params))
+        if self._group is not None and self._group.numel == n:
+            # same size (e.g. parameters re-created): adopt the new tensors into the same row
+            self._stage = _Staging(params, self._group.rows[0])
         else:
-            n = int(sum(p.numel() for p in params))
-            self._group = VirtualWorkerGroup(self.topology, numel=n, rank=self.rank, nranks=self.size,
-                                             comm=comm)
-            self._stage = _Staging([p.data for p in params], self._group.rows[0])
+            on_gpu = all(p.device.type == "cuda" for p in params)
+            self._group = VirtualWorkerGroup(self.topology, [model] if on_gpu else None,
+                                             numel=None if on_gpu else n, rank=self.rank,
+                                             nranks=self.size, comm=self._comm(), idle_rows=self.idle_rows)
+            self._stage = _Staging(params, self._group.rows[0])
         self._model_params = params
 
     def communicate(self, model):
@@ -132,8 +167,6 @@ class decenCommunicator(Communicator):
             return 0
         if self._group is None or not _same_params(model, self._model_params):
             self._bind(model)
-        else:
-            self._stage.tensors = [p.data for p in self._model_params]
         self._stage.load()
         torch.cuda.synchronize()
         tic = time.time()
@@ -168,18 +201,21 @@ class ChocoCommunicator(Communicator):
 
     def _bind(self, model):
         params = [p for p in model.parameters()]
-        on_gpu = all(p.device.type == "cuda" for p in params)
-        comm = self._comm()
-        if on_gpu:
-            self._group = ChocoWorkerGroup(self.topology, [model], ratio=self.ratio,
-                                           consensus_lr=self.consensus_lr, rank=self.rank,
-                                           nranks=self.size, comm=comm)
+        n = int(sum(p.numel() for p in params))
+        if self._group is not None:
+            # x_hat / s persist for the communicator's life (communicator.py:179-182): new parameter
+            # tensors of the same size are adopted into the same row, keeping the Choco state
+            if self._group.numel != n:
+                raise ValueError(f"ChocoCommunicator: the model now has {n} parameters, its x_hat / s "
+                                 f"hold {self._group.numel}")
+            self._stage = _Staging(params, self._group.rows[0])
         else:
-            n = int(sum(p.numel() for p in params))
-            self._group = ChocoWorkerGroup(self.topology, numel=n, ratio=self.ratio,
+            on_gpu = all(p.device.type == "cuda" for p in params)
+            self._group = ChocoWorkerGroup(self.topology, [model] if on_gpu else None,
+                                           numel=None if on_gpu else n, ratio=self.ratio,
                                            consensus_lr=self.consensus_lr, rank=self.rank,
-                                           nranks=self.size, comm=comm)
-        self._stage = _Staging([p.data for p in params], self._group.rows[0])
+                                           nranks=self.size, comm=self._comm())
+            self._stage = _Staging(params, self._group.rows[0])
         self._model_params = params
         self.initialized = True
 
@@ -191,8 +227,6 @@ class ChocoCommunicator(Communicator):
             return 0
         if self._group is None or not _same_params(model, self._model_params):
             self._bind(model)
-        else:
-            self._stage.tensors = [p.data for p in self._model_params]
         self._stage.load()
         torch.cuda.synchronize()
         tic = time.time()

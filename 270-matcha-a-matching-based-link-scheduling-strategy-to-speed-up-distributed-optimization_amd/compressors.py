@@ -36,8 +36,9 @@ def get_top_k(x, ratio):
     vals = torch.empty(k, dtype=torch.float32, device=x_data.device)
     idx = torch.empty(k, dtype=torch.int64, device=x_data.device)
     work = _work(x_data.device, int(lib.mx_topk_work_bytes(P)))
-    check(lib.mx_topk_abs_diff(x_data.data_ptr(), None, P, k, vals.data_ptr(), idx.data_ptr(),
-                               work.data_ptr(), stream_ptr()), "mx_topk_abs_diff")
+    with torch.cuda.device(x_data.device):   # launch on the stream of the tensor's own device
+        check(lib.mx_topk_abs_diff(x_data.data_ptr(), None, P, k, vals.data_ptr(), idx.data_ptr(),
+                                   work.data_ptr(), stream_ptr()), "mx_topk_abs_diff")
     if host:
         return vals.to(x.device), idx.to(x.device)
     return vals, idx

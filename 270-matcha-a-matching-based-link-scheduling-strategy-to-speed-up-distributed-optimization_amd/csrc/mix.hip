@@ -68,7 +68,9 @@ __device__ __forceinline__ void st1(float* p, float v) { *(GPtr<float>)(p) = v; 
 
 
 // Plan record of this iteration, decoded into LDS (see mx_plan_build); returns the bit mask of
-// slots that must be loaded, or 0 when every flag of the round is 0.
+// slots that must be loaded, or 0 when every flag of the round is 0.  Rows of degree 0 are left
+// untouched unless the record's idle word (mx_plan_set_idle) asks for the reference's
+// `0 + 1.0 * x` (then they are streamed like any other row, with selfweight 1).
 template <int NS>
 struct PlanLds {
     int32_t w[mx::kPlanHeader + 2 * NS + NS * kMaxM];
@@ -92,10 +94,11 @@ __device__ __forceinline__ uint64_t load_plan(PlanLds<NS>& sp, const int32_t* pl
     __syncthreads();
     if (sp.w[0] == 0) return 0;
     const int n_remote = sp.w[1];
+    const bool idle = sp.w[2] != 0;
     const int32_t* deg = sp.w + mx::kPlanHeader;
     uint64_t need = 0;
     for (int r = 0; r < n_local; ++r)
-        if (deg[r] > 0) need |= 1ull << r;
+        if (deg[r] > 0 || idle) need |= 1ull << r;
     for (int k = 0; k < n_remote; ++k) need |= 1ull << (n_local + k);
     return need;
 }
@@ -288,7 +291,7 @@ __global__ __launch_bounds__(kTPB) void mix_kernel(float* const* __restrict__ se
         }
 #pragma unroll
         for (int r = 0; r < NS; ++r) {
-            if (dg[r] == 0) continue;
+            if (r >= n_local || ((need >> r) & 1ull) == 0) continue;   // degree 0 unless idle rows are kept
             const float s = sw[r];
 #pragma unroll
             for (int u = 0; u < U; ++u) {
@@ -373,7 +376,7 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_reg(float* const* __restrict_
         const bool full = seg_vec[seg] && (g + (U - 1) * kTPB) * 4 + 4 <= lim;
         for (int r = 0; r < n_local; ++r) {
             const int d = deg[r];
-            if (d == 0) continue;
+            if (((need >> r) & 1ull) == 0) continue;
             F acc[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) acc[u] = F{0.0f, 0.0f, 0.0f, 0.0f};
@@ -495,7 +498,7 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict
     // deal the items (row r, pass q) = r * NQ + q to the waves: wave 0 ranks them by weight
     if (wave == 0) {
         const int r = lane / NQ;
-        const int w = (lane < NI && r < n_local && deg[r] > 0) ? deg[r] + 1 : 0;
+        const int w = (lane < NI && r < n_local && ((need >> r) & 1ull)) ? deg[r] + 1 : 0;
         int rank = 0;
         for (int j = 0; j < NI; ++j) {
             const int wj = __builtin_amdgcn_readlane(w, j);

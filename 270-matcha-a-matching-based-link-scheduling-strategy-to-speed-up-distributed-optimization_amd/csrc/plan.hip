@@ -55,7 +55,7 @@ __global__ __launch_bounds__(256) void plan_kernel(const uint8_t* __restrict__ f
     }
     rec[0] = any;
     rec[1] = remote;
-    rec[2] = 0;
+    rec[2] = 0;                                // idle rows skipped (mx_plan_set_idle)
     rec[3] = 0;
     for (int r = 0; r < n_local; ++r) {
         const double s = 1.0 - (double)deg[r] * alpha;  // Python float arithmetic, then f32
@@ -65,7 +65,24 @@ __global__ __launch_bounds__(256) void plan_kernel(const uint8_t* __restrict__ f
 }
 }  // namespace
 
+namespace {
+__global__ void idle_kernel(int32_t* __restrict__ plan, int64_t T, int64_t W, int32_t mode) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < T) plan[t * W + 2] = mode;
+}
+}  // namespace
+
 extern "C" int64_t mx_plan_words(int n_local, int M) { return mx::plan_words(n_local, M); }
+
+extern "C" int mx_plan_set_idle(int32_t* plan_dev, int64_t T, int n_local, int M, int mode, void* stream) {
+    MX_CHECK(plan_dev && T >= 0 && n_local >= 1 && M >= 1, "mx_plan_set_idle: bad arguments");
+    MX_CHECK(mode == 0 || mode == 1, "mx_plan_set_idle: mode %d", mode);
+    if (T == 0) return MX_OK;
+    hipLaunchKernelGGL(idle_kernel, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, mx::as_stream(stream),
+                       plan_dev, T, mx::plan_words(n_local, M), (int32_t)mode);
+    MX_LAUNCH_CHECK();
+    return MX_OK;
+}
 
 extern "C" int mx_plan_build(const uint8_t* flags_dev, int64_t T, int M, const int32_t* partner_dev,
                              int n_global, const int32_t* owner_dev, int my_rank, int row_base,

@@ -168,11 +168,22 @@ class Layout:
                       self.seg_vec.data_ptr(), nseg, self.total_tiles, n_slots)
 
 
-class GossipEngine:
-    """Schedule + plans for one block of workers of a FixedProcessor / MatchaProcessor."""
+IDLE_MODES = {"skip": 0, "canonical": 1}
 
-    def __init__(self, topology, row_base=0, n_local=None, comm=None, owner=None):
+
+class GossipEngine:
+    """Schedule + plans for one block of workers of a FixedProcessor / MatchaProcessor.
+
+    idle_rows -- workers with no active partner in an active round: "skip" (default; not read or
+    written) or "canonical" (rewritten as 0 + 1.0 * x like the reference's averaging, which turns
+    -0.0 into +0.0 -- bit-identical to the reference at the cost of streaming those rows;
+    mx_plan_set_idle)."""
+
+    def __init__(self, topology, row_base=0, n_local=None, comm=None, owner=None, idle_rows="skip"):
         require_device()
+        if idle_rows not in IDLE_MODES:
+            raise ValueError(f"idle_rows must be one of {sorted(IDLE_MODES)}")
+        self.idle_rows = idle_rows
         self.topology = topology
         self.n = int(topology.size)
         partner_all = np.asarray(topology.neighbors_info, dtype=np.int32).reshape(-1, self.n)
@@ -208,6 +219,9 @@ class GossipEngine:
         check(lib.mx_plan_build(self.flags_dev.data_ptr(), self.T, self.M, self.partner_dev.data_ptr(),
                                 self.n, None, self.rank, self.row_base, self.n_local, self.alpha,
                                 self.plan.data_ptr(), stream_ptr()), "mx_plan_build")
+        if IDLE_MODES[idle_rows]:
+            check(lib.mx_plan_set_idle(self.plan.data_ptr(), self.T, self.n_local, self.M, IDLE_MODES[idle_rows],
+                                       stream_ptr()), "mx_plan_set_idle")
         self.any_active = self.flags_host.any(axis=1).tolist()
         self._plan_ptr = self.plan.data_ptr()
 
@@ -311,10 +325,11 @@ class VirtualWorkerGroup:
                consecutive ids), "auto" (placement.best_placement: fewest rows over the busiest
                xGMI pair) or an explicit worker order.  `workers` lists the worker id of each
                local row (models are given in that order).
+    idle_rows -- "skip" (default) or "canonical": see GossipEngine.
     """
 
     def __init__(self, topology, models=None, numel=None, *, rank=0, nranks=1, comm=None, adopt=True,
-                 chunk_cols=None, placement=None):
+                 chunk_cols=None, placement=None, idle_rows="skip"):
         require_device()
         from .placement import block_workers, place
         n = int(topology.size)
@@ -325,7 +340,7 @@ class VirtualWorkerGroup:
         if nranks > 1 and comm is None:
             comm = default_comm()
         self.engine = GossipEngine(topology, self.row_base, self.n_local, comm=comm,
-                                   owner=owner_table(n, nranks))
+                                   owner=owner_table(n, nranks), idle_rows=idle_rows)
         self.topology = topology
         self.iter = 0
         self.iter_dev = torch.zeros(1, dtype=torch.int64, device="cuda")   # device_round's counter

@@ -422,7 +422,17 @@ class VirtualTrainer:
         for o, s in zip(self.optimizers, state["optimizers"]):
             o.load_state_dict(s)
         if self.batched:
-            self._mom = {k: v.clone() for k, v in state.get("momentum", {}).items()}
+            loaded = state.get("momentum", {})
+            if set(loaded) == set(self._mom) and all(self._mom[k].shape == v.shape for k, v in loaded.items()):
+                # captured graphs update these buffers at their captured addresses: load in place
+                with torch.no_grad():
+                    for k, v in loaded.items():
+                        self._mom[k].copy_(v)
+            else:
+                self._mom = {k: v.clone() for k, v in loaded.items()}
+                self._graphs = {}            # captured against the old buffers: recapture on next use
+        # the device-side round counter of graph replays restarts from the loaded host counter
+        self._dev_iter_synced = False
 
     def save(self, path):
         torch.save(self.state_dict(), path)

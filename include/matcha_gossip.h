@@ -63,7 +63,8 @@ int mx_flags_binomial_sequential(const uint32_t* key_in, int pos_in, const doubl
  *   partner_dev  int32 [M][n_global]   (GraphProcessor.neighbors_info, graph_manager.py:157-180)
  *   owner_dev    int32 [n_global]      rank owning each worker; NULL = all local
  *   plan_dev     int32 [T][mx_plan_words(n_local, M)]
- * Plan record layout (int32 words): [0] any flag set, [1] n_remote, [2..3] reserved,
+ * Plan record layout (int32 words): [0] any flag set, [1] n_remote, [2] idle-row mode
+ *   (mx_plan_set_idle; 0 after mx_plan_build), [3] reserved,
  *   [4, 4+n_local) degree, [4+n_local, 4+2n_local) selfweight (f32 bits),
  *   [4+2n_local + r*M + e] source slot of row r's e-th partner (slot < n_local: local row,
  *   slot >= n_local: receive slab row slot - n_local).
@@ -72,6 +73,15 @@ int64_t mx_plan_words(int n_local, int M);
 int mx_plan_build(const uint8_t* flags_dev, int64_t T, int M, const int32_t* partner_dev,
                   int n_global, const int32_t* owner_dev, int my_rank, int row_base,
                   int n_local, double alpha, int32_t* plan_dev, void* stream);
+
+/* Idle rows of an active round (degree 0 while some matching is active).  The reference still
+ * runs them through averaging: recv = zeros; recv.add_(x, alpha=1 - 0*alpha) (communicator.py:
+ * 113-117), i.e. x = 0 + 1.0 * x, which is x itself except that -0.0 becomes +0.0 (and a
+ * signalling NaN is quieted).  mode 0 (mx_plan_build's default): such rows are not touched -- no
+ * HBM traffic for them, equal to the reference under IEEE ==.  mode 1: they are streamed and
+ * rewritten as fma(1.0f, x, 0.0f), bit-identical to the reference.  Sets word [2] of every
+ * record of a plan table built by mx_plan_build. */
+int mx_plan_set_idle(int32_t* plan_dev, int64_t T, int n_local, int M, int mode, void* stream);
 
 /* ---------------------------------------------------------------- the hot path
  * One decentralized averaging round, in place, for every local worker:

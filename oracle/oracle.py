@@ -45,6 +45,8 @@ def lib():
                                       ctypes.c_int, ctypes.c_double]
         L.orc_topk_abs.argtypes = [_f32p, ctypes.c_int64, ctypes.c_int64, _f32p, _i64p]
         L.orc_topk_abs.restype = ctypes.c_int
+        L.orc_topk_abs_sort.argtypes = [_f32p, ctypes.c_int64, ctypes.c_int64, _f32p, _i64p]
+        L.orc_topk_abs_sort.restype = ctypes.c_int
         L.orc_choco_round.argtypes = [_f32p, _f32p, _f32p, ctypes.c_int, ctypes.c_int64, _i32p,
                                       _u8p, ctypes.c_int, ctypes.c_double, ctypes.c_int64,
                                       ctypes.c_double]
@@ -106,12 +108,14 @@ def topk_k(P, ratio):
     return max(1, int(P * (1 - ratio)))
 
 
-def topk_abs(x, k):
-    """compressors.get_top_k (compressors.py:3-19), index-sorted; ties -> lowest index."""
+def topk_abs(x, k, sort=False):
+    """compressors.get_top_k (compressors.py:3-19), index-sorted; ties -> lowest index.
+    sort=True: the full-sort statement of the same rule (cross-check; slow at large P)."""
     x = np.ascontiguousarray(x, dtype=np.float32)
     vals = np.empty(k, np.float32)
     idx = np.empty(k, np.int64)
-    rc = lib().orc_topk_abs(x, x.shape[0], k, vals, idx)
+    f = lib().orc_topk_abs_sort if sort else lib().orc_topk_abs
+    rc = f(x, x.shape[0], k, vals, idx)
     assert rc == 0, rc
     return vals, idx
 
@@ -163,7 +167,12 @@ def synth(seed, n):
 
 def synth_np(seed, n):
     """Same generator in numpy (cross-check of orc_synth)."""
-    i = np.arange(1, n + 1, dtype=np.uint64)
+    return synth_at(seed, np.arange(n, dtype=np.int64))
+
+
+def synth_at(seed, cols):
+    """synth(seed, n)[cols] without generating the whole row (the generator is counter-based)."""
+    i = np.asarray(cols, dtype=np.uint64) + np.uint64(1)
     with np.errstate(over="ignore"):
         z = np.uint64(seed) + i * np.uint64(0x9E3779B97F4A7C15)
         z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)

@@ -1,0 +1,155 @@
+"""GPU parity at every BASELINE.json config's own size (VERDICT r01 "configs_untested").
+
+Each case runs the product path (VirtualWorkerGroup / ChocoWorkerGroup over the HIP kernels) on
+the config's exact parameter count and compares, bit for bit (uint32 views), with the CPU oracle
+on the same seeded inputs:
+
+  config 1  MLP (models/MLP.py, 666,547 params) D-PSGD, FixedProcessor schedule, graph 0
+  config 2  the repo's CIFAR ResNet (ResNet(18,100), 181,668 params), MATCHA C_b = 0.5, graph 0
+  config 3  WRN-28-10 (36,546,980 params) MATCHA C_b = 0.5, graph 0, 3 rounds
+  config 4  VGG-16 (14,774,436 params) ChocoSGD top-1 % (ratio 0.99), gamma 0.1, 3 rounds with
+            parameter drift between rounds; x, x_hat and s all compared
+  config 5  64-worker Erdos-Renyi(0.1) topology, 1e9 params per worker (a 256 GB arena), MATCHA
+            C_b = 0.5, 2 rounds; 64 sampled columns of every worker checked (columns are
+            independent in a gossip round, so the oracle runs the round on those columns only)
+
+Reference: communicator.py:92-122 (decen averaging), 175-230 (Choco), graph_manager.py:208-225,
+298-309 (schedules).  Model sizes: SURVEY.md §2 row 10.
+"""
+import random
+
+import numpy as np
+import pytest
+
+from conftest import Topo
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+MLP_P, RESNET_P, WRN_P, VGG_P = 666_547, 181_668, 36_546_980, 14_774_436
+
+
+def _fill(pkg, grp, seed0):
+    for r in range(grp.n_local):
+        pkg._lib.check(pkg.lib.mx_synth_fill(grp.rows[r].data_ptr(), grp.numel, seed0 + grp.workers[r], None))
+
+
+def _u32(a):
+    return np.ascontiguousarray(a).view(np.uint32)
+
+
+@pytest.mark.parametrize("cfg", ["mlp_fixed", "resnet_matcha"])
+def test_small_configs_schedules(pkg, O, cfg):
+    """Configs 1 and 2: the processors' own schedules (Fixed: alternating matchings 0 / 1 after
+    the discarded draws; MATCHA: GPU flags from the solved p), 12 rounds incl. skipped ones."""
+    n, T = 8, 12
+    np.random.seed(1234)
+    if cfg == "mlp_fixed":
+        GP = pkg.FixedProcessor(pkg.select_graph(0), 0.5, 0, n, T, True)
+        P = MLP_P
+    else:
+        GP = pkg.MatchaProcessor(pkg.select_graph(0), 0.5, 0, n, T, True)
+        P = RESNET_P
+    grp = pkg.VirtualWorkerGroup(GP, numel=P)
+    _fill(pkg, grp, 77)
+    X = np.stack([O.synth(77 + i, P) for i in range(n)])
+    partner = np.asarray(GP.neighbors_info, np.int32)
+    flags = np.asarray(GP.active_flags, np.uint8)
+    for it in range(T):
+        grp.communicate()
+        if flags[it].any():
+            X = O.decen_round(X, partner[:flags.shape[1]], flags[it], GP.neighbor_weight)
+    assert np.array_equal(_u32(grp.rows.cpu().numpy()), _u32(X))
+
+
+def test_wrn_config_full_size(pkg, O):
+    """Config 3 on one GPU: 8 workers x 36,546,980 params, MatchaProcessor C_b = 0.5 on graph 0
+    (solver p, GPU flags), the first 3 rounds of its schedule, uint32-exact after every round."""
+    n, P = 8, WRN_P
+    np.random.seed(1234)
+    GP = pkg.MatchaProcessor(pkg.select_graph(0), 0.5, 0, n, 8, True)
+    torch.cuda.empty_cache()
+    grp = pkg.VirtualWorkerGroup(GP, numel=P)
+    _fill(pkg, grp, 1234)
+    X = np.stack([O.synth(1234 + i, P) for i in range(n)])
+    partner = np.asarray(GP.neighbors_info, np.int32)
+    flags = np.asarray(GP.active_flags, np.uint8)
+    assert flags[:3].any(axis=1).all(), "the schedule's first rounds are expected to be active"
+    for it in range(3):
+        grp.communicate()
+        X = O.decen_round(X, partner, flags[it], GP.neighbor_weight)
+        assert np.array_equal(_u32(grp.rows.cpu().numpy()), _u32(X)), f"round {it}"
+    del grp
+    torch.cuda.empty_cache()
+
+
+def test_vgg_choco_config_full_size(pkg, O):
+    """Config 4's gossip on one GPU: 8 workers x 14,774,436 params, ratio 0.99 (k = 147,744),
+    consensus_lr 0.1, a full round then two partial ones, parameter drift between rounds (the
+    optimizer step of train_mpi.py:134); x, x_hat and s uint32-exact after every round."""
+    n, P, ratio, gamma = 8, VGG_P, 0.99, 0.1
+    gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, n, 4, True)
+    flags = np.array([[1, 1, 1, 1, 1], [1, 0, 1, 1, 0], [0, 1, 1, 0, 1]], np.uint8)
+    topo = Topo(gp.neighbors_info, 2 / 7, flags)
+    torch.cuda.empty_cache()
+    grp = pkg.ChocoWorkerGroup(topo, numel=P, ratio=ratio, consensus_lr=gamma)
+    k = O.topk_k(P, ratio)
+    assert grp.k == k == 147_744
+    _fill(pkg, grp, 500)
+    X = np.stack([O.synth(500 + i, P) for i in range(n)])
+    XH, S = np.zeros_like(X), np.zeros_like(X)
+    for t, f in enumerate(flags):
+        if t:
+            D = np.stack([np.float32(0.01) * O.synth(9000 + 31 * t + i, P) for i in range(n)])
+            X += D
+            grp.rows.add_(torch.from_numpy(D).cuda())
+            del D
+        grp.communicate()
+        O.choco_round(X, XH, S, topo.neighbors_info, f, 2 / 7, k, gamma)
+        assert np.array_equal(_u32(grp.rows.cpu().numpy()), _u32(X)), f"x, round {t}"
+        assert np.array_equal(_u32(grp.x_hat[:, :P].cpu().numpy()), _u32(XH)), f"x_hat, round {t}"
+        assert np.array_equal(_u32(grp.s[:, :P].cpu().numpy()), _u32(S)), f"s, round {t}"
+    del grp
+    torch.cuda.empty_cache()
+
+
+def test_er64_config_large(pkg, O):
+    """Config 5 on one GPU: ER(64, 0.1, seed 1234) decomposed on the host, 64 workers x 1e9
+    params (256 GB resident; smaller only if the device has less free memory), MatchaProcessor
+    C_b = 0.5 on that decomposition, 2 rounds.  Before each round 64 columns spread over the row
+    are snapshotted; the oracle runs the round on the snapshot and the GPU's columns must match
+    bit for bit (a gossip round mixes each column independently)."""
+    n, seed = 64, 1234
+    random.seed(0)
+    base = pkg.erdos_renyi(n, 0.1, seed)
+    np.random.seed(seed)
+    GP = pkg.MatchaProcessor(base, 0.5, 0, n, 4, False)
+    torch.cuda.empty_cache()
+    free, _ = torch.cuda.mem_get_info()
+    P = 1_000_000_000
+    while n * P * 4 > free - (6 << 30):            # leave room for the engine and the snapshots
+        P //= 2
+    grp = pkg.VirtualWorkerGroup(GP, numel=P)
+    _fill(pkg, grp, 1234)
+    cols_h = np.linspace(0, P - 1, 64).astype(np.int64)
+    cols_h[1] = 1023                               # a 1024-column tile edge
+    cols = torch.from_numpy(cols_h).cuda()
+    snap = grp.rows.index_select(1, cols).cpu().numpy()
+    assert np.array_equal(snap, np.stack([O.synth_at(1234 + i, cols_h) for i in range(n)]))   # the fill
+    partner = np.asarray(GP.neighbors_info, np.int32)
+    flags = np.asarray(GP.active_flags, np.uint8)
+    active = 0
+    for it in range(4):                            # until 2 active rounds (skipped ones checked too)
+        grp.communicate()
+        want = (O.decen_round(np.ascontiguousarray(snap), partner, flags[it], GP.neighbor_weight)
+                if flags[it].any() else snap)
+        snap = grp.rows.index_select(1, cols).cpu().numpy()
+        assert np.array_equal(_u32(snap), _u32(want)), f"round {it} (P = {P})"
+        active += int(flags[it].any())
+        if active == 2:
+            break
+    assert active == 2
+    # the last column and a sub-tile edge are in the sample: the row's tail is exercised
+    assert int(cols[-1]) == P - 1
+    del grp
+    torch.cuda.empty_cache()

@@ -146,3 +146,28 @@ def test_graph_mode_identical_to_batched(pkg, momentum, nesterov, matcha, compre
         assert [s["train_acc"] for s in se] == [s["train_acc"] for s in sg]
     assert eag.group.iter == gra.group.iter == 12
     assert len(gra._graphs) == 1
+
+
+@pytest.mark.parametrize("compress", [False, True])
+def test_graph_mode_checkpoint_reload(pkg, compress):
+    """Loading a checkpoint into a graph-mode trainer whose graphs are already captured: the
+    replays continue from the loaded iteration counter and momentum (loaded in place into the
+    captured buffers), so the next epoch equals the eager batched trainer's from the same state."""
+    H = pkg.harness
+    args = _args(pkg, momentum=0.9, epoch=4, lr=0.05, compress=compress, ratio=0.9, budget=0.5)
+    eag = H.VirtualTrainer(args, H.model_factory(args), n_batches=3, batched=True)
+    gra = H.VirtualTrainer(args, H.model_factory(args), n_batches=3, batched=True, graph=True)
+    for _ in range(2):
+        eag.train_epoch()
+        gra.train_epoch()
+    ckpt = {k: v for k, v in gra.state_dict().items()}
+    gra.train_epoch()                       # moves iter / momentum / rows past the checkpoint
+    gra.load_state_dict(ckpt)
+    assert gra.group.iter == 6 and gra.epoch == 2
+    se = eag.train_epoch()
+    sg = gra.train_epoch()
+    assert torch.equal(eag.group.rows, gra.group.rows)
+    if compress:
+        assert torch.equal(eag.group.x_hat, gra.group.x_hat) and torch.equal(eag.group.s, gra.group.s)
+    assert [s["loss"] for s in se] == [s["loss"] for s in sg]
+    assert len(gra._graphs) == 1            # reused, not recaptured

@@ -109,3 +109,27 @@ def test_baseline_port_matches_round(O):
         X = O.decen_round(X, partner, f, 2 / 7)
     got = np.stack([np.concatenate(s) for s in segs])
     assert np.array_equal(got, X)
+
+
+@pytest.mark.parametrize("P,k,pattern", [(1, 1, "rand"), (10_007, 100, "rand"), (10_007, 10_007, "rand"),
+                                         (50_000, 4_999, "ties"), (50_000, 777, "const"), (65_536, 655, "zeros"),
+                                         (200_003, 2_000, "signed_zero")])
+def test_topk_select_equals_sort(O, P, k, pattern):
+    """The O(P) quickselect top-k equals the full-sort statement of the rule (|x| descending,
+    lowest index first among equal magnitudes) on random data and on heavy ties."""
+    x = O.synth(P + 17, P)
+    if pattern == "ties":
+        x[::3] = np.float32(0.75)
+        x[1::5] = np.float32(-0.75)
+    elif pattern == "const":
+        x[:] = np.float32(-0.5)
+    elif pattern == "zeros":
+        x[:] = 0
+        x[::97] = np.float32(1e-30)
+    elif pattern == "signed_zero":
+        x[::2] = np.float32(-0.0)
+        x[1::4] = np.float32(0.0)
+    v1, i1 = O.topk_abs(x, k)
+    v2, i2 = O.topk_abs(x, k, sort=True)
+    assert np.array_equal(i1, i2)
+    assert np.array_equal(v1.view(np.uint32), v2.view(np.uint32))
