@@ -53,6 +53,9 @@ SIGNATURES = {
     "mx_exchange_round": (c_int, [c_p, c_p, c_int, c_p, c_int, c_p, c_int, c_int, c_int, c_p, c_p, c_i64,
                                   c_i64, c_p, c_p]),
     "mx_allreduce_mean": (c_int, [c_p, c_p, c_i64, c_int, c_p]),
+    "mx_allreduce_mean_ordered": (c_int, [c_p, c_p, c_i64, c_p, c_int, c_p]),
+    "mx_allgather": (c_int, [c_p, c_p, c_i64, c_p, c_p]),
+    "mx_mean_rows": (c_int, [c_p, c_int, c_i64, c_i64, c_int, c_p, c_p]),
     "mx_synth_fill": (c_int, [c_p, c_i64, c_u64, c_p]),
 }
 

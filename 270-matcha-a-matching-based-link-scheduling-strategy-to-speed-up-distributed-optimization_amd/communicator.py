@@ -237,11 +237,51 @@ class ChocoCommunicator(Communicator):
         return toc - tic
 
 
-class centralizedCommunicator(Communicator):
-    """communicator.py:46-76 -- all-reduce averaging: x = allreduce_sum(x) / size (RCCL)."""
+ORDERS = {"tree": 0, "sequential": 1}
 
-    def __init__(self, rank, size, *, transport=None):
+
+class centralizedCommunicator(Communicator):
+    """communicator.py:46-76 -- all-reduce averaging: x = allreduce_sum(x) / size.
+
+    order -- how the ranks' vectors are summed:
+      "tree" (default): bit-identical to the reference's comm.allreduce(obj, op=MPI.SUM) under
+          mpi4py's default object reduction (a binomial tree to rank 0, then a broadcast):
+          every vector is all-gathered over RCCL and each rank sums them in that order on its GPU
+          (mx_allreduce_mean_ordered / mx_mean_rows) before the division of communicator.py:62;
+      "sequential": the same with a rank-order left fold (mpi4py with rc.fast_reduce off);
+      "ring": RCCL's own all-reduce + division (mx_allreduce_mean) -- less traffic per rank, equal
+          to the reference within fp32 reassociation only."""
+
+    def __init__(self, rank, size, *, transport=None, order="tree"):
         super(centralizedCommunicator, self).__init__(rank, size, transport=transport)
+        if order not in ORDERS and order != "ring":
+            raise ValueError(f"order must be 'tree', 'sequential' or 'ring', not {order!r}")
+        self.order = order
+        self._gather = None
+
+    def _gather_buf(self, count, device):
+        if self._gather is None or self._gather.numel() < self.size * count or self._gather.device != device:
+            self._gather = torch.empty(self.size * count, dtype=torch.float32, device=device)
+        return self._gather
+
+    def _average(self, flat):
+        comm = self._comm()
+        count = flat.numel()
+        if self.order == "ring":
+            if hasattr(comm, "allreduce_mean"):
+                comm.allreduce_mean(flat, self.size)
+            else:
+                check(lib.mx_allreduce_mean(comm.handle, flat.data_ptr(), count, self.size, stream_ptr()),
+                      "mx_allreduce_mean")
+            return
+        gather = self._gather_buf(count, flat.device)
+        if hasattr(comm, "allgather"):          # a test transport: gathers, then the same kernel
+            comm.allgather(flat, gather[:self.size * count])
+            check(lib.mx_mean_rows(gather.data_ptr(), self.size, count, count, ORDERS[self.order],
+                                   flat.data_ptr(), stream_ptr()), "mx_mean_rows")
+        else:
+            check(lib.mx_allreduce_mean_ordered(comm.handle, flat.data_ptr(), count, gather.data_ptr(),
+                                                ORDERS[self.order], stream_ptr()), "mx_allreduce_mean_ordered")
 
     def communicate(self, model):
         tensors = [p.data for p in model.parameters()]
@@ -249,13 +289,8 @@ class centralizedCommunicator(Communicator):
         flat = flatten_tensors([t if on_gpu else t.cuda() for t in tensors])
         torch.cuda.synchronize()
         tic = time.time()
-        if self.size > 1:
-            comm = self._comm()
-            if hasattr(comm, "allreduce_mean"):
-                comm.allreduce_mean(flat, self.size)
-            else:
-                check(lib.mx_allreduce_mean(comm.handle, flat.data_ptr(), flat.numel(), self.size,
-                                            stream_ptr()), "mx_allreduce_mean")
+        if self.size > 1 and flat.numel():
+            self._average(flat)
         torch.cuda.synchronize()
         toc = time.time()
         with torch.no_grad():

@@ -108,10 +108,13 @@ extern "C" int mx_exchange_post(void* comm_v, const int32_t* ops, int n_ops, voi
     MX_CHECK(comm_v && (ops || n_ops == 0) && n_ops >= 0, "mx_exchange_post: bad arguments");
     MX_CHECK(row_bytes > 0 && row_bytes % 4 == 0, "mx_exchange_post: row_bytes %lld", (long long)row_bytes);
     if (n_ops == 0) return MX_OK;
+    int nranks = 0;
+    MX_NCCL(ncclCommCount(reinterpret_cast<ncclComm_t>(comm_v), &nranks));
     for (int i = 0; i < n_ops; ++i) {                     // validate everything before posting
         const int32_t* o = ops + 4 * i;
         MX_CHECK(o[0] == 0 || o[0] == 1, "mx_exchange_post: op %d kind %d", i, o[0]);
-        MX_CHECK(o[1] >= 0, "mx_exchange_post: op %d peer %d", i, o[1]);
+        MX_CHECK(o[1] >= 0 && o[1] < nranks, "mx_exchange_post: op %d peer %d outside the communicator's %d ranks",
+                 i, o[1], nranks);
         if (o[0] == 0)
             MX_CHECK(rows && o[2] >= 0 && o[2] < n_rows && rows[o[2]], "mx_exchange_post: op %d row %d of %d", i,
                      o[2], n_rows);
@@ -166,6 +169,43 @@ __global__ void div_kernel(float* __restrict__ x, int64_t n, float d) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         x[i] = x[i] / d;
 }
+
+// out[i] = (sum of rows[0..nrows)[i] in the reference's order) / nrows, fp32 adds, one rounding
+// each (no contraction: -ffp-contract=off), then one correctly rounded division -- the
+// centralizedCommunicator's comm.allreduce(obj, MPI.SUM) + div_(size) (communicator.py:61-62):
+//   TREE = 1  mpi4py's default object all-reduce (rc.fast_reduce): a binomial-tree reduction to
+//             rank 0 -- at mask 1, 2, 4, ... rank r (a multiple of 2 * mask) adds the partial
+//             sum of rank r + mask -- then a broadcast: ((x0 + x1) + (x2 + x3)) + ((x4 + x5) + ...)
+//   TREE = 0  rank order ((x0 + x1) + x2) + ... (mpi4py with fast_reduce off: allgather, then
+//             functools-style left fold)
+// MAXR bounds nrows; the tree runs over a register array with compile-time indices.
+template <int TREE, int MAXR>
+__global__ __launch_bounds__(256) void mean_rows_kernel(const float* rows, int nrows, int64_t ld,
+                                                        int64_t count, float size, float* out) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x) {
+        float acc;
+        if (TREE) {
+            float v[MAXR];
+#pragma unroll
+            for (int r = 0; r < MAXR; ++r) v[r] = r < nrows ? rows[r * ld + i] : 0.0f;
+#pragma unroll
+            for (int m = 1; m < MAXR; m <<= 1)
+#pragma unroll
+                for (int r = 0; r + m < MAXR; r += 2 * m)
+                    if (r + m < nrows) v[r] = v[r] + v[r + m];
+            acc = v[0];
+        } else {
+            acc = rows[i];
+            for (int r = 1; r < nrows; ++r) acc = acc + rows[r * ld + i];
+        }
+        out[i] = acc / size;
+    }
+}
+
+inline unsigned grid_of(int64_t count) {
+    int64_t g = (count + 255) / 256;
+    return (unsigned)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
 }  // namespace
 
 extern "C" int mx_allreduce_mean(void* comm_v, float* buf, int64_t count, int nranks, void* stream) {
@@ -174,9 +214,48 @@ extern "C" int mx_allreduce_mean(void* comm_v, float* buf, int64_t count, int nr
     hipStream_t st = mx::as_stream(stream);
     MX_NCCL(ncclAllReduce(buf, buf, (size_t)count, ncclFloat32, ncclSum,
                           reinterpret_cast<ncclComm_t>(comm_v), st));
-    int64_t g = (count + 255) / 256;
-    if (g > 8192) g = 8192;
-    hipLaunchKernelGGL(div_kernel, dim3((unsigned)g), dim3(256), 0, st, buf, count, (float)nranks);
+    hipLaunchKernelGGL(div_kernel, dim3(grid_of(count)), dim3(256), 0, st, buf, count, (float)nranks);
     MX_LAUNCH_CHECK();
     return MX_OK;
+}
+
+extern "C" int mx_mean_rows(const float* rows, int nrows, int64_t ld, int64_t count, int order, float* out,
+                            void* stream) {
+    MX_CHECK(rows && out && nrows >= 1 && nrows <= 64 && ld >= count && count >= 0,
+             "mx_mean_rows: nrows=%d (1..64) ld=%lld count=%lld", nrows, (long long)ld, (long long)count);
+    MX_CHECK(order == 0 || order == 1, "mx_mean_rows: order %d (0 tree, 1 rank order)", order);
+    if (count == 0) return MX_OK;
+    hipStream_t st = mx::as_stream(stream);
+    const float d = (float)nrows;
+    if (order == 1) {
+        hipLaunchKernelGGL((mean_rows_kernel<0, 1>), dim3(grid_of(count)), dim3(256), 0, st, rows, nrows, ld, count, d,
+                           out);
+    } else if (nrows <= 8) {
+        hipLaunchKernelGGL((mean_rows_kernel<1, 8>), dim3(grid_of(count)), dim3(256), 0, st, rows, nrows, ld, count, d,
+                           out);
+    } else {
+        hipLaunchKernelGGL((mean_rows_kernel<1, 64>), dim3(grid_of(count)), dim3(256), 0, st, rows, nrows, ld, count, d,
+                           out);
+    }
+    MX_LAUNCH_CHECK();
+    return MX_OK;
+}
+
+extern "C" int mx_allgather(void* comm_v, const float* send, int64_t count, float* gather, void* stream) {
+    MX_CHECK(comm_v && count >= 0 && (count == 0 || (send && gather)), "mx_allgather: bad arguments");
+    if (count == 0) return MX_OK;
+    MX_NCCL(ncclAllGather(send, gather, (size_t)count, ncclFloat32, reinterpret_cast<ncclComm_t>(comm_v),
+                          mx::as_stream(stream)));
+    return MX_OK;
+}
+
+extern "C" int mx_allreduce_mean_ordered(void* comm_v, float* buf, int64_t count, float* gather, int order,
+                                         void* stream) {
+    MX_CHECK(comm_v && (count == 0 || (buf && gather)), "mx_allreduce_mean_ordered: bad arguments");
+    if (count == 0) return MX_OK;
+    int nranks = 0;
+    MX_NCCL(ncclCommCount(reinterpret_cast<ncclComm_t>(comm_v), &nranks));
+    int rc = mx_allgather(comm_v, buf, count, gather, stream);
+    if (rc != MX_OK) return rc;
+    return mx_mean_rows(gather, nranks, count, count, order, buf, stream);
 }

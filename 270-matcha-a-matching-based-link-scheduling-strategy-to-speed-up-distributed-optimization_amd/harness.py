@@ -25,6 +25,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ._lib import check, lib, stream_ptr
 from .choco import ChocoWorkerGroup
 from .engine import VirtualWorkerGroup
 from .graph_manager import FixedProcessor, MatchaProcessor
@@ -162,15 +163,21 @@ def make_topology(args, rank, size, iterations):
     return FixedProcessor(subGraphs, args.budget, rank, size, iterations, True)
 
 
-def sync_rows(rows):
-    """sync_allreduce (train_mpi.py:34-56) for workers held as rows: every row becomes
-    (sum over workers in rank order) / size."""
+def sync_rows(rows, order=0):
+    """sync_allreduce (train_mpi.py:34-56) for workers held as rows of one arena: every row
+    becomes (sum over workers) / size -- mx_mean_rows, the same kernel and summation order
+    (order 0: mpi4py's binomial tree, 1: rank order) as centralizedCommunicator's per-rank path.
+    (The reference's buffer Allreduce sums in the MPI library's own order; either order is within
+    fp32 reassociation of it.)"""
+    n, count = rows.shape
+    if n == 1 or count == 0:
+        return
+    if rows.stride(1) != 1:
+        raise ValueError("sync_rows: rows must be contiguous along the parameter axis")
+    check(lib.mx_mean_rows(rows.data_ptr(), n, rows.stride(0), count, int(order), rows[0].data_ptr(),
+                           stream_ptr()), "mx_mean_rows")
     with torch.no_grad():
-        acc = rows[0].clone()
-        for r in range(1, rows.shape[0]):
-            acc.add_(rows[r])
-        acc.div_(float(rows.shape[0]))
-        rows.copy_(acc.expand_as(rows))
+        rows[1:].copy_(rows[0].expand(n - 1, count))
 
 
 class VirtualTrainer:

@@ -43,6 +43,8 @@ def parse():
                     help="N > 1 partner exchange: rccl (the product path, one GPU per rank) or gloo "
                          "(tests/gloo_transport.py: host staging, lets N ranks share one GPU to test "
                          "the multi-process path; never a performance number)")
+    ap.add_argument("--staged", type=int, default=1, help="N = 1: also time host-resident models (the drop-in "
+                    "communicators' staging path for CPU models)")
     ap.add_argument("--allreduce", type=int, default=1, help="also time all-reduce averaging (the paper's "
                     "centralized baseline) on the same rows")
     ap.add_argument("--overlap", choices=("auto", "on", "off"), default="auto",
@@ -56,9 +58,27 @@ def parse():
     return ap.parse_args()
 
 
+def pickle_leg(partner, alpha, P, seconds):
+    """The reference's per-rank sequence with its pickled transport (oracle/pickle_ranks.py): one
+    process per worker pinned to its own core, torch.cat flatten, pickle.dumps -> pipe ->
+    pickle.loads per active edge, add_(alpha), copy_ back -- what mpirun's 8 ranks spend per
+    round (pickling dominates).  Full rounds; bounded by `seconds`."""
+    import pickle_ranks as PR
+    flags1 = np.ones((1, partner.shape[0]), np.uint8)
+    one, cores, _ = PR.run(partner, flags1, alpha, P)
+    rounds = max(1, min(20, int(seconds / max(one, 1e-6))))
+    el, cores, _ = PR.run(partner, np.ones((rounds, partner.shape[0]), np.uint8), alpha, P)
+    return {"value": rounds / el, "unit": "rounds/s", "cores": cores, "kind": "port",
+            "sample": f"{rounds} full rounds, graph 0, {partner.shape[1]} worker processes x {P} fp32 in "
+                      f"{PR.TENSOR_SPLIT} tensors, {el:.1f} s; oracle/pickle_ranks.py: torch.cat flatten, "
+                      f"pickled tensor per active edge over OS pipes, add_ chain, copy_ back, one process "
+                      f"pinned per core (nproc {os.cpu_count()})"}
+
+
 def cpu_baseline(pkg, partner, alpha, n, P, seconds):
     """The oracle's port of the reference per-rank sequence (cat-flatten, sendrecv copy, add_
-    FMA chain, copy_ back), one OpenMP thread per worker, on this box's host cores."""
+    FMA chain, copy_ back), one OpenMP thread per worker, on this box's host cores; beside it the
+    same sequence with the reference's pickled transport, one process per worker."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     threads = min(n, os.cpu_count() or 1)
@@ -81,7 +101,8 @@ def cpu_baseline(pkg, partner, alpha, n, P, seconds):
                       f"{el:.1f} s; oracle/matcha_oracle.c orc_baseline_rounds, {threads} OpenMP threads "
                       f"(one per worker, like the mpirun ranks) of {os.cpu_count()} host CPUs",
             "single_core": {"value": 1.0 / el1, "unit": "rounds/s", "cores": 1,
-                            "sample": f"1 full round, all {n} workers on one thread, {el1:.1f} s"}}
+                            "sample": f"1 full round, all {n} workers on one thread, {el1:.1f} s"},
+            "pickle": pickle_leg(partner, alpha, P, seconds)}
 
 
 def pmc_traffic(kernel_prefix="mix_kernel"):
@@ -108,8 +129,8 @@ def max_over_ranks(x, world, dev):
 
 
 def exchange_only(group, first, K, world, dev):
-    """N > 1 diagnostic: the RCCL exchange of K rounds alone (no mixing; rows do not change),
-    max over ranks of the back-to-back wall time per round."""
+    """N > 1 diagnostic: the RCCL exchange of K rounds alone (no mixing; rows do not change):
+    (max over ranks, [per rank]) of the back-to-back wall time per round."""
     import torch.distributed as dist
     eng = group.engine
     slab = group.slab.data_ptr() if group.slab is not None else None
@@ -119,8 +140,51 @@ def exchange_only(group, first, K, world, dev):
     for j in range(K):
         eng.exchange(first + j, group._row_ptrs, slab, group.ld * 4, group.numel * 4)
     torch.cuda.synchronize()
+    mine = (time.perf_counter() - t) / K
+    per = [None] * world
+    dist.all_gather_object(per, mine)
     dist.barrier()
-    return max_over_ranks((time.perf_counter() - t) / K, world, dev)
+    return max(per), per
+
+
+def sample_columns(P):
+    """64 columns spread over a row, including both ends and a 1024-column tile edge"""
+    c = np.linspace(0, P - 1, 64).astype(np.int64)
+    if P > 1025:
+        c[1], c[2] = 1023, 1024
+    return np.unique(c)
+
+
+def gather_columns(g, cols_dev, world, dev):
+    """{worker id: its row at the sampled columns} from every rank, on every rank"""
+    import torch.distributed as dist
+    loc = g.rows.index_select(1, cols_dev).cpu().numpy()
+    mine = (list(g.workers), loc)
+    objs = [mine]
+    if world > 1:
+        objs = [None] * world
+        dist.all_gather_object(objs, mine)
+    out = {}
+    for ws, blk in objs:
+        for i, w in enumerate(ws):
+            out[int(w)] = blk[i]
+    return out
+
+
+def replay_parity(pkg, GP, n, init, final, applied):
+    """The rounds one group went through (its iteration list, in order), recomputed on ONE GPU
+    by a single-process VirtualWorkerGroup over just the sampled columns (a gossip round mixes
+    each column on its own), compared bit for bit with what the timed group holds."""
+    P = init[0].shape[0]
+    ref = pkg.VirtualWorkerGroup(GP, numel=P)
+    ref.rows.copy_(torch.from_numpy(np.stack([init[w] for w in range(n)])))
+    for it in applied:
+        ref.step(it)
+    got = ref.rows.cpu().numpy()
+    want = np.stack([final[w] for w in range(n)])
+    ok = bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
+    del ref
+    return ok
 
 
 def p2p_probe(rank, world, nbytes, dev, reps=5):
@@ -193,7 +257,9 @@ def allreduce_figure(group, n, world, dev, K, W):
 
 def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99, gamma=0.1, placement=None):
     """Secondary figure: ChocoSGD rounds (BASELINE config: VGG-16 size, top-1 %, graph 0, every
-    matching active) on the same GPUs -- top-k compress + [N > 1] message exchange + fused apply."""
+    matching active) on the same GPUs -- top-k compress + [N > 1] message exchange + fused apply.
+    At N > 1 every worker's final row is gathered to rank 0 and compared bit for bit with the
+    same rounds recomputed by one single-GPU ChocoWorkerGroup (parity_ok)."""
     import torch.distributed as dist
     grp = pkg.ChocoWorkerGroup(GP, numel=P, ratio=ratio, consensus_lr=gamma, rank=rank, nranks=world,
                                comm=comm, placement=placement)
@@ -212,19 +278,71 @@ def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99
         dist.barrier()
     el = max_over_ranks(time.perf_counter() - t, world, dev)
     out = {"config": f"P={P} (VGG-16 size by default), ratio {ratio} (k={grp.k}), gamma {gamma}, graph 0 full rounds",
-           "rounds_per_s": K / el, "ms_per_round": 1e3 * el / K}
+           "rounds_per_s": K / el, "ms_per_round": 1e3 * el / K, "rows_per_gpu": grp.n_local, "parity_ok": None}
+    if world > 1:
+        mine = (list(grp.workers), grp.rows.cpu().numpy())
+        objs = [None] * world if rank == 0 else None
+        dist.gather_object(mine, objs, dst=0)
+        if rank == 0:
+            n = int(GP.size) if hasattr(GP, "size") else len(GP.neighbors_info[0])
+            ref = pkg.ChocoWorkerGroup(GP, numel=P, ratio=ratio, consensus_lr=gamma)
+            for r in range(n):
+                pkg._lib.check(pkg.lib.mx_synth_fill(ref.rows[r].data_ptr(), P, 1234 + r, None))
+            for it in range(W + K):
+                ref.step(it)
+            want = ref.rows.cpu().numpy()
+            ok = True
+            for ws, blk in objs:
+                for i, w in enumerate(ws):
+                    ok &= bool(np.array_equal(blk[i].view(np.uint32), want[w].view(np.uint32)))
+            out["parity_ok"] = ok
+            out["parity"] = "every worker's row vs a 1-GPU recompute of the same rounds, uint32"
+            del ref
+        dist.barrier()
     del grp
     torch.cuda.empty_cache()
     return out
 
 
-def timed_rounds(group, first, K):
+def staged_figure(pkg, GP, n, P, K, first):
+    """Secondary figure (N = 1): workers whose models stay on the host, as the reference's
+    train_mpi.py keeps them -- each round the drop-in communicator's staging (communicator.py
+    _Staging: torch.cat + H2D copy, round, D2H copy + copy_ into the model's tensors) for every
+    worker around the same mixing launch."""
+    from importlib import import_module
+    C = import_module(PKG_NAME + ".communicator")
+    grp = pkg.VirtualWorkerGroup(GP, numel=P)
+    host = []
+    for r in range(n):
+        pkg._lib.check(pkg.lib.mx_synth_fill(grp.rows[r].data_ptr(), P, 1234 + r, None))
+        row = grp.rows[r].cpu()
+        cuts = np.linspace(0, P, 55).astype(np.int64)          # VGG-16's 54 parameter tensors
+        ps = [torch.nn.Parameter(row[a:b].clone()) for a, b in zip(cuts[:-1], cuts[1:])]
+        host.append(C._Staging(ps, grp.rows[r]))
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    for j in range(K):
+        for st in host:
+            st.load()
+        grp.step(first + j)
+        torch.cuda.synchronize()
+        for st in host:
+            st.store()
+    el = time.perf_counter() - t
+    del grp, host
+    torch.cuda.empty_cache()
+    return {"rounds_per_s": K / el, "ms_per_round": 1e3 * el / K, "rounds": K,
+            "how": "8 host-resident models (54 pageable tensors each): stage in (torch.cat + H2D), mixing "
+                   "launch, stage out (D2H + copy_) per round -- the drop-in communicators' path for CPU models"}
+
+
+def timed_rounds(run, group, first, K):
     """K rounds from iteration `first` with per-round HIP events on the launch stream."""
     stream = torch.cuda.current_stream()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
     for j in range(K):
         ev[j][0].record(stream)
-        group.step(first + j)
+        run(group, first + j)
         ev[j][1].record(stream)
     return ev
 
@@ -262,17 +380,25 @@ def main():
     R = 4                                        # N > 1: untimed calibration rounds per exchange form
     np.random.seed(1234)
     GP = pkg.MatchaProcessor(pkg.select_graph(args.graph), args.budget, rank, n,
-                             W + 2 * K + (R + 1 if world > 1 else 0), True)
+                             W + 3 * K + (R + 1 if world > 1 else 0), True)
     group = pkg.VirtualWorkerGroup(GP, numel=P, rank=rank, nranks=world, comm=comm, placement=args.placement)
     for r in range(group.n_local):
         pkg._lib.check(pkg.lib.mx_synth_fill(group.rows[r].data_ptr(), P, 1234 + group.workers[r], None))
     torch.cuda.synchronize()
+    cols = torch.from_numpy(sample_columns(P)).cuda()
+    init_cols = gather_columns(group, cols, world, dev)      # self-check: the columns before any round
+    applied = {}                                             # group -> iterations it ran, in order
+
+    def run(g, it):
+        g.step(it)
+        applied.setdefault(id(g), []).append(it)
 
     for it in range(W):
-        group.step(it)
+        run(group, it)
     torch.cuda.synchronize()
     timed, overlap = group, None
     any_remote = world > 1 and max_over_ranks(float(group.engine.max_remote), world, dev) > 0   # collective
+    base_it = W + 3 * K
     if any_remote and args.overlap != "off":
         # column pipelining: chunk c+1 of every exchanged row travels on a side stream while chunk c
         # is mixed (bit-identical results).  Whether it pays depends on the link rate vs the extra
@@ -283,19 +409,20 @@ def main():
                                         chunk_cols=C)
         for r in range(gchunk.n_local):
             pkg._lib.check(pkg.lib.mx_synth_fill(gchunk.rows[r].data_ptr(), P, 1234 + gchunk.workers[r], None))
-        base_it = W + 2 * K
+        for it in range(W):
+            run(gchunk, it)
 
         def calib(g, first):
             torch.cuda.synchronize()
             dist.barrier()
             t = time.perf_counter()
             for j in range(R):
-                g.step(first + j)
+                run(g, first + j)
             torch.cuda.synchronize()
             dist.barrier()
             return max_over_ranks((time.perf_counter() - t) / R, world, dev)
 
-        gchunk.step(base_it)                     # first chunked round (side stream, events) untimed
+        run(gchunk, base_it)                     # first chunked round (side stream, events) untimed
         t_plain = calib(group, base_it) if args.overlap == "auto" else None
         t_chunk = calib(gchunk, base_it + 1)
         use_chunk = args.overlap == "on" or t_chunk < t_plain
@@ -307,28 +434,33 @@ def main():
             timed = gchunk
         else:
             del gchunk
+    # per-round HIP events of the whole round (diagnostic) -- K real rounds, run BEFORE the timed
+    # region so that the timed rounds start on a GPU already streaming (not after a pause)
+    ev = timed_rounds(run, timed, W, K)
+    torch.cuda.synchronize()
+    step_ms = np.array([a.elapsed_time(b) for a, b in ev])
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for j in range(K):                           # the timed rounds: back to back, nothing else
-        timed.step(W + j)
+        run(timed, W + K + j)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed, world, dev)
-    # per-round HIP events (diagnostic, outside the timed region): K more rounds
-    ev = timed_rounds(group, W + K, K)
-    torch.cuda.synchronize()
-    step_ms = np.array([a.elapsed_time(b) for a, b in ev])
-    # mixing kernel alone (N > 1: without the RCCL exchange) -> its HBM roofline
+    # self-check: every worker's sampled columns vs the same rounds recomputed on one GPU
+    final_cols = gather_columns(timed, cols, world, dev)
+    parity_ok = (replay_parity(pkg, GP, n, init_cols, final_cols, applied[id(timed)])
+                 if rank == 0 else None)
+    # mixing kernel alone (N > 1: without the RCCL exchange, so rows go stale) -> its HBM roofline
     stream = torch.cuda.current_stream()
     mev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
     for j in range(K):
         mev[j][0].record(stream)
-        group.engine.mix(W + j, group.layout)
+        group.engine.mix(W + 2 * K + j, group.layout)
         mev[j][1].record(stream)
     torch.cuda.synchronize()
     mix_ms = np.array([a.elapsed_time(b) for a, b in mev])
@@ -379,8 +511,9 @@ def main():
     choco = (choco_figure(pkg, GP, rank, world, max(5, K // 5), 3, comm, dev, P=args.choco_params,
                           placement=args.placement)
              if args.choco else None)
+    staged = staged_figure(pkg, GP, n, P, 3, W) if (world == 1 and args.staged) else None
 
-    flags = np.asarray(GP.active_flags[W:W + K], np.uint8)
+    flags = np.asarray(GP.active_flags[W + K:W + 2 * K], np.uint8)
     # algorithmic HBM bytes of the mixing kernel on this GPU: every local row with degree > 0 read
     # and written once, every received slab row read once (positions of the engine's table: with a
     # placement, worker group.workers[i] sits at position row_base + i)
@@ -418,9 +551,9 @@ def main():
             pair[key] = pair.get(key, 0) + v
         pair_bytes.append(max(pair.values()) if pair else 0)
     avg_ms = float(step_ms.mean())
-    exch_s = probe = None
+    exch_s = exch_per = probe = None
     if world > 1:             # (with --transport gloo: the same code over host staging, tests only)
-        exch_s = exchange_only(group, W + K, K, world, dev)
+        exch_s, exch_per = exchange_only(group, W + K, K, world, dev)
         probe = p2p_probe(rank, world, P * 4, dev)
     mix_avg_ms = float(mix_ms.mean())
     mix_bytes = float(np.mean(hbm_bytes))
@@ -449,11 +582,20 @@ def main():
                                       (", column-pipelined exchange" if timed is not group else ""),
                        "placement": group.placement if world > 1 else None,
                        "transport": args.transport if world > 1 else None},
+            "parity_ok": parity_ok,
+            "parity": (f"every worker's {len(sample_columns(P))} sampled columns after all "
+                       f"{len(applied[id(timed)])} rounds this run applied, vs the same rounds recomputed on one "
+                       f"GPU by a single-process VirtualWorkerGroup (uint32 compare)"),
+            "round_us": {"events_min": 1e3 * float(step_ms.min()), "events_median": 1e3 * float(np.median(step_ms)),
+                         "events_mean": 1e3 * avg_ms, "timed_mean": 1e6 * elapsed / K,
+                         "note": "per-round HIP events of K untimed rounds run just before the timed region (rank 0)"},
             "roofline": {"bound": "hbm", "kernel": f"{pkg.engine.mix_kernel_name(eng.n_slots)} (mx_gossip_mix)",
                          "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK, "traffic": traffic,
                          "traffic_source": traffic_src, "bytes_per_launch": mix_bytes,
-                         "avg_launch_ms": mix_avg_ms,
+                         "avg_launch_ms": mix_avg_ms, "min_launch_ms": float(mix_ms.min()),
+                         "median_launch_ms": float(np.median(mix_ms)),
+                         "frac_timed_region": (mix_bytes / (elapsed / K)) / HBM_PEAK if world == 1 else None,
                          "same_box_torch_copy_ms": ref_copy_ms,
                          "vs_same_box_copy": (ref_copy_ms / mix_avg_ms) if ref_copy_ms else None,
                          "tuning": pkg.engine.mix_tuning(),
@@ -463,6 +605,7 @@ def main():
             "allreduce_baseline": allreduce,
             "overlap": overlap,
             "choco": choco,
+            "cpu_resident_models": staged,
         }
         if world > 1:
             lb = float(np.mean(link_bytes))
@@ -478,6 +621,7 @@ def main():
                            "aggregate_achieved": float(np.mean(total_bytes)) / round_s / 1e9,
                            "round_ms": 1e3 * round_s, "round_ms_events_rank0": avg_ms,
                            "exchange_only_ms": 1e3 * exch_s if exch_s else None,
+                           "exchange_only_ms_per_rank": [1e3 * x for x in exch_per] if exch_per else None,
                            "exchange_only_busiest_link_GBps": lb / exch_s / 1e9 if exch_s else None,
                            "exchange_only_busiest_pair_both_directions_GBps": pb / exch_s / 1e9 if exch_s else None,
                            "p2p_probe": ({"bytes": P * 4, "uni_ms": 1e3 * probe["uni"],

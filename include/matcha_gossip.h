@@ -251,8 +251,22 @@ int mx_exchange_round(void* comm, const uint8_t* flags_row, int M, const int32_t
                       int n_global, const int32_t* owner, int my_rank, int row_base, int n_local,
                       void* const* rows, void* slab, int64_t slab_ld_bytes, int64_t row_bytes,
                       int* n_remote_out, void* stream);
-/* centralizedCommunicator.averaging (communicator.py:56-67): buf = allreduce_sum(buf) / size */
+/* centralizedCommunicator.averaging (communicator.py:56-67): buf = allreduce_sum(buf) / size.
+ * mx_allreduce_mean: RCCL's all-reduce (ring / tree order of RCCL's choosing), then the division;
+ *   equal to the reference within fp32 reassociation (1e-6 relative for well-conditioned sums).
+ * mx_allreduce_mean_ordered: bit-identical to the reference -- every rank's buffer is
+ *   all-gathered into `gather` (float[nranks][count], device) and each rank sums the rows in the
+ *   reference's order (mx_mean_rows) and divides by nranks.  order 0: the binomial tree of
+ *   mpi4py's object all-reduce (rc.fast_reduce, its default); 1: rank order (fast_reduce off). */
 int mx_allreduce_mean(void* comm, float* buf, int64_t count, int nranks, void* stream);
+int mx_allreduce_mean_ordered(void* comm, float* buf, int64_t count, float* gather, int order, void* stream);
+/* ncclAllGather of `count` floats per rank into gather[nranks][count] (rank order). */
+int mx_allgather(void* comm, const float* send, int64_t count, float* gather, void* stream);
+/* out[i] = (rows[0][i] + ... + rows[nrows-1][i] in the given order) / nrows for i < count; rows
+ * are nrows x ld floats (device), 1 <= nrows <= 64; out may be rows[0].  The division step of
+ * the centralized communicator (communicator.py:61-62) and of sync_allreduce (train_mpi.py:46-55),
+ * callable after any transport's gather. */
+int mx_mean_rows(const float* rows, int nrows, int64_t ld, int64_t count, int order, float* out, void* stream);
 
 /* ---------------------------------------------------------------- utilities
  * splitmix64 -> fp32 uniform[-1,1) synthetic inputs, x[i] for counter i+1. */

@@ -1,7 +1,7 @@
 """Test double for the RCCL transport across REAL processes: gloo over the host.
 
-GossipEngine accepts any object with ``exchange_round`` (and ``allreduce_mean`` for the
-centralized communicator) in place of the RCCL communicator.  This one moves each row the
+GossipEngine accepts any object with ``exchange_round`` (and ``allgather`` / ``allreduce_mean``
+for the centralized communicator) in place of the RCCL communicator.  This one moves each row the
 native mx_exchange_plan names through host memory with gloo isend / irecv, in the plan's order,
 so several processes can run the multi-GPU code path (partition, plan slots, receive slab,
 chunked pipelining, the bench's N > 1 timing) on ONE GPU -- RCCL refuses two ranks on one
@@ -64,6 +64,12 @@ class GlooTransport:
                 nrem += 1
         torch.cuda.synchronize()
         return nrem
+
+    def allgather(self, flat, gather):
+        """every rank's `flat` into gather[rank * n : (rank + 1) * n] (device), rank order"""
+        host = [torch.empty(flat.numel(), dtype=torch.float32) for _ in range(self.nranks)]
+        dist.all_gather(host, flat.cpu(), group=self.group)
+        gather.copy_(torch.cat(host).to(gather.device))
 
     def allreduce_mean(self, flat, size):
         host = flat.cpu()

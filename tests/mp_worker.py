@@ -21,6 +21,7 @@ for p in (ROOT, HERE, os.path.join(ROOT, "oracle")):
 import oracle as O  # noqa: E402
 from conftest import PKG_NAME, Topo  # noqa: E402
 from gloo_transport import GlooTransport, gather_rows  # noqa: E402
+from reforder import mpi4py_sum as _mpi4py_sum  # noqa: E402
 
 
 def by_worker(grp, rows):
@@ -78,14 +79,33 @@ def choco_case(pkg, T, P, ratio, rounds, seed=9, placement=None):
 
 
 def centralized_case(pkg, T):
+    """centralizedCommunicator through the product path (gather over the transport, then the
+    native mx_mean_rows in the reference's order + the div_ of communicator.py:62) on random rows:
+    bit-exact for "tree" / "sequential", within 1e-6 relative for "ring"."""
     rank, world = dist.get_rank(), dist.get_world_size()
-    m = torch.nn.Linear(7, 5).cuda()
-    with torch.no_grad():
-        for p in m.parameters():
-            p.copy_(torch.full_like(p, float(rank + 1)))
-    pkg.centralizedCommunicator(rank, world, transport=T).communicate(m)
-    want = sum(range(1, world + 1)) / world
-    return all(bool(torch.all(p == want)) for p in m.parameters())
+    ok = True
+    for order in ("tree", "sequential", "ring"):
+        torch.manual_seed(0)
+        m = torch.nn.Sequential(torch.nn.Linear(300, 200), torch.nn.Linear(200, 77)).cuda()
+        shapes = [p.shape for p in m.parameters()]
+        P = sum(p.numel() for p in m.parameters())
+        rows = [O.synth(555 + r, P) * np.float32(10.0 ** (r % 3)) for r in range(world)]
+        with torch.no_grad():
+            off = 0
+            for p in m.parameters():
+                p.copy_(torch.from_numpy(rows[rank][off:off + p.numel()].reshape(p.shape)))
+                off += p.numel()
+        pkg.centralizedCommunicator(rank, world, transport=T, order=order).communicate(m)
+        got = torch.cat([p.detach().reshape(-1) for p in m.parameters()]).cpu().numpy()
+        assert [p.shape for p in m.parameters()] == shapes
+        if order == "ring":
+            want = _mpi4py_sum(rows, "tree") / np.float32(world)
+            scale = np.abs(np.stack(rows)).sum(0) / np.float32(world)   # reassociation bound
+            ok &= bool(np.all(np.abs(got - want) <= 1e-6 * scale))
+        else:
+            want = _mpi4py_sum(rows, order) / np.float32(world)
+            ok &= bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
+    return ok
 
 
 def main():

@@ -71,6 +71,18 @@ def main():
     rc = pkg.lib.mx_exchange_post(comm.handle, bad.ctypes.data, len(bad), ptrs, 3, slab.data_ptr(), ld * 4,
                                   P2 * 4, pkg._lib.stream_ptr())
     out["post_validates"] = rc != 0
+    bad = ops.copy()
+    bad[1, 1] = 1                                    # peer 1 of a one-rank communicator: refused
+    rc = pkg.lib.mx_exchange_post(comm.handle, bad.ctypes.data, len(bad), ptrs, 3, slab.data_ptr(), ld * 4,
+                                  P2 * 4, pkg._lib.stream_ptr())
+    out["post_validates_peer"] = rc != 0
+    # the reference-order all-reduce mean (all-gather + mx_mean_rows): one rank -> x / 1 = x
+    z = x.clone()
+    gather = torch.empty_like(z)
+    pkg._lib.check(pkg.lib.mx_allreduce_mean_ordered(comm.handle, z.data_ptr(), z.numel(), gather.data_ptr(), 0,
+                                                     pkg._lib.stream_ptr()))
+    torch.cuda.synchronize()
+    out["allreduce_ordered_identity"] = bool(torch.equal(x, z) and torch.equal(gather, x))
     comm.close()
     dist.destroy_process_group()
     print(json.dumps(out), flush=True)

@@ -171,3 +171,21 @@ def test_graph_mode_checkpoint_reload(pkg, compress):
         assert torch.equal(eag.group.x_hat, gra.group.x_hat) and torch.equal(eag.group.s, gra.group.s)
     assert [s["loss"] for s in se] == [s["loss"] for s in sg]
     assert len(gra._graphs) == 1            # reused, not recaptured
+
+
+@pytest.mark.parametrize("order", [0, 1])
+def test_sync_rows_reference_order_mean(pkg, order):
+    """sync_allreduce for arena rows: every row = (tree / rank-order sum) / n via mx_mean_rows."""
+    import sys, os
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from reforder import mpi4py_sum
+    arena = torch.zeros((5, 1088), dtype=torch.float32, device="cuda")
+    rows = arena[:, :1000]
+    host = [np.random.RandomState(r).standard_normal(1000).astype(np.float32) * np.float32(10.0 ** r)
+            for r in range(5)]
+    rows.copy_(torch.from_numpy(np.stack(host)))
+    pkg.harness.sync_rows(rows, order=order)
+    want = mpi4py_sum(host, "tree" if order == 0 else "sequential") / np.float32(5)
+    got = rows.cpu().numpy()
+    for r in range(5):
+        assert np.array_equal(got[r].view(np.uint32), want.view(np.uint32))

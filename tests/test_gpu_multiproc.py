@@ -57,6 +57,8 @@ def test_bench_multiprocess_path():
     assert ov["calib_ms_unchunked"] > 0 and ov["calib_ms_chunked"] > 0
     assert out["choco"]["rounds_per_s"] > 0 and out["cpu_baseline"] is None
     assert out["allreduce_baseline"]["rounds_per_s"] > 0
+    assert out["parity_ok"] is True and out["choco"]["parity_ok"] is True     # self-checks vs 1-GPU recompute
+    assert len(out["xgmi"]["exchange_only_ms_per_rank"]) == 2
 
 
 @pytest.mark.parametrize("nproc,overlap", [(2, "on"), (4, "off")])
@@ -66,7 +68,7 @@ def test_bench_multiprocess_overlap_forms(nproc, overlap):
                           "--params", "100000", "--choco", "0", "--cpu-seconds", "0", "--overlap", overlap])
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
-    assert out["value"] > 0
+    assert out["value"] > 0 and out["parity_ok"] is True
     if overlap == "on":
         assert out["overlap"]["chosen"] == "chunked" and "column-pipelined" in out["config"]["parallelism"]
     else:
@@ -92,4 +94,23 @@ def test_rccl_single_rank_linkage():
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out == {"rank": 0, "nranks": 1, "allreduce_identity": True, "decen_bit_exact": True,
-                   "post_self_exchange": True, "post_validates": True}, out
+                   "post_self_exchange": True, "post_validates": True, "post_validates_peer": True,
+                   "allreduce_ordered_identity": True}, out
+
+
+def test_bench_single_gpu_line():
+    """bench.py at N = 1 on a small shape: the line's contract fields, the self-check, the
+    per-round event statistics, the host-model staging figure and both CPU baseline legs."""
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "4", "--warmup", "2", "--params", "300000",
+                        "--choco-params", "200000", "--cpu-seconds", "1"], cwd=ROOT, capture_output=True,
+                       text=True, timeout=280, env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["n_gpus"] == 1 and out["steps"] == 4 and out["warmup"] == 2 and out["value"] > 0
+    assert out["parity_ok"] is True
+    ru = out["round_us"]
+    assert 0 < ru["events_min"] <= ru["events_median"]
+    assert out["roofline"]["frac"] > 0 and out["roofline"]["min_launch_ms"] > 0
+    assert out["cpu_resident_models"]["rounds_per_s"] > 0
+    cb = out["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["value"] > 0 and cb["pickle"]["value"] > 0 and cb["pickle"]["cores"] >= 1

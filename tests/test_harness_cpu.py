@@ -71,11 +71,3 @@ def test_synthetic_batches_deterministic(pkg):
     assert all(torch.equal(x[0], y[0]) and torch.equal(x[1], y[1]) for x, y in zip(a, b))
     assert not torch.equal(a[0][0], c[0][0])
     assert a[0][0].shape == (5, 1, 28, 28) and int(a[0][1].max()) < 100
-
-
-def test_sync_rows_is_rank_order_mean(pkg):
-    rows = torch.tensor([[1.0, 2.0], [3.0, 5.0], [0.5, -1.0]])
-    want = ((rows[0] + rows[1]) + rows[2]) / 3.0
-    pkg.harness.sync_rows(rows)
-    for r in range(3):
-        assert torch.equal(rows[r], want)
