@@ -9,7 +9,7 @@ torch.distributed (for bootstrap) plus an RCCL communicator owned by the native 
 rank's model is a one-row VirtualWorkerGroup / ChocoWorkerGroup on its GPU and partner rows
 travel over xGMI.  If torch.distributed is not initialised, it is initialised here from the
 environment (torchrun's RANK/WORLD_SIZE/MASTER_*, or the (rank, size) given, with
-MASTER_ADDR 127.0.0.1).
+MASTER_ADDR 127.0.0.1 and a MASTER_PORT derived from the launcher's job id -- rendezvous_port).
 
 Model parameters on the GPU are re-homed into the group's arena on the first call (views, so
 identity, shapes and optimizer references are kept) and mixed in place every round.  Models
@@ -33,12 +33,30 @@ def _same_params(model, params):
     return params is not None and len(cur) == len(params) and all(a is b for a, b in zip(cur, params))
 
 
+_JOB_ID_VARS = ("PMIX_NAMESPACE", "OMPI_MCA_ess_base_jobid", "SLURM_JOB_ID", "PBS_JOBID", "LSB_JOBID")
+
+
+def rendezvous_port(env=None):
+    """MASTER_PORT for the bootstrap when the launcher did not set one (mpirun, as the reference
+    is launched: README.md:62-65).  Derived from the launcher's job id, so every rank of one job
+    agrees on it without talking and two jobs on one node do not collide; 29533 only when no job
+    id is visible either."""
+    env = os.environ if env is None else env
+    if env.get("MASTER_PORT"):
+        return int(env["MASTER_PORT"])
+    for k in _JOB_ID_VARS:
+        if env.get(k):
+            import zlib
+            return 20000 + zlib.crc32(env[k].encode()) % 30000
+    return 29533
+
+
 def _ensure_process_group(rank, size):
     import torch.distributed as dist
     require_device()
     if size > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ["MASTER_PORT"] = str(rendezvous_port())
         dist.init_process_group("gloo", rank=rank, world_size=size)
     if size > 1:
         if dist.get_world_size() != size or dist.get_rank() != rank:

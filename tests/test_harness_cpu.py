@@ -71,3 +71,15 @@ def test_synthetic_batches_deterministic(pkg):
     assert all(torch.equal(x[0], y[0]) and torch.equal(x[1], y[1]) for x, y in zip(a, b))
     assert not torch.equal(a[0][0], c[0][0])
     assert a[0][0].shape == (5, 1, 28, 28) and int(a[0][1].max()) < 100
+
+
+def test_rendezvous_port_from_job_id(pkg):
+    """MASTER_PORT: the launcher's if set, else derived from the job id (mpirun / slurm), so two
+    jobs on one node get different ports and all ranks of a job the same one."""
+    rp = pkg.communicator.rendezvous_port
+    assert rp({"MASTER_PORT": "4711"}) == 4711
+    a = rp({"PMIX_NAMESPACE": "prterun-node-1234@1"})
+    b = rp({"PMIX_NAMESPACE": "prterun-node-1235@1"})
+    assert a != b and 20000 <= a < 50000 and a == rp({"PMIX_NAMESPACE": "prterun-node-1234@1"})
+    assert rp({"SLURM_JOB_ID": "77"}) == rp({"SLURM_JOB_ID": "77"})
+    assert rp({}) == 29533
