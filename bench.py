@@ -43,6 +43,8 @@ def parse():
                     help="N > 1 partner exchange: rccl (the product path, one GPU per rank) or gloo "
                          "(tests/gloo_transport.py: host staging, lets N ranks share one GPU to test "
                          "the multi-process path; never a performance number)")
+    ap.add_argument("--settle-ms", type=float, default=50.0, help="diagnostic rounds (per-round HIP events) "
+                    "run for at least this long between the warmup and the timed region")
     ap.add_argument("--staged", type=int, default=1, help="N = 1: also time host-resident models (the drop-in "
                     "communicators' staging path for CPU models)")
     ap.add_argument("--allreduce", type=int, default=1, help="also time all-reduce averaging (the paper's "
@@ -378,9 +380,10 @@ def main():
     n, P = args.workers, args.params
     K, W = args.steps, args.warmup
     R = 4                                        # N > 1: untimed calibration rounds per exchange form
+    DMAX = max(K, 4000)                          # most diagnostic (settling) rounds
     np.random.seed(1234)
     GP = pkg.MatchaProcessor(pkg.select_graph(args.graph), args.budget, rank, n,
-                             W + 3 * K + (R + 1 if world > 1 else 0), True)
+                             W + DMAX + 2 * K + (R + 1 if world > 1 else 0), True)
     group = pkg.VirtualWorkerGroup(GP, numel=P, rank=rank, nranks=world, comm=comm, placement=args.placement)
     for r in range(group.n_local):
         pkg._lib.check(pkg.lib.mx_synth_fill(group.rows[r].data_ptr(), P, 1234 + group.workers[r], None))
@@ -398,7 +401,7 @@ def main():
     torch.cuda.synchronize()
     timed, overlap = group, None
     any_remote = world > 1 and max_over_ranks(float(group.engine.max_remote), world, dev) > 0   # collective
-    base_it = W + 3 * K
+    base_it = W + DMAX + 2 * K
     if any_remote and args.overlap != "off":
         # column pipelining: chunk c+1 of every exchanged row travels on a side stream while chunk c
         # is mixed (bit-identical results).  Whether it pays depends on the link rate vs the extra
@@ -434,23 +437,37 @@ def main():
             timed = gchunk
         else:
             del gchunk
-    # per-round HIP events of the whole round (diagnostic) -- K real rounds, run BEFORE the timed
-    # region so that the timed rounds start on a GPU already streaming (not after a pause)
-    ev = timed_rounds(run, timed, W, K)
-    torch.cuda.synchronize()
-    step_ms = np.array([a.elapsed_time(b) for a, b in ev])
+    # per-round HIP events of the whole round (diagnostic): real rounds run BEFORE the timed region,
+    # in blocks of K, for at least --settle-ms (an idle MI355X takes ~10 ms of streaming to reach
+    # its steady clocks: tools/ramp.py), so the timed rounds measure the steady state of the loop
+    step_ms = []
+    it = W
+    t_settle = time.perf_counter()
+    while True:
+        ev = timed_rounds(run, timed, it, K)
+        torch.cuda.synchronize()
+        step_ms += [a.elapsed_time(b) for a, b in ev]
+        it += K
+        done = (time.perf_counter() - t_settle) * 1e3 >= args.settle_ms or it - W + K > DMAX
+        if world > 1:                            # every rank leaves after the same block
+            done = max_over_ranks(float(done), world, dev) > 0
+        if done:
+            break
+    diag_rounds = it - W
+    step_ms = np.array(step_ms)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for j in range(K):                           # the timed rounds: back to back, nothing else
-        run(timed, W + K + j)
+        run(timed, it + j)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed, world, dev)
+    timed_first = it
     # self-check: every worker's sampled columns vs the same rounds recomputed on one GPU
     final_cols = gather_columns(timed, cols, world, dev)
     parity_ok = (replay_parity(pkg, GP, n, init_cols, final_cols, applied[id(timed)])
@@ -460,7 +477,7 @@ def main():
     mev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
     for j in range(K):
         mev[j][0].record(stream)
-        group.engine.mix(W + 2 * K + j, group.layout)
+        group.engine.mix(timed_first + K + j, group.layout)
         mev[j][1].record(stream)
     torch.cuda.synchronize()
     mix_ms = np.array([a.elapsed_time(b) for a, b in mev])
@@ -513,7 +530,7 @@ def main():
              if args.choco else None)
     staged = staged_figure(pkg, GP, n, P, 3, W) if (world == 1 and args.staged) else None
 
-    flags = np.asarray(GP.active_flags[W + K:W + 2 * K], np.uint8)
+    flags = np.asarray(GP.active_flags[timed_first:timed_first + K], np.uint8)
     # algorithmic HBM bytes of the mixing kernel on this GPU: every local row with degree > 0 read
     # and written once, every received slab row read once (positions of the engine's table: with a
     # placement, worker group.workers[i] sits at position row_base + i)
@@ -553,7 +570,7 @@ def main():
     avg_ms = float(step_ms.mean())
     exch_s = exch_per = probe = None
     if world > 1:             # (with --transport gloo: the same code over host staging, tests only)
-        exch_s, exch_per = exchange_only(group, W + K, K, world, dev)
+        exch_s, exch_per = exchange_only(group, timed_first, K, world, dev)
         probe = p2p_probe(rank, world, P * 4, dev)
     mix_avg_ms = float(mix_ms.mean())
     mix_bytes = float(np.mean(hbm_bytes))
@@ -587,8 +604,11 @@ def main():
                        f"{len(applied[id(timed)])} rounds this run applied, vs the same rounds recomputed on one "
                        f"GPU by a single-process VirtualWorkerGroup (uint32 compare)"),
             "round_us": {"events_min": 1e3 * float(step_ms.min()), "events_median": 1e3 * float(np.median(step_ms)),
-                         "events_mean": 1e3 * avg_ms, "timed_mean": 1e6 * elapsed / K,
-                         "note": "per-round HIP events of K untimed rounds run just before the timed region (rank 0)"},
+                         "events_mean": 1e3 * avg_ms, "events_last_block_mean": 1e3 * float(step_ms[-K:].mean()),
+                         "events_first_block_mean": 1e3 * float(step_ms[:K].mean()),
+                         "diag_rounds": int(diag_rounds), "timed_mean": 1e6 * elapsed / K,
+                         "note": f"per-round HIP events of {diag_rounds} untimed rounds (blocks of K, >= "
+                                 f"{args.settle_ms} ms) run between the warmup and the timed region (rank 0)"},
             "roofline": {"bound": "hbm", "kernel": f"{pkg.engine.mix_kernel_name(eng.n_slots)} (mx_gossip_mix)",
                          "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK, "traffic": traffic,
