@@ -57,6 +57,7 @@ SIGNATURES = {
     "mx_allgather": (c_int, [c_p, c_p, c_i64, c_p, c_p]),
     "mx_mean_rows": (c_int, [c_p, c_int, c_i64, c_i64, c_int, c_p, c_p]),
     "mx_synth_fill": (c_int, [c_p, c_i64, c_u64, c_p]),
+    "mx_max_weight_matching": (c_int, [c_int, c_p, c_p, c_p, c_int, c_p, c_p, c_p]),
 }
 
 

@@ -7,9 +7,11 @@ Same class names, constructor signature and attributes as the reference's graph_
     GP.subGraphs, GP.L_matrices, GP.neighbors_info, GP.probabilities, GP.neighbor_weight,
     GP.active_flags  (list of iterations+1 rows, one 0/1 entry per matching)
 
-Host side (as in the reference): matching decomposition (networkx max_weight_matching plus
-the greedy colouring), Laplacians, partner table, FixedProcessor's closed-form alpha and the
-MATCHA probability / alpha solves (solver.py; cvxpy/CVXOPT are absent).
+Host side (as in the reference): matching decomposition (max_weight_matching plus the greedy
+colouring), Laplacians, partner table, FixedProcessor's closed-form alpha and the MATCHA
+probability / alpha solves (solver.py; cvxpy/CVXOPT are absent).  No networkx: the graph and the
+blossom matching are restated in graph_core.py / csrc/matching.cpp with networkx 3.4.2's visiting
+orders, so the decomposition is the reference's (pinned by tests/golden/decomposition.json).
 
 GPU side: the per-iteration Bernoulli flags.  They are drawn on the MI355X from numpy's
 global MT19937 state (mx_flags_binomial), bit-exact with np.random.binomial, and numpy's
@@ -22,10 +24,10 @@ import ctypes
 import random
 import sys
 
-import networkx as nx
 import numpy as np
 
 from . import solver
+from .graph_core import OrderedGraph, is_perfect_matching, max_weight_matching
 from ._lib import check, lib, require_device, stream_ptr
 
 
@@ -57,22 +59,23 @@ class GraphProcessor(object):
         raise NotImplementedError
 
     def getGraphFromSub(self, subGraphs):
-        """graph_manager.py:51-55: union of the edge lists."""
-        G = nx.Graph()
+        """graph_manager.py:51-55: union of the edge lists (nx.Graph's insertion-ordered
+        adjacency, graph_core.OrderedGraph)."""
+        G = OrderedGraph()
         for edges in subGraphs:
             G.add_edges_from(edges)
         return G
 
     def getSubGraphs(self):
-        """graph_manager.py:57-83.  Peel perfect matchings with nx.max_weight_matching for up to
+        """graph_manager.py:57-83.  Peel perfect matchings with max_weight_matching for up to
         size-1 rounds (re-ordering the edge list with Python's global `random` when the matching
-        is not perfect, which changes networkx's tie-breaking), then colour the rest greedily.
-        Mutates self.base_graph exactly as the reference does."""
+        is not perfect, which changes the blossom search's tie-breaking), then colour the rest
+        greedily.  Mutates self.base_graph exactly as the reference does."""
         G = self.base_graph
         found = []
         for _ in range(self.size - 1):
-            matching = nx.max_weight_matching(G)
-            if nx.is_perfect_matching(G, matching):
+            matching = max_weight_matching(G)
+            if is_perfect_matching(G, matching):
                 G.remove_edges_from(list(matching))
                 found.append(list(matching))
             else:
@@ -84,8 +87,8 @@ class GraphProcessor(object):
 
     def graphToLaplacian(self):
         """graph_manager.py:86-93: one dense n x n Laplacian per matching over nodes range(size).
-        (networkx>=3 rejects nodelist entries missing from the graph; the Laplacian is built
-        directly, which is what networkx 2.x returned.)"""
+        (nx.laplacian_matrix over nodelist range(size); built directly -- networkx>=3 would reject
+        nodes missing from a matching, networkx 2.x returned zero rows for them, as here.)"""
         out = []
         for edges in self.subGraphs:
             L = np.zeros((self.size, self.size), dtype=np.int64)
@@ -93,7 +96,7 @@ class GraphProcessor(object):
             for a, b in edges:
                 a, b = int(a), int(b)
                 key = (min(a, b), max(a, b))
-                if a == b or key in seen:     # nx.Graph collapses duplicates; self loops cancel
+                if a == b or key in seen:     # a Graph collapses duplicates; self loops cancel
                     continue
                 seen.add(key)
                 L[a, a] += 1

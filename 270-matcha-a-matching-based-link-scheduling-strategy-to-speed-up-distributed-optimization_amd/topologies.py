@@ -3,7 +3,7 @@
 Each graph is a list of matchings (edge lists); pass it to FixedProcessor / MatchaProcessor
 with issubgraph=True to use the matchings as given, or issubgraph=False to re-decompose.
 """
-import networkx as nx
+from .graph_core import gnp_random_graph
 
 _GRAPHS = [
     # graph 0: 8-node Erdos-Renyi graph, Fig. 1(a) of the MATCHA paper
@@ -46,6 +46,6 @@ def select_graph(graphid):
 
 
 def erdos_renyi(n, p, seed):
-    """A base graph given as one edge list (decompose with issubgraph=False)."""
-    g = nx.gnp_random_graph(n, p, seed=seed)
-    return [sorted(tuple(sorted(e)) for e in g.edges())]
+    """A base graph given as one edge list (decompose with issubgraph=False): the edges of
+    nx.gnp_random_graph(n, p, seed) (graph_core.gnp_random_graph, no networkx), sorted."""
+    return [sorted(tuple(sorted(e)) for e in gnp_random_graph(n, p, seed))]

@@ -268,6 +268,17 @@ int mx_allgather(void* comm, const float* send, int64_t count, float* gather, vo
  * callable after any transport's gather. */
 int mx_mean_rows(const float* rows, int nrows, int64_t ld, int64_t count, int order, float* out, void* stream);
 
+/* ---------------------------------------------------------------- host: matching decomposition
+ * nx.max_weight_matching (graph_manager.py:64, inside GraphProcessor.getSubGraphs 57-83) without
+ * networkx: the blossom algorithm networkx 3.4.2 runs, in its visiting orders, so the same maximum
+ * matching comes back.  Host memory, no GPU.  Nodes are 0..n-1 in the graph's node order; node v's
+ * neighbours are adj[adj_off[v] .. adj_off[v+1]) in its adjacency order (each edge in both lists),
+ * adj_w their integer weights (NULL: all 1).  mate_out[v] = partner or -1; order_out[0..*n_order)
+ * = nodes in the order they first entered networkx's `mate` dict (its result set is built by
+ * iterating that dict). */
+int mx_max_weight_matching(int n, const int64_t* adj_off, const int32_t* adj, const int64_t* adj_w,
+                           int maxcardinality, int32_t* mate_out, int32_t* order_out, int* n_order);
+
 /* ---------------------------------------------------------------- utilities
  * splitmix64 -> fp32 uniform[-1,1) synthetic inputs, x[i] for counter i+1. */
 int mx_synth_fill(float* dst, int64_t n, uint64_t seed, void* stream);
