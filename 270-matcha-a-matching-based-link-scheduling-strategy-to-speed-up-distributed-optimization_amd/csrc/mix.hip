@@ -587,6 +587,87 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict
     }
 }
 
+// Wide kernel: any matching count and up to kWideMaxSlots slots (more workers per GPU, or more
+// remote partners, than the NS <= 64 kernels and their 32-matching plan records in LDS take).
+// A layout tile is worked in 256-column pieces; a piece of every needed slot is staged in dynamic
+// LDS (1 KB per slot), then each wave takes rows wave, wave + 4, ... and walks the row's partner
+// list, read with wave-uniform loads from the plan record in global memory, in matching order
+// with the self term last -- the same FMA chain as every other kernel.  One piece in flight per
+// workgroup (no prefetch): a correctness-first fallback, HBM-bound but not tuned.
+constexpr int kWideMaxSlots = 156;            // 156 KB of LDS at 256 columns per slot piece
+
+__global__ __launch_bounds__(kTPB) void mix_kernel_wide(float* const* __restrict__ seg_ptrs,
+                                                        const int64_t* __restrict__ seg_len,
+                                                        const int64_t* __restrict__ tile_off,
+                                                        const uint8_t* __restrict__ seg_vec, int nseg,
+                                                        int64_t total_tiles, int tile_cols, int n_slots,
+                                                        const int32_t* __restrict__ plan, int64_t iter,
+                                                        const int64_t* __restrict__ iter_dev, int n_local, int M,
+                                                        float alpha, int nontemporal) {
+    using F = typename VT<4>::type;
+    extern __shared__ F wlds[];               // [n_slots][64] float4
+    iter = round_of(iter, iter_dev);
+    if (iter < 0) return;
+    const int32_t* rec = plan + iter * mx::plan_words(n_local, M);
+    if (rec[0] == 0) return;                  // all flags zero
+    const int n_remote = rec[1];
+    const bool idle = rec[2] != 0;
+    const int32_t* deg = rec + mx::kPlanHeader;
+    const float* sw = reinterpret_cast<const float*>(deg + n_local);
+    const int32_t* src = deg + 2 * n_local;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int pieces = tile_cols / 256;
+    const int64_t work = total_tiles * pieces;
+    for (int64_t wi = blockIdx.x; wi < work; wi += gridDim.x) {
+        const int64_t tile = wi / pieces;
+        int lo = 0, hi = nseg;
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (tile_off[mid] <= tile) lo = mid; else hi = mid;
+        }
+        float* const* ptrs = seg_ptrs + (int64_t)lo * n_slots;
+        const int64_t col0 = (tile - tile_off[lo]) * tile_cols + (wi % pieces) * 256;
+        const int64_t lim = seg_len[lo];
+        const bool vec_ok = seg_vec[lo] != 0;
+        if (col0 >= lim) continue;            // block-uniform: the last tile's empty pieces
+        for (int q = threadIdx.x; q < n_slots * 64; q += kTPB) {
+            const int k = q >> 6;
+            const bool need = k < n_local ? (deg[k] > 0 || idle) : (k - n_local < n_remote);
+            if (!need) continue;
+            const int64_t c = col0 + (int64_t)(q & 63) * 4;
+            F v;
+            if (vec_ok && c + 4 <= lim) {
+                v = nontemporal ? ld<true, F>(ptrs[k] + c) : ld<false, F>(ptrs[k] + c);
+            } else {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) v[t] = (c + t < lim) ? ld1(ptrs[k] + c + t) : 0.0f;
+            }
+            wlds[q] = v;
+        }
+        __syncthreads();
+        for (int r = wave; r < n_local; r += kTPB / 64) {
+            const int d = __builtin_amdgcn_readfirstlane(deg[r]);
+            if (d == 0 && !idle) continue;
+            F a = F{0.0f, 0.0f, 0.0f, 0.0f};
+            for (int e = 0; e < d; ++e) {
+                const int sl = __builtin_amdgcn_readfirstlane(src[(int64_t)r * M + e]);
+                const F x = wlds[sl * 64 + lane];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) a[t] = __builtin_fmaf(alpha, x[t], a[t]);
+            }
+            const F xs = wlds[r * 64 + lane];
+            const float s = sw[r];
+#pragma unroll
+            for (int t = 0; t < 4; ++t) a[t] = __builtin_fmaf(s, xs[t], a[t]);
+            const int64_t c = col0 + (int64_t)lane * 4;
+            if (nontemporal) store_one<4, true>(ptrs[r], c, lim, vec_ok && c + 4 <= lim, a);
+            else store_one<4, false>(ptrs[r], c, lim, vec_ok && c + 4 <= lim, a);
+        }
+        __syncthreads();                      // the piece is read by every wave before restaging
+    }
+}
+
 struct Cfg {
     int vec, ns;
 };
@@ -596,6 +677,7 @@ Cfg pick(int n_slots) {
     if (n_slots <= 16) return {4, 16};
     if (n_slots <= 32) return {2, 32};
     if (n_slots <= 64) return {1, 64};
+    if (n_slots <= kWideMaxSlots) return {1, 0};    // wide kernel only (256-column layout tiles)
     return {0, 0};
 }
 
@@ -698,6 +780,7 @@ int launch_reg(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* ti
 
 extern "C" int mx_mix_tile(int n_slots) {
     const Cfg c = pick(n_slots);
+    if (c.vec > 0 && c.ns == 0) return kTPB;           // wide kernel: 256-column tiles
     return c.vec * kTPB * unroll_for(c.ns);
 }
 
@@ -756,10 +839,11 @@ extern "C" int mx_mix_get(const char* key) {
     return MX_ERR_INVALID;
 }
 
-// mirrors mx_gossip_mix's dispatch
+// mirrors mx_gossip_mix's dispatch (for M <= 32 matchings; more always take mix_kernel_wide)
 extern "C" const char* mx_mix_kernel_name(int n_slots) {
     const Cfg c = pick(n_slots);
     if (c.vec == 0) return "";
+    if (c.ns == 0) return "mix_kernel_wide";
     if ((g_tune.rows && c.ns >= 16) || (g_tune.rows == 2 && unroll_for(8) <= 2)) return "mix_kernel_rows";
     if (g_tune.regidx && c.ns == 8) return "mix_kernel_reg";
     return "mix_kernel";
@@ -768,7 +852,7 @@ extern "C" const char* mx_mix_kernel_name(int n_slots) {
 extern "C" int mx_mix_layout(const int64_t* seg_len_host, int nseg, int n_slots, int64_t* tile_off_host) {
     MX_CHECK(seg_len_host && tile_off_host && nseg >= 1, "mx_mix_layout: bad arguments");
     const int tile = mx_mix_tile(n_slots);
-    MX_CHECK(tile > 0, "mx_mix_layout: n_slots=%d exceeds 64", n_slots);
+    MX_CHECK(tile > 0, "mx_mix_layout: n_slots=%d exceeds %d", n_slots, kWideMaxSlots);
     tile_off_host[0] = 0;
     for (int s = 0; s < nseg; ++s) {
         MX_CHECK(seg_len_host[s] >= 0, "mx_mix_layout: negative length");
@@ -840,12 +924,30 @@ int gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev, const int
              "mx_gossip_mix: null pointer");
     MX_CHECK(nseg >= 1 && n_local >= 1 && n_slots >= n_local, "mx_gossip_mix: nseg=%d n_local=%d n_slots=%d",
              nseg, n_local, n_slots);
-    MX_CHECK(M >= 1 && M <= kMaxM, "mx_gossip_mix: M=%d outside [1, %d]", M, kMaxM);
+    MX_CHECK(M >= 1, "mx_gossip_mix: M=%d", M);
     MX_CHECK(iter >= 0, "mx_gossip_mix: iter < 0");
     const Cfg c = pick(n_slots);
-    MX_CHECK(c.vec > 0, "mx_gossip_mix: n_slots=%d exceeds 64", n_slots);
+    MX_CHECK(c.vec > 0, "mx_gossip_mix: n_slots=%d exceeds %d", n_slots, kWideMaxSlots);
     hipStream_t st = mx::as_stream(stream);
     if (total_tiles <= 0) return MX_OK;
+    if (c.ns == 0 || M > kMaxM) {             // wide kernel: > 64 slots or > 32 matchings
+        const int tile_cols = mx_mix_tile(n_slots);
+        const int64_t work = total_tiles * (tile_cols / kTPB);
+        const size_t lds = (size_t)n_slots * 64 * sizeof(float) * 4;
+        static bool lds_set = false;
+        if (!lds_set) {                       // > 64 KB of dynamic LDS (gfx950: 160 KB per CU)
+            MX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mix_kernel_wide),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kWideMaxSlots * 1024));
+            lds_set = true;
+        }
+        int64_t grid = (int64_t)cu_count() * (lds <= 32768 ? 4 : lds <= 80000 ? 2 : 1);
+        if (grid > work) grid = work;
+        hipLaunchKernelGGL(mix_kernel_wide, dim3((unsigned)(grid < 1 ? 1 : grid)), dim3(kTPB), lds, st, seg_ptrs_dev,
+                           seg_len_dev, tile_off_dev, seg_vec_dev, nseg, total_tiles, tile_cols, n_slots, plan_dev, iter,
+                           iter_dev, n_local, M, alpha, g_tune.nontemporal);
+        MX_LAUNCH_CHECK();
+        return MX_OK;
+    }
     const int key = (g_tune.nontemporal ? 1 : 0) | (g_tune.prefetch ? 2 : 0);
 #define MX_ARGS seg_ptrs_dev, seg_len_dev, tile_off_dev, seg_vec_dev, nseg, n_slots, plan_dev, iter, \
                 iter_dev, n_local, M, alpha, total_tiles, st

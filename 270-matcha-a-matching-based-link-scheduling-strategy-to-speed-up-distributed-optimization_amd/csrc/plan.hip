@@ -15,7 +15,7 @@
 #include "mx_common.h"
 
 namespace {
-constexpr int kMaxRemote = 64;                 // the mixing kernels take at most 64 slots
+constexpr int kMaxRemote = 156;                // the mixing kernels take at most 156 slots
 
 __global__ __launch_bounds__(256) void plan_kernel(const uint8_t* __restrict__ flags, int64_t T,
                                                    int M, const int32_t* __restrict__ partner,
@@ -30,7 +30,7 @@ __global__ __launch_bounds__(256) void plan_kernel(const uint8_t* __restrict__ f
     int32_t* sw = deg + n_local;
     int32_t* src = sw + n_local;
     for (int r = 0; r < n_local; ++r) deg[r] = 0;
-    int any = 0, remote = 0;
+    int any = 0, remote = 0, overflow = 0;
     int32_t who[kMaxRemote];                   // slab slot -> remote worker (first appearance)
     for (int g = 0; g < M; ++g) {
         if (!f[g]) continue;
@@ -46,7 +46,13 @@ __global__ __launch_bounds__(256) void plan_kernel(const uint8_t* __restrict__ f
             } else {
                 int k = 0;
                 while (k < remote && who[k] != p) ++k;
-                if (k == remote) who[remote++] = p;
+                if (k == remote) {
+                    if (remote == kMaxRemote) {    // more distinct remote partners than any kernel
+                        overflow = 1;              // takes: flagged in word [3], row left out
+                        continue;
+                    }
+                    who[remote++] = p;
+                }
                 slot = n_local + k;
             }
             src[r * M + deg[r]] = slot;
@@ -56,7 +62,7 @@ __global__ __launch_bounds__(256) void plan_kernel(const uint8_t* __restrict__ f
     rec[0] = any;
     rec[1] = remote;
     rec[2] = 0;                                // idle rows skipped (mx_plan_set_idle)
-    rec[3] = 0;
+    rec[3] = overflow;
     for (int r = 0; r < n_local; ++r) {
         const double s = 1.0 - (double)deg[r] * alpha;  // Python float arithmetic, then f32
         const float s32 = (float)s;

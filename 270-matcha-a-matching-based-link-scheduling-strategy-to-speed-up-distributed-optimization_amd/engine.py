@@ -209,10 +209,9 @@ class GossipEngine:
             raise ValueError("workers outside this block have partners inside it: an RCCL "
                              "communicator is required")
         self.n_slots = self.n_local + self.max_remote
-        if self.n_slots > 64:
-            raise MXError(f"{self.n_slots} slots per GPU exceed the mixing kernel's 64")
-        if self.M > 32:
-            raise MXError(f"{self.M} matchings exceed the mixing kernel's 32")
+        if lib.mx_mix_tile(self.n_slots) <= 0:   # 1-64 slots: tuned kernels; 65-156: mix_kernel_wide
+            raise MXError(f"{self.n_slots} slots per GPU (local workers + distinct remote partners) exceed "
+                          "the 156 a mixing tile holds in LDS: spread the workers over more GPUs")
         self.plan_words = int(lib.mx_plan_words(self.n_local, self.M))
         self.partner_dev = torch.from_numpy(self.partner).to("cuda")
         self.plan = torch.empty(max(1, self.T) * self.plan_words, dtype=torch.int32, device="cuda")

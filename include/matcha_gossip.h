@@ -64,7 +64,8 @@ int mx_flags_binomial_sequential(const uint32_t* key_in, int pos_in, const doubl
  *   owner_dev    int32 [n_global]      rank owning each worker; NULL = all local
  *   plan_dev     int32 [T][mx_plan_words(n_local, M)]
  * Plan record layout (int32 words): [0] any flag set, [1] n_remote, [2] idle-row mode
- *   (mx_plan_set_idle; 0 after mx_plan_build), [3] reserved,
+ *   (mx_plan_set_idle; 0 after mx_plan_build), [3] 1 if the round has more than 155 distinct
+ *   remote partners (not representable; callers size n_slots <= 156 beforehand),
  *   [4, 4+n_local) degree, [4+n_local, 4+2n_local) selfweight (f32 bits),
  *   [4+2n_local + r*M + e] source slot of row r's e-th partner (slot < n_local: local row,
  *   slot >= n_local: receive slab row slot - n_local).
@@ -98,7 +99,9 @@ int mx_plan_set_idle(int32_t* plan_dev, int64_t T, int n_local, int M, int mode,
  *                 total_tiles = tile_off[nseg] (host copy, sizes the grid)
  *   seg_vec_dev   uint8 [nseg]: 1 if every slot pointer of that tensor is 16-byte aligned
  *   plan_dev      plan table from mx_plan_build; iter selects the record
- * Rows with degree 0 are neither read nor written.  No-op when the record's flags are all 0.
+ * Rows with degree 0 are neither read nor written (unless mx_plan_set_idle asked for the
+ * reference's 0 + 1.0 * x).  No-op when the record's flags are all 0.  1-156 slots (> 64, or
+ * M > 32 matchings: the untuned mix_kernel_wide); mx_mix_tile returns 0 above that.
  */
 int mx_mix_tile(int n_slots);
 /* Tuning knobs of the mixing kernel (process-wide), by name:
@@ -121,7 +124,9 @@ int mx_mix_tile(int n_slots);
  * "unroll" changes the tile size: rebuild layouts (mx_mix_layout) after setting it.
  * mx_mix_get returns the current value (negative on an unknown key).
  * mx_mix_kernel_name: the kernel mx_gossip_mix launches for n_slots under the current knobs
- * ("mix_kernel_rows", "mix_kernel_reg", "mix_kernel"; "" when n_slots > 64). */
+ * ("mix_kernel_rows", "mix_kernel_reg", "mix_kernel" for <= 64 slots and <= 32 matchings;
+ * "mix_kernel_wide" for 65-156 slots -- also used for any slot count when M > 32; "" when
+ * n_slots > 156). */
 int mx_mix_set(const char* key, int value);
 int mx_mix_get(const char* key);
 const char* mx_mix_kernel_name(int n_slots);

@@ -1,0 +1,93 @@
+"""Wide layouts: more than 64 slots per GPU or more than 32 matchings (the 64-slot /
+32-matching hard caps).  mix_kernel_wide takes 65-156 slots and any matching count; bit-exact vs
+the oracle on ER topologies decomposed by the host path, 1 process and 2-3 loopback ranks, plus
+ChocoSGD on 96 workers."""
+import random
+
+import numpy as np
+import pytest
+
+from conftest import LoopbackHub, Topo
+
+torch = pytest.importorskip("torch")
+pytestmark = pytest.mark.gpu
+
+
+def _er(pkg, n, p, seed):
+    random.seed(0)
+    gp = pkg.GraphProcessor(pkg.erdos_renyi(n, p, seed), 1.0, 0, n, 4, False)
+    return np.asarray(gp.neighbors_info, np.int32)
+
+
+@pytest.mark.parametrize("n,p,seed,P", [(96, 0.06, 1, 9_001), (128, 0.05, 2, 5_000), (150, 0.04, 3, 3_001),
+                                        (48, 0.9, 4, 7_777), (24, 0.3, 5, 1_000)])
+@pytest.mark.parametrize("idle_rows", ["skip", "canonical"])
+def test_wide_slots_and_matchings(pkg, O, n, p, seed, P, idle_rows):
+    partner = _er(pkg, n, p, seed)
+    M = partner.shape[0]
+    rng = np.random.RandomState(seed)
+    flags = (rng.uniform(size=(4, M)) < 0.5).astype(np.uint8)
+    flags[0] = 1
+    topo = Topo(partner, 0.5 / M, flags)
+    grp = pkg.VirtualWorkerGroup(topo, numel=P, idle_rows=idle_rows)
+    wide = n > 64 or M > 32
+    if wide:
+        assert grp.engine.n_slots > 64 or M > 32
+    X = np.stack([O.synth(17 * seed + i, P) for i in range(n)])
+    grp.rows.copy_(torch.from_numpy(X))
+    for f in flags:
+        grp.communicate()
+        X = O.decen_round(X, partner, f, topo.neighbor_weight)
+    got = grp.rows.cpu().numpy()          # (synth has no -0.0: "skip" idle rows equal the oracle too)
+    assert np.array_equal(got.view(np.uint32), X.view(np.uint32))
+
+
+@pytest.mark.parametrize("nranks", [2, 3])
+def test_wide_multirank_loopback(pkg, O, nranks):
+    """150 workers over 2-3 ranks: local rows + many remote slab slots per rank."""
+    n, P = 150, 4_097
+    partner = _er(pkg, n, 0.04, 9)
+    M = partner.shape[0]
+    rng = np.random.RandomState(3)
+    flags = (rng.uniform(size=(3, M)) < 0.6).astype(np.uint8)
+    flags[0] = 1
+    topo = Topo(partner, 0.3 / M, flags)
+    hub = LoopbackHub(nranks)
+    groups = [pkg.VirtualWorkerGroup(topo, numel=P, rank=r, nranks=nranks, comm=hub.comm(r)) for r in range(nranks)]
+    assert max(g.engine.n_slots for g in groups) > 64
+    X = np.stack([O.synth(300 + i, P) for i in range(n)])
+    for g in groups:
+        g.rows.copy_(torch.from_numpy(X[g.row_base:g.row_base + g.n_local]))
+        hub.register(g.row_base, g._row_ptrs)
+    for it, f in enumerate(flags):
+        for g in groups:
+            g.step(it)
+        torch.cuda.synchronize()
+        X = O.decen_round(X, partner, f, topo.neighbor_weight)
+    got = np.concatenate([g.rows.cpu().numpy() for g in groups])
+    assert np.array_equal(got.view(np.uint32), X.view(np.uint32))
+
+
+def test_wide_choco(pkg, O):
+    n, P, ratio = 96, 20_011, 0.9
+    partner = _er(pkg, n, 0.06, 1)
+    M = partner.shape[0]
+    flags = np.ones((2, M), np.uint8)
+    flags[1, ::2] = 0
+    topo = Topo(partner, 0.5 / M, flags)
+    grp = pkg.ChocoWorkerGroup(topo, numel=P, ratio=ratio, consensus_lr=0.2)
+    X = np.stack([O.synth(40 + i, P) for i in range(n)])
+    XH, S = np.zeros_like(X), np.zeros_like(X)
+    grp.rows.copy_(torch.from_numpy(X))
+    k = O.topk_k(P, ratio)
+    for f in flags:
+        grp.communicate()
+        O.choco_round(X, XH, S, partner, f, topo.neighbor_weight, k, 0.2)
+    assert np.array_equal(grp.rows.cpu().numpy().view(np.uint32), X.view(np.uint32))
+
+
+def test_slot_limit_message(pkg):
+    partner = _er(pkg, 160, 0.05, 5)
+    topo = Topo(partner, 0.01, np.ones((2, partner.shape[0]), np.uint8))
+    with pytest.raises(pkg.MXError, match="156"):
+        pkg.VirtualWorkerGroup(topo, numel=100)
