@@ -21,9 +21,23 @@ import time
 import numpy as np
 
 
-def trace_gaps(path):
-    rows = [r for r in csv.DictReader(open(path)) if "mix_kernel" in r["Kernel_Name"]]
-    rows.sort(key=lambda r: int(r["Start_Timestamp"]))
+def trace_gaps(path, K=20):
+    """All mixing launches of a kernel trace, and bench.py's timed region: the last K launches of
+    the headline kernel before the first launch of the self-check replay (the 64-column round
+    kernel, mix_kernel_rows<8, 256, ...>), which bench.py runs right after the timed rounds."""
+    allrows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
+    names = [r["Kernel_Name"] for r in allrows]
+    replay = [i for i, nm in enumerate(names) if "mix_kernel_rows<8, 256" in nm]
+    timed = None
+    if replay:
+        head = [r for r in allrows[:replay[0]] if "mix_kernel_rows<8, 1024" in r["Kernel_Name"]][-K:]
+        if len(head) == K:
+            st = np.array([int(r["Start_Timestamp"]) for r in head], np.int64)
+            en = np.array([int(r["End_Timestamp"]) for r in head], np.int64)
+            timed = {"launches": K, "kernel_us_mean": float(((en - st) / 1e3).mean()),
+                     "gaps_us": [round(float(g), 3) for g in (st[1:] - en[:-1]) / 1e3],
+                     "span_us_per_round": float((en[-1] - st[0]) / 1e3 / K)}
+    rows = [r for r in allrows if "mix_kernel" in r["Kernel_Name"]]
     st = np.array([int(r["Start_Timestamp"]) for r in rows], np.int64)
     en = np.array([int(r["End_Timestamp"]) for r in rows], np.int64)
     dur = (en - st) / 1e3
@@ -32,7 +46,10 @@ def trace_gaps(path):
     print(json.dumps({"launches": len(rows), "dur_us_median": float(np.median(dur)), "dur_us_min": float(dur.min()),
                       "gap_us_median": float(np.median(gap)) if len(gap) else None,
                       "gap_us_p10_p90": [float(np.percentile(gap, 10)), float(np.percentile(gap, 90))] if len(gap) else None,
-                      "gaps_counted": int(len(gap))}))
+                      "gaps_counted": int(len(gap)), "timed_region": timed,
+                      "note": "all mixing launches incl. per-round-event diagnostic blocks (events between "
+                              "launches) and the 64-column self-check replay; timed_region = bench.py's K "
+                              "back-to-back rounds"}))
 
 
 def main():
