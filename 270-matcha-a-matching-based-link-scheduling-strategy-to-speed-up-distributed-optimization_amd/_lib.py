@@ -58,6 +58,11 @@ SIGNATURES = {
     "mx_mean_rows": (c_int, [c_p, c_int, c_i64, c_i64, c_int, c_p, c_p]),
     "mx_synth_fill": (c_int, [c_p, c_i64, c_u64, c_p]),
     "mx_max_weight_matching": (c_int, [c_int, c_p, c_p, c_p, c_int, c_p, c_p, c_p]),
+    "mx_ipc_handle_bytes": (c_int, []),
+    "mx_ipc_alloc": (c_int, [c_i64, c_p, c_p]),
+    "mx_ipc_open": (c_int, [c_p, c_p]),
+    "mx_ipc_close": (c_int, [c_p]),
+    "mx_ipc_free": (c_int, [c_p]),
 }
 
 

@@ -259,3 +259,51 @@ extern "C" int mx_allreduce_mean_ordered(void* comm_v, float* buf, int64_t count
     if (rc != MX_OK) return rc;
     return mx_mean_rows(gather, nranks, count, count, order, buf, stream);
 }
+
+// ---------------------------------------------------------------------------------- pull transport
+// Device buffers shared between the processes of one node (one per GPU): each rank publishes a
+// snapshot of its rows in a buffer of its own, the peers map it (IPC, dmabuf) and the mixing
+// kernel reads a partner's row straight from the peer's HBM over xGMI -- no RCCL FIFO copies,
+// no receive slab.  See engine.PullTransport for the round protocol (double-buffered snapshots,
+// one barrier per round).
+static_assert(sizeof(hipIpcMemHandle_t) == 64, "hipIpcMemHandle_t is expected to be 64 bytes");
+
+extern "C" int mx_ipc_handle_bytes(void) { return (int)sizeof(hipIpcMemHandle_t); }
+
+extern "C" int mx_ipc_alloc(int64_t bytes, void** ptr_out, void* handle_out) {
+    MX_CHECK(bytes > 0 && ptr_out && handle_out, "mx_ipc_alloc: bad arguments");
+    void* p = nullptr;
+    MX_HIP(hipMalloc(&p, (size_t)bytes));
+    hipIpcMemHandle_t h;
+    const hipError_t e = hipIpcGetMemHandle(&h, p);
+    if (e != hipSuccess) {
+        (void)hipFree(p);
+        mx::set_error("mx_ipc_alloc: hipIpcGetMemHandle -> %s", hipGetErrorString(e));
+        return MX_ERR_HIP;
+    }
+    memcpy(handle_out, &h, sizeof(h));
+    *ptr_out = p;
+    return MX_OK;
+}
+
+extern "C" int mx_ipc_open(const void* handle, void** ptr_out) {
+    MX_CHECK(handle && ptr_out, "mx_ipc_open: bad arguments");
+    hipIpcMemHandle_t h;
+    memcpy(&h, handle, sizeof(h));
+    void* p = nullptr;
+    MX_HIP(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+    *ptr_out = p;
+    return MX_OK;
+}
+
+extern "C" int mx_ipc_close(void* ptr) {
+    if (!ptr) return MX_OK;
+    MX_HIP(hipIpcCloseMemHandle(ptr));
+    return MX_OK;
+}
+
+extern "C" int mx_ipc_free(void* ptr) {
+    if (!ptr) return MX_OK;
+    MX_HIP(hipFree(ptr));
+    return MX_OK;
+}

@@ -117,6 +117,88 @@ class RcclComm:
             self.handle = None
 
 
+class PullTransport:
+    """Cross-GPU partner rows without RCCL: every rank publishes a snapshot of its rows in an
+    IPC-shared device buffer (mx_ipc_alloc); its peers map it (mx_ipc_open) and their mixing
+    kernel reads the partner rows straight from this GPU's HBM over xGMI (communicator.py:110's
+    sendrecv becomes a remote load inside the FMA chain).  Round protocol (VirtualWorkerGroup):
+        1. copy the local rows into snapshot buffer `round % 2` (local HBM copy);
+        2. synchronize + barrier: every rank's snapshot of this round is complete;
+        3. point the receive slots of this round's plan at the peers' snapshot rows and mix.
+    Snapshots alternate between two buffers, so round r+1's copy never overwrites what a slower
+    peer still reads in round r; round r+2's copy comes after round r+1's barrier, which every
+    rank passes only once its round-r mix has finished.  Needs one process per GPU of ONE node
+    (the peers' HBM must be mappable) -- or, for tests, several processes sharing a GPU.
+    Bootstrap and barrier use torch.distributed (any backend)."""
+
+    handle = None
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        require_device()
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.nranks = dist.get_world_size(group)
+
+    def bind(self, vwg):
+        """Collective: allocate vwg's snapshot buffer, exchange handles, map the peers'.  Every
+        rank takes part in every exchange even when its own step failed, and all ranks raise
+        together (MXError) if any failed, so a refusal on one GPU cannot leave the others waiting."""
+        import torch.distributed as dist
+        hb = int(lib.mx_ipc_handle_bytes())
+        half = vwg.n_local * vwg.ld * 4
+        own = ctypes.c_void_p()
+        handle = (ctypes.c_char * hb)()
+        err = None
+        try:
+            check(lib.mx_ipc_alloc(2 * half, ctypes.byref(own), ctypes.cast(handle, ctypes.c_void_p)), "mx_ipc_alloc")
+        except MXError as e:
+            err = str(e)
+        objs = [None] * self.nranks
+        dist.all_gather_object(objs, (self.rank, None if err else bytes(handle)), group=self.group)
+        peers = [0] * self.nranks
+        opened = []
+        if err is None and all(h is not None for _, h in objs):
+            try:
+                for r, h in objs:
+                    if r == self.rank:
+                        peers[r] = own.value
+                        continue
+                    buf = (ctypes.c_char * hb).from_buffer_copy(h)
+                    p = ctypes.c_void_p()
+                    check(lib.mx_ipc_open(ctypes.cast(buf, ctypes.c_void_p), ctypes.byref(p)), "mx_ipc_open")
+                    peers[r] = p.value
+                    opened.append(p.value)
+            except MXError as e:
+                err = str(e)
+        elif err is None:
+            err = "a peer could not allocate its snapshot buffer"
+        oks = [None] * self.nranks
+        dist.all_gather_object(oks, err, group=self.group)
+        bad = [(r, e) for r, e in enumerate(oks) if e is not None]
+        if bad:
+            for p in opened:
+                lib.mx_ipc_close(p)
+            if own.value:
+                lib.mx_ipc_free(own.value)
+            raise MXError(f"pull transport unavailable: rank {bad[0][0]}: {bad[0][1]}")
+        return _PullState(self, own.value, peers, opened, half)
+
+
+class _PullState:
+    def __init__(self, transport, own, peers, opened, half):
+        self.transport, self.own, self.peers, self.opened, self.half = transport, own, peers, opened, half
+        self.round = 0
+
+    def close(self):
+        for p in self.opened:
+            lib.mx_ipc_close(p)
+        self.opened = []
+        if self.own:
+            lib.mx_ipc_free(self.own)
+            self.own = 0
+
+
 _DEFAULT_COMM = None
 
 
@@ -360,7 +442,9 @@ class VirtualWorkerGroup:
         self.arena = torch.zeros((self.n_local, self.ld), dtype=torch.float32, device="cuda")
         # column pipelining of the cross-GPU exchange (N > 1): chunk c+1 travels over RCCL on a side
         # stream while chunk c is mixed; the receive slab is two chunk-wide buffers
-        self.chunked = bool(self.engine.max_remote and chunk_cols and int(chunk_cols) < self.numel)
+        self._pull = None
+        self.chunked = bool(self.engine.max_remote and chunk_cols and int(chunk_cols) < self.numel
+                            and not isinstance(comm, PullTransport))
         if self.chunked:
             W = (int(chunk_cols) + ROW_ALIGN - 1) // ROW_ALIGN * ROW_ALIGN
             self.chunk_w = W
@@ -369,7 +453,7 @@ class VirtualWorkerGroup:
             self.comm_stream = torch.cuda.Stream()
         else:
             self.slab = (torch.empty((self.engine.max_remote, self.ld), dtype=torch.float32, device="cuda")
-                         if self.engine.max_remote else None)
+                         if self.engine.max_remote and not isinstance(comm, PullTransport) else None)
         if models is not None:
             for r, m in enumerate(models):
                 off = 0
@@ -392,6 +476,16 @@ class VirtualWorkerGroup:
                 self.chunk_layouts.append(Layout([c1 - c0], ptrs, self.engine.n_slots))
             self.layout = Layout([self.numel], [[p] for p in self._row_ptrs] +
                                  [[self.slab[0, 0].data_ptr()]] * self.engine.max_remote, self.engine.n_slots)
+        elif isinstance(comm, PullTransport):
+            # receive slots point at the peers' snapshot rows, set per round (_step_pull); no slab
+            self._pull = comm.bind(self)
+            self._pull_table = np.zeros((1, self.engine.n_slots), np.int64)
+            self._pull_table[0, :self.n_local] = self._row_ptrs
+            self._pull_table[0, self.n_local:] = self._pull.own
+            self.layout = Layout([self.numel], [[int(p)] for p in self._pull_table[0]], self.engine.n_slots)
+            self._pull_seg = torch.tensor([self.arena.data_ptr()], dtype=torch.int64, device="cuda")
+            self._pull_off = torch.tensor([0, self.n_local * self.ld], dtype=torch.int64, device="cuda")
+            self._blocks = partition(n, nranks)
         else:
             slot_ptrs = [[p] for p in self._row_ptrs]
             if self.slab is not None:
@@ -409,12 +503,46 @@ class VirtualWorkerGroup:
             return False
         if self.chunked:
             return self._step_chunked(it, stream)
+        if self._pull is not None:
+            return self._step_pull(it, stream)
         if self.engine.comm is not None:
             self.engine.exchange(it, self._row_ptrs,
                                  self.slab.data_ptr() if self.slab is not None else None,
                                  self.ld * 4, self.numel * 4, stream)
         self.engine.mix(it, self.layout, stream)
         return True
+
+    def _step_pull(self, it, stream=None):
+        """PullTransport round: snapshot, barrier, receive slots -> peers' snapshots, mix."""
+        import torch.distributed as dist
+        st = self._pull
+        par = st.round & 1
+        st.round += 1
+        total = self.n_local * self.ld
+        check(lib.mx_gather(self._pull_seg.data_ptr(), self._pull_off.data_ptr(), 1, total, st.own + par * st.half,
+                            stream_ptr(stream)), "mx_gather")
+        torch.cuda.synchronize()
+        dist.barrier(group=st.transport.group)
+        eng = self.engine
+        table = self._pull_table
+        for kind, peer, idx, who in eng.exchange_plan(it):
+            if kind == 1:
+                owner = int(eng.owner[who])
+                base, n_loc = self._blocks[owner]
+                table[0, self.n_local + int(idx)] = (st.peers[owner] + par * n_loc * self.ld * 4 +
+                                                     (int(who) - base) * self.ld * 4)
+        self.layout.seg_ptrs.copy_(torch.from_numpy(table), non_blocking=False)
+        if stream is not None:
+            stream.wait_stream(torch.cuda.current_stream())
+        eng.mix(it, self.layout, stream)
+        return True
+
+    def close(self):
+        """Release the pull transport's shared buffers (collective use ends; see PullTransport)."""
+        if self._pull is not None:
+            torch.cuda.synchronize()
+            self._pull.close()
+            self._pull = None
 
     def _step_chunked(self, it, stream=None):
         cur = stream if stream is not None else torch.cuda.current_stream()

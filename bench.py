@@ -53,6 +53,9 @@ def parse():
                     help="N > 1: column-pipelined exchange (RCCL on a side stream overlapped with mixing; "
                          "VirtualWorkerGroup chunk_cols) -- auto: time both forms over a few untimed rounds and "
                          "use the faster for the timed region; on / off: force")
+    ap.add_argument("--pull", choices=("auto", "on", "off"), default="auto",
+                    help="N > 1: also calibrate the pull transport (partner rows read from the peers' IPC-mapped "
+                         "HBM by the mixing kernel) and time it if fastest (auto), force it (on) or skip it (off)")
     ap.add_argument("--chunk-cols", type=int, default=0, help="pipelined chunk width (0: a quarter of the row)")
     ap.add_argument("--placement", choices=("auto", "contiguous"), default="auto",
                     help="N > 1: which workers share a GPU -- auto (placement.best_placement, fewest rows "
@@ -402,11 +405,10 @@ def main():
     timed, overlap = group, None
     any_remote = world > 1 and max_over_ranks(float(group.engine.max_remote), world, dev) > 0   # collective
     base_it = W + DMAX + 2 * K
+    forms = {"rccl": group}
     if any_remote and args.overlap != "off":
         # column pipelining: chunk c+1 of every exchanged row travels on a side stream while chunk c
-        # is mixed (bit-identical results).  Whether it pays depends on the link rate vs the extra
-        # RCCL groups per round, so with "auto" both forms run R untimed rounds and the faster one
-        # (max over ranks, so every rank picks the same) is the one timed.
+        # is mixed (bit-identical results)
         C = args.chunk_cols or ((P + 3) // 4 + 63) // 64 * 64
         gchunk = pkg.VirtualWorkerGroup(GP, numel=P, rank=rank, nranks=world, comm=comm, placement=args.placement,
                                         chunk_cols=C)
@@ -414,7 +416,25 @@ def main():
             pkg._lib.check(pkg.lib.mx_synth_fill(gchunk.rows[r].data_ptr(), P, 1234 + gchunk.workers[r], None))
         for it in range(W):
             run(gchunk, it)
-
+        run(gchunk, base_it)                     # first chunked round (side stream, events) untimed
+        forms["rccl_chunked"] = gchunk
+    pull_err = None
+    if any_remote and args.pull != "off":
+        # the pull transport: partner rows read straight from the peers' HBM (IPC-mapped
+        # snapshots) by the mixing kernel -- no RCCL copies; collective setup, all ranks agree
+        try:
+            gpull = pkg.VirtualWorkerGroup(GP, numel=P, rank=rank, nranks=world, comm=pkg.PullTransport(),
+                                           placement=args.placement)
+            for r in range(gpull.n_local):
+                pkg._lib.check(pkg.lib.mx_synth_fill(gpull.rows[r].data_ptr(), P, 1234 + gpull.workers[r], None))
+            for it in range(W):
+                run(gpull, it)
+            forms["pull"] = gpull
+        except pkg.MXError as e:
+            pull_err = str(e)
+    if len(forms) > 1:
+        # every form runs R untimed rounds; the fastest (max over ranks, so every rank picks the
+        # same) is the one timed -- unless one is forced (--overlap on / --pull on)
         def calib(g, first):
             torch.cuda.synchronize()
             dist.barrier()
@@ -425,18 +445,27 @@ def main():
             dist.barrier()
             return max_over_ranks((time.perf_counter() - t) / R, world, dev)
 
-        run(gchunk, base_it)                     # first chunked round (side stream, events) untimed
-        t_plain = calib(group, base_it) if args.overlap == "auto" else None
-        t_chunk = calib(gchunk, base_it + 1)
-        use_chunk = args.overlap == "on" or t_chunk < t_plain
-        overlap = {"mode": args.overlap, "chunk_cols": C, "chunks": len(getattr(gchunk, "chunks", [None])),
-                   "calib_ms_unchunked": 1e3 * t_plain if t_plain else None, "calib_ms_chunked": 1e3 * t_chunk,
-                   "chosen": "chunked" if use_chunk else "unchunked",
-                   "note": f"{R} untimed rounds per form before the timed region, max over ranks"}
-        if use_chunk:
-            timed = gchunk
+        calib_ms = {name: 1e3 * calib(g, base_it + 1) for name, g in forms.items()}
+        if args.pull == "on" and "pull" in forms:
+            chosen = "pull"
+        elif args.overlap == "on" and "rccl_chunked" in forms:
+            chosen = "rccl_chunked"
         else:
-            del gchunk
+            chosen = min(calib_ms, key=calib_ms.get)
+        timed = forms[chosen]
+        overlap = {"mode": args.overlap, "pull": args.pull, "chunk_cols": C if "rccl_chunked" in forms else None,
+                   "chunks": len(forms["rccl_chunked"].chunks) if "rccl_chunked" in forms else None,
+                   "calib_ms": calib_ms, "calib_ms_unchunked": calib_ms.get("rccl"),
+                   "calib_ms_chunked": calib_ms.get("rccl_chunked"), "chosen_form": chosen,
+                   "chosen": "chunked" if chosen == "rccl_chunked" else "unchunked",
+                   "pull_unavailable": pull_err,
+                   "note": f"{R} untimed rounds per exchange form before the timed region, max over ranks"}
+        for name in list(forms):
+            if forms[name] is not timed and forms[name] is not group:
+                forms[name].close()
+                del forms[name]
+    elif pull_err is not None:
+        overlap = {"pull_unavailable": pull_err}
     # per-round HIP events of the whole round (diagnostic): real rounds run BEFORE the timed region,
     # in blocks of K, for at least --settle-ms (an idle MI355X takes ~10 ms of streaming to reach
     # its steady clocks: tools/ramp.py), so the timed rounds measure the steady state of the loop
@@ -596,7 +625,8 @@ def main():
                        "workers": n, "params_per_worker": P, "graph": args.graph, "budget": args.budget,
                        "parallelism": f"{n} workers over {world} GPU(s)" +
                                       (f", placement {args.placement}" if world > 1 else "") +
-                                      (", column-pipelined exchange" if timed is not group else ""),
+                                      (f", exchange form {overlap['chosen_form']}" if overlap and
+                                       overlap.get("chosen_form") else ""),
                        "placement": group.placement if world > 1 else None,
                        "transport": args.transport if world > 1 else None},
             "parity_ok": parity_ok,
@@ -660,6 +690,8 @@ def main():
         print(json.dumps(out))
     if world > 1:
         dist.barrier()
+        timed.close()                            # the pull transport's shared buffers, if any
+        group.close()
         if not gloo:
             comm.close()
         dist.destroy_process_group()

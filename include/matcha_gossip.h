@@ -256,6 +256,18 @@ int mx_exchange_round(void* comm, const uint8_t* flags_row, int M, const int32_t
                       int n_global, const int32_t* owner, int my_rank, int row_base, int n_local,
                       void* const* rows, void* slab, int64_t slab_ld_bytes, int64_t row_bytes,
                       int* n_remote_out, void* stream);
+/* Pull transport (one process per GPU of a node): device buffers shared through IPC handles
+ * (64 bytes, mx_ipc_handle_bytes).  A rank publishes snapshots of its rows in an mx_ipc_alloc
+ * buffer and sends the handle to its peers (any host channel); a peer mx_ipc_open's it and the
+ * mixing kernel reads the partner rows straight from the owner's HBM over xGMI, in place of
+ * comm.sendrecv (communicator.py:110).  mx_ipc_close unmaps a peer buffer, mx_ipc_free releases
+ * one's own. */
+int mx_ipc_handle_bytes(void);
+int mx_ipc_alloc(int64_t bytes, void** ptr_out, void* handle_out);
+int mx_ipc_open(const void* handle, void** ptr_out);
+int mx_ipc_close(void* ptr);
+int mx_ipc_free(void* ptr);
+
 /* centralizedCommunicator.averaging (communicator.py:56-67): buf = allreduce_sum(buf) / size.
  * mx_allreduce_mean: RCCL's all-reduce (ring / tree order of RCCL's choosing), then the division;
  *   equal to the reference within fp32 reassociation (1e-6 relative for well-conditioned sums).

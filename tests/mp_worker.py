@@ -51,6 +51,7 @@ def decen_case(pkg, T, gid, P, rounds, chunk_cols=None, seed=5, placement=None):
         if flags[it].any():
             X = O.decen_round(X, topo.neighbors_info, flags[it], 0.21)
     got = by_worker(grp, gather_rows(grp.rows, grp.row_base, n))
+    grp.close()
     return bool(np.array_equal(got.view(np.uint32), X.view(np.uint32)))
 
 
@@ -121,6 +122,10 @@ def main():
         "decen_g2_placed": decen_case(pkg, T, 2, 9_001, 4, placement="auto"),
         "choco_g0_placed": choco_case(pkg, T, 20_011, 0.9, 3, placement="auto"),
         "centralized": centralized_case(pkg, T),
+        # the pull transport: peers map each rank's IPC-shared snapshot buffer and the mixing
+        # kernel reads partner rows from it (processes share GPU 0 here; xGMI on a real node)
+        "decen_g0_pull": decen_case(pkg, pkg.PullTransport(), 0, 30_011, 6),
+        "decen_g2_pull_placed": decen_case(pkg, pkg.PullTransport(), 2, 9_001, 5, placement="auto"),
     }
     torch.cuda.synchronize()
     if dist.get_rank() == 0:

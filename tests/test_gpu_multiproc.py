@@ -61,18 +61,25 @@ def test_bench_multiprocess_path():
     assert len(out["xgmi"]["exchange_only_ms_per_rank"]) == 2
 
 
-@pytest.mark.parametrize("nproc,overlap", [(2, "on"), (4, "off")])
-def test_bench_multiprocess_overlap_forms(nproc, overlap):
-    """bench.py's N > 1 branch with the exchange form forced (column-pipelined / plain)."""
+@pytest.mark.parametrize("nproc,overlap,pull", [(2, "on", "off"), (4, "off", "off"), (2, "off", "on"),
+                                               (4, "auto", "auto")])
+def test_bench_multiprocess_overlap_forms(nproc, overlap, pull):
+    """bench.py's N > 1 branch with the exchange form forced (column-pipelined / plain / pull) or
+    calibrated among all three; the timed form passes the self-check."""
     r = _torchrun(nproc, ["bench.py", "--gpus", str(nproc), "--transport", "gloo", "--steps", "3", "--warmup", "1",
-                          "--params", "100000", "--choco", "0", "--cpu-seconds", "0", "--overlap", overlap])
+                          "--params", "100000", "--choco", "0", "--cpu-seconds", "0", "--overlap", overlap,
+                          "--pull", pull])
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["value"] > 0 and out["parity_ok"] is True
     if overlap == "on":
-        assert out["overlap"]["chosen"] == "chunked" and "column-pipelined" in out["config"]["parallelism"]
-    else:
+        assert out["overlap"]["chosen_form"] == "rccl_chunked" and "rccl_chunked" in out["config"]["parallelism"]
+    elif pull == "on":
+        assert out["overlap"]["chosen_form"] == "pull" and out["overlap"]["pull_unavailable"] is None
+    elif overlap == "off" and pull == "off":
         assert out["overlap"] is None
+    else:
+        assert set(out["overlap"]["calib_ms"]) == {"rccl", "rccl_chunked", "pull"}
 
 
 def test_dropin_communicators_one_process_per_worker():
