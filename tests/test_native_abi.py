@@ -29,7 +29,8 @@ def test_version_and_plan_geometry(pkg):
     assert L.mx_version().startswith(b"matcha-gossip")
     assert L.mx_plan_words(8, 5) == 4 + 2 * 8 + 8 * 5
     assert L.mx_mix_tile(8) == 1024 and L.mx_mix_tile(16) == 1024
-    assert L.mx_mix_tile(32) == 512 and L.mx_mix_tile(64) == 256 and L.mx_mix_tile(65) == 0
+    assert L.mx_mix_tile(32) == 512 and L.mx_mix_tile(64) == 256 and L.mx_mix_tile(65) == 256
+    assert L.mx_mix_tile(156) == 256 and L.mx_mix_tile(157) == 0          # mix_kernel_wide up to 156 slots
     assert L.mx_choco_msg_bytes(10, 3) == 4 * 4 + 8 * 3 + 4 * 2          # + tile bounds [1 tile + 1]
     assert L.mx_choco_msg_bytes(8193, 4) == 4 * 4 + 8 * 4 + 4 * 4        # 3 tiles of 4096
     assert L.mx_choco_apply_work_bytes(1 << 20, 8) == 0
