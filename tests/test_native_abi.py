@@ -107,7 +107,8 @@ def test_mix_kernel_dispatch_names(pkg):
     try:
         assert saved["rows"] == 2
         assert [E.mix_kernel_name(s) for s in (1, 8, 9, 16, 33, 64)] == ["mix_kernel_rows"] * 6
-        assert E.mix_kernel_name(65) == ""
+        assert E.mix_kernel_name(65) == E.mix_kernel_name(156) == "mix_kernel_wide"
+        assert E.mix_kernel_name(157) == ""
         E.set_mix_tuning(rows=1)
         assert [E.mix_kernel_name(s) for s in (8, 16, 64)] == ["mix_kernel_reg", "mix_kernel_rows", "mix_kernel_rows"]
         E.set_mix_tuning(rows=0, regidx=0)
