@@ -102,6 +102,12 @@ class _Staging:
                     p.data = view
                 off += k
 
+    def _pinned(self):
+        n = self.row.numel()
+        if getattr(self, "_pin", None) is None or self._pin.numel() != n:
+            self._pin = torch.empty(n, dtype=torch.float32, pin_memory=True)
+        return self._pin
+
     def load(self):
         if self.on_gpu:
             if not self.adopted():
@@ -110,16 +116,24 @@ class _Staging:
                     self.adopt()
             if self.on_gpu:
                 return
-        tensors = [p.data for p in self.params]
-        flat = torch.cat([t.reshape(-1) for t in tensors]) if len(tensors) > 1 else tensors[0].reshape(-1)
-        self.row.copy_(flat, non_blocking=False)
+        # host model: flatten into a pinned staging buffer (comm_helpers.py:27-30's torch.cat),
+        # then one DMA to the row
+        pin = self._pinned()
+        tensors = [p.data.reshape(-1) for p in self.params]
+        if len(tensors) > 1:
+            torch.cat(tensors, out=pin)
+        else:
+            pin.copy_(tensors[0])
+        self.row.copy_(pin, non_blocking=True)
 
     def store(self):
         if not self.on_gpu:
-            host = self.row.cpu()
+            pin = self._pinned()
+            pin.copy_(self.row, non_blocking=True)
+            torch.cuda.current_stream().synchronize()
             tensors = [p.data for p in self.params]
             with torch.no_grad():
-                for f, t in zip(unflatten_tensors(host, tensors), tensors):
+                for f, t in zip(unflatten_tensors(pin, tensors), tensors):
                     t.copy_(f)
 
 
