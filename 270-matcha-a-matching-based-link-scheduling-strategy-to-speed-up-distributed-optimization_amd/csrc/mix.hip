@@ -589,13 +589,17 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict
 
 // Wide kernel: any matching count and up to kWideMaxSlots slots (more workers per GPU, or more
 // remote partners, than the NS <= 64 kernels and their 32-matching plan records in LDS take).
-// A layout tile is worked in 256-column pieces; a piece of every needed slot is staged in dynamic
-// LDS (1 KB per slot), then each wave takes rows wave, wave + 4, ... and walks the row's partner
-// list, read with wave-uniform loads from the plan record in global memory, in matching order
-// with the self term last -- the same FMA chain as every other kernel.  One piece in flight per
-// workgroup (no prefetch): a correctness-first fallback, HBM-bound but not tuned.
-constexpr int kWideMaxSlots = 156;            // 156 KB of LDS at 256 columns per slot piece
+// A layout tile (256 columns) is worked in pieces of 64 * VEC columns, VEC = 4 / 2 / 1 chosen so
+// that a piece of every slot fits in <= 40 KB of dynamic LDS (4 workgroups per CU): the whole
+// workgroup stages a piece of every needed slot (16 / 8 / 4-byte loads, slot wave-uniform), the
+// next piece's loads are issued into registers right after the barrier and fly while this piece
+// is mixed; each wave then takes rows wave, wave + 4, ... and walks the row's partner list, read
+// with wave-uniform loads from the plan record in global memory, in matching order with the self
+// term last -- the same FMA chain as every other kernel.
+constexpr int kWideMaxSlots = 156;
+constexpr int kWideRegs = (kWideMaxSlots * 64 + kTPB - 1) / kTPB;   // staged vectors per lane
 
+template <int VEC, bool NT>
 __global__ __launch_bounds__(kTPB) void mix_kernel_wide(float* const* __restrict__ seg_ptrs,
                                                         const int64_t* __restrict__ seg_len,
                                                         const int64_t* __restrict__ tile_off,
@@ -603,9 +607,12 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_wide(float* const* __restrict
                                                         int64_t total_tiles, int tile_cols, int n_slots,
                                                         const int32_t* __restrict__ plan, int64_t iter,
                                                         const int64_t* __restrict__ iter_dev, int n_local, int M,
-                                                        float alpha, int nontemporal) {
-    using F = typename VT<4>::type;
-    extern __shared__ F wlds[];               // [n_slots][64] float4
+                                                        float alpha) {
+    using F = typename VT<VEC>::type;
+    constexpr int PW = 64 * VEC;              // columns per piece
+    constexpr int NR = VEC == 4 ? 10 : VEC == 2 ? 20 : kWideRegs;   // 40 / 80 / 156 slots
+    extern __shared__ __attribute__((aligned(16))) float wlds_raw[];
+    F* wlds = reinterpret_cast<F*>(wlds_raw);  // [n_slots][64] vectors
     iter = round_of(iter, iter_dev);
     if (iter < 0) return;
     const int32_t* rec = plan + iter * mx::plan_words(n_local, M);
@@ -617,54 +624,84 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_wide(float* const* __restrict
     const int32_t* src = deg + 2 * n_local;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int pieces = tile_cols / 256;
+    const int pieces = tile_cols / PW;
     const int64_t work = total_tiles * pieces;
-    for (int64_t wi = blockIdx.x; wi < work; wi += gridDim.x) {
+    const int nj = (n_slots * 64 + kTPB - 1) / kTPB;   // staged vectors per lane (slot = wave + 4 j)
+    struct Geo {
+        float* const* ptrs;
+        int64_t col0, lim;
+        bool vec_ok;
+    };
+    auto geo = [&](int64_t wi) {
         const int64_t tile = wi / pieces;
         int lo = 0, hi = nseg;
         while (hi - lo > 1) {
             const int mid = (lo + hi) >> 1;
             if (tile_off[mid] <= tile) lo = mid; else hi = mid;
         }
-        float* const* ptrs = seg_ptrs + (int64_t)lo * n_slots;
-        const int64_t col0 = (tile - tile_off[lo]) * tile_cols + (wi % pieces) * 256;
-        const int64_t lim = seg_len[lo];
-        const bool vec_ok = seg_vec[lo] != 0;
-        if (col0 >= lim) continue;            // block-uniform: the last tile's empty pieces
-        for (int q = threadIdx.x; q < n_slots * 64; q += kTPB) {
-            const int k = q >> 6;
-            const bool need = k < n_local ? (deg[k] > 0 || idle) : (k - n_local < n_remote);
-            if (!need) continue;
-            const int64_t c = col0 + (int64_t)(q & 63) * 4;
-            F v;
-            if (vec_ok && c + 4 <= lim) {
-                v = nontemporal ? ld<true, F>(ptrs[k] + c) : ld<false, F>(ptrs[k] + c);
-            } else {
+        Geo g;
+        g.ptrs = seg_ptrs + (int64_t)lo * n_slots;
+        g.col0 = (tile - tile_off[lo]) * tile_cols + (wi % pieces) * PW;
+        g.lim = seg_len[lo];
+        g.vec_ok = seg_vec[lo] != 0;
+        return g;
+    };
+    auto needed = [&](int k) {
+        return k < n_local ? (deg[k] > 0 || idle) : (k - n_local < n_remote);
+    };
+    F R[NR];
+    auto stage = [&](const Geo& g) {
 #pragma unroll
-                for (int t = 0; t < 4; ++t) v[t] = (c + t < lim) ? ld1(ptrs[k] + c + t) : 0.0f;
+        for (int j = 0; j < NR; ++j) {
+            const int k = wave + 4 * j;                    // wave-uniform slot
+            if (j < nj && k < n_slots && needed(k)) {
+                const int64_t c = g.col0 + (int64_t)lane * VEC;
+                if (g.vec_ok && c + VEC <= g.lim) {
+                    R[j] = ld<NT, F>(g.ptrs[k] + c);
+                } else {
+#pragma unroll
+                    for (int t = 0; t < VEC; ++t) R[j][t] = (c + t < g.lim) ? ld1(g.ptrs[k] + c + t) : 0.0f;
+                }
             }
-            wlds[q] = v;
+        }
+    };
+    int64_t wi = blockIdx.x;
+    if (wi >= work) return;
+    Geo cur = geo(wi);
+    stage(cur);
+    for (; wi < work; wi += gridDim.x) {
+#pragma unroll
+        for (int j = 0; j < NR; ++j) {
+            const int k = wave + 4 * j;
+            if (j < nj && k < n_slots && needed(k)) wlds[k * 64 + lane] = R[j];
         }
         __syncthreads();
+        Geo nxt = cur;
+        if (wi + gridDim.x < work) {           // the next piece's loads fly while this one is mixed
+            nxt = geo(wi + gridDim.x);
+            stage(nxt);
+        }
         for (int r = wave; r < n_local; r += kTPB / 64) {
             const int d = __builtin_amdgcn_readfirstlane(deg[r]);
             if (d == 0 && !idle) continue;
-            F a = F{0.0f, 0.0f, 0.0f, 0.0f};
+            F a;
+#pragma unroll
+            for (int t = 0; t < VEC; ++t) a[t] = 0.0f;
             for (int e = 0; e < d; ++e) {
                 const int sl = __builtin_amdgcn_readfirstlane(src[(int64_t)r * M + e]);
                 const F x = wlds[sl * 64 + lane];
 #pragma unroll
-                for (int t = 0; t < 4; ++t) a[t] = __builtin_fmaf(alpha, x[t], a[t]);
+                for (int t = 0; t < VEC; ++t) a[t] = __builtin_fmaf(alpha, x[t], a[t]);
             }
             const F xs = wlds[r * 64 + lane];
             const float s = sw[r];
 #pragma unroll
-            for (int t = 0; t < 4; ++t) a[t] = __builtin_fmaf(s, xs[t], a[t]);
-            const int64_t c = col0 + (int64_t)lane * 4;
-            if (nontemporal) store_one<4, true>(ptrs[r], c, lim, vec_ok && c + 4 <= lim, a);
-            else store_one<4, false>(ptrs[r], c, lim, vec_ok && c + 4 <= lim, a);
+            for (int t = 0; t < VEC; ++t) a[t] = __builtin_fmaf(s, xs[t], a[t]);
+            const int64_t c = cur.col0 + (int64_t)lane * VEC;
+            if (c < cur.lim) store_one<VEC, NT>(cur.ptrs[r], c, cur.lim, cur.vec_ok && c + VEC <= cur.lim, a);
         }
         __syncthreads();                      // the piece is read by every wave before restaging
+        cur = nxt;
     }
 }
 
@@ -932,19 +969,20 @@ int gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev, const int
     if (total_tiles <= 0) return MX_OK;
     if (c.ns == 0 || M > kMaxM) {             // wide kernel: > 64 slots or > 32 matchings
         const int tile_cols = mx_mix_tile(n_slots);
-        const int64_t work = total_tiles * (tile_cols / kTPB);
-        const size_t lds = (size_t)n_slots * 64 * sizeof(float) * 4;
-        static bool lds_set = false;
-        if (!lds_set) {                       // > 64 KB of dynamic LDS (gfx950: 160 KB per CU)
-            MX_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mix_kernel_wide),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, kWideMaxSlots * 1024));
-            lds_set = true;
-        }
-        int64_t grid = (int64_t)cu_count() * (lds <= 32768 ? 4 : lds <= 80000 ? 2 : 1);
+        const int vec = n_slots <= 40 ? 4 : n_slots <= 80 ? 2 : 1;   // <= 40 KB of LDS per piece
+        const size_t lds = (size_t)n_slots * 64 * vec * sizeof(float);
+        int64_t grid = (int64_t)cu_count() * 4;
+        const int64_t work = total_tiles * (tile_cols / (64 * vec));
         if (grid > work) grid = work;
-        hipLaunchKernelGGL(mix_kernel_wide, dim3((unsigned)(grid < 1 ? 1 : grid)), dim3(kTPB), lds, st, seg_ptrs_dev,
-                           seg_len_dev, tile_off_dev, seg_vec_dev, nseg, total_tiles, tile_cols, n_slots, plan_dev, iter,
-                           iter_dev, n_local, M, alpha, g_tune.nontemporal);
+        const bool nt = g_tune.nontemporal != 0;
+#define MX_WIDE(V, N)                                                                                      \
+    hipLaunchKernelGGL((mix_kernel_wide<V, N>), dim3((unsigned)(grid < 1 ? 1 : grid)), dim3(kTPB), lds, st, \
+                       seg_ptrs_dev, seg_len_dev, tile_off_dev, seg_vec_dev, nseg, total_tiles, tile_cols,   \
+                       n_slots, plan_dev, iter, iter_dev, n_local, M, alpha)
+        if (vec == 4) { if (nt) MX_WIDE(4, true); else MX_WIDE(4, false); }
+        else if (vec == 2) { if (nt) MX_WIDE(2, true); else MX_WIDE(2, false); }
+        else { if (nt) MX_WIDE(1, true); else MX_WIDE(1, false); }
+#undef MX_WIDE
         MX_LAUNCH_CHECK();
         return MX_OK;
     }
