@@ -597,6 +597,7 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict
 // with wave-uniform loads from the plan record in global memory, in matching order with the self
 // term last -- the same FMA chain as every other kernel.
 constexpr int kWideMaxSlots = 156;
+constexpr int kWideSrcWords = 4096;           // partner-list words kept in LDS (16 KB)
 constexpr int kWideRegs = (kWideMaxSlots * 64 + kTPB - 1) / kTPB;   // staged vectors per lane
 
 template <int VEC, bool NT>
@@ -649,6 +650,11 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_wide(float* const* __restrict
     auto needed = [&](int k) {
         return k < n_local ? (deg[k] > 0 || idle) : (k - n_local < n_remote);
     };
+    // the partner lists are the same for every piece: copied to LDS once when they fit
+    int32_t* lsrc = reinterpret_cast<int32_t*>(wlds_raw + (size_t)n_slots * PW);
+    const bool use_lsrc = (int64_t)n_local * M <= kWideSrcWords;
+    if (use_lsrc)
+        for (int i = threadIdx.x; i < n_local * M; i += kTPB) lsrc[i] = src[i];
     F R[NR];
     auto stage = [&](const Geo& g) {
 #pragma unroll
@@ -681,24 +687,54 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_wide(float* const* __restrict
             nxt = geo(wi + gridDim.x);
             stage(nxt);
         }
-        for (int r = wave; r < n_local; r += kTPB / 64) {
-            const int d = __builtin_amdgcn_readfirstlane(deg[r]);
-            if (d == 0 && !idle) continue;
-            F a;
-#pragma unroll
-            for (int t = 0; t < VEC; ++t) a[t] = 0.0f;
-            for (int e = 0; e < d; ++e) {
-                const int sl = __builtin_amdgcn_readfirstlane(src[(int64_t)r * M + e]);
-                const F x = wlds[sl * 64 + lane];
-#pragma unroll
-                for (int t = 0; t < VEC; ++t) a[t] = __builtin_fmaf(alpha, x[t], a[t]);
-            }
+        // rows wave, wave + 4, ..., two at a time so their LDS reads and FMA chains interleave
+        auto finish = [&](int r, F a) {
             const F xs = wlds[r * 64 + lane];
             const float s = sw[r];
 #pragma unroll
             for (int t = 0; t < VEC; ++t) a[t] = __builtin_fmaf(s, xs[t], a[t]);
             const int64_t c = cur.col0 + (int64_t)lane * VEC;
             if (c < cur.lim) store_one<VEC, NT>(cur.ptrs[r], c, cur.lim, cur.vec_ok && c + VEC <= cur.lim, a);
+        };
+        auto slot = [&](int r, int e) {
+            return __builtin_amdgcn_readfirstlane(use_lsrc ? lsrc[r * M + e] : src[(int64_t)r * M + e]);
+        };
+        int ra = wave;
+        while (ra < n_local) {
+            while (ra < n_local && !(deg[ra] > 0 || idle)) ra += kTPB / 64;
+            if (ra >= n_local) break;
+            int rb = ra + kTPB / 64;
+            while (rb < n_local && !(deg[rb] > 0 || idle)) rb += kTPB / 64;
+            const bool two = rb < n_local;
+            const int da = __builtin_amdgcn_readfirstlane(deg[ra]);
+            const int db = two ? __builtin_amdgcn_readfirstlane(deg[rb]) : 0;
+            F a, b;
+#pragma unroll
+            for (int t = 0; t < VEC; ++t) a[t] = b[t] = 0.0f;
+            const int dmin = da < db ? da : db;
+            int e = 0;
+            for (; e < dmin; ++e) {
+                const F xa = wlds[slot(ra, e) * 64 + lane];
+                const F xb = wlds[slot(rb, e) * 64 + lane];
+#pragma unroll
+                for (int t = 0; t < VEC; ++t) {
+                    a[t] = __builtin_fmaf(alpha, xa[t], a[t]);
+                    b[t] = __builtin_fmaf(alpha, xb[t], b[t]);
+                }
+            }
+            for (int ea = e; ea < da; ++ea) {
+                const F xa = wlds[slot(ra, ea) * 64 + lane];
+#pragma unroll
+                for (int t = 0; t < VEC; ++t) a[t] = __builtin_fmaf(alpha, xa[t], a[t]);
+            }
+            for (int eb = e; eb < db; ++eb) {
+                const F xb = wlds[slot(rb, eb) * 64 + lane];
+#pragma unroll
+                for (int t = 0; t < VEC; ++t) b[t] = __builtin_fmaf(alpha, xb[t], b[t]);
+            }
+            finish(ra, a);
+            if (two) finish(rb, b);
+            ra = two ? rb + kTPB / 64 : n_local;
         }
         __syncthreads();                      // the piece is read by every wave before restaging
         cur = nxt;
@@ -970,7 +1006,8 @@ int gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev, const int
     if (c.ns == 0 || M > kMaxM) {             // wide kernel: > 64 slots or > 32 matchings
         const int tile_cols = mx_mix_tile(n_slots);
         const int vec = n_slots <= 40 ? 4 : n_slots <= 80 ? 2 : 1;   // <= 40 KB of LDS per piece
-        const size_t lds = (size_t)n_slots * 64 * vec * sizeof(float);
+        const size_t lds = (size_t)n_slots * 64 * vec * sizeof(float) +
+                           ((int64_t)n_local * M <= kWideSrcWords ? (size_t)n_local * M * sizeof(int32_t) : 0);
         int64_t grid = (int64_t)cu_count() * 4;
         const int64_t work = total_tiles * (tile_cols / (64 * vec));
         if (grid > work) grid = work;
