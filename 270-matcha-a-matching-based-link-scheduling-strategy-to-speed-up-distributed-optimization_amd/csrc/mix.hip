@@ -597,7 +597,6 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict
 // with wave-uniform loads from the plan record in global memory, in matching order with the self
 // term last -- the same FMA chain as every other kernel.
 constexpr int kWideMaxSlots = 156;
-constexpr int kWideSrcWords = 4096;           // partner-list words kept in LDS (16 KB)
 constexpr int kWideRegs = (kWideMaxSlots * 64 + kTPB - 1) / kTPB;   // staged vectors per lane
 
 template <int VEC, bool NT>
@@ -650,11 +649,6 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_wide(float* const* __restrict
     auto needed = [&](int k) {
         return k < n_local ? (deg[k] > 0 || idle) : (k - n_local < n_remote);
     };
-    // the partner lists are the same for every piece: copied to LDS once when they fit
-    int32_t* lsrc = reinterpret_cast<int32_t*>(wlds_raw + (size_t)n_slots * PW);
-    const bool use_lsrc = (int64_t)n_local * M <= kWideSrcWords;
-    if (use_lsrc)
-        for (int i = threadIdx.x; i < n_local * M; i += kTPB) lsrc[i] = src[i];
     F R[NR];
     auto stage = [&](const Geo& g) {
 #pragma unroll
@@ -697,7 +691,7 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_wide(float* const* __restrict
             if (c < cur.lim) store_one<VEC, NT>(cur.ptrs[r], c, cur.lim, cur.vec_ok && c + VEC <= cur.lim, a);
         };
         auto slot = [&](int r, int e) {
-            return __builtin_amdgcn_readfirstlane(use_lsrc ? lsrc[r * M + e] : src[(int64_t)r * M + e]);
+            return __builtin_amdgcn_readfirstlane(src[(int64_t)r * M + e]);
         };
         int ra = wave;
         while (ra < n_local) {
@@ -1006,8 +1000,7 @@ int gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev, const int
     if (c.ns == 0 || M > kMaxM) {             // wide kernel: > 64 slots or > 32 matchings
         const int tile_cols = mx_mix_tile(n_slots);
         const int vec = n_slots <= 40 ? 4 : n_slots <= 80 ? 2 : 1;   // <= 40 KB of LDS per piece
-        const size_t lds = (size_t)n_slots * 64 * vec * sizeof(float) +
-                           ((int64_t)n_local * M <= kWideSrcWords ? (size_t)n_local * M * sizeof(int32_t) : 0);
+        const size_t lds = (size_t)n_slots * 64 * vec * sizeof(float);
         int64_t grid = (int64_t)cu_count() * 4;
         const int64_t work = total_tiles * (tile_cols / (64 * vec));
         if (grid > work) grid = work;
