@@ -681,54 +681,24 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_wide(float* const* __restrict
             nxt = geo(wi + gridDim.x);
             stage(nxt);
         }
-        // rows wave, wave + 4, ..., two at a time so their LDS reads and FMA chains interleave
-        auto finish = [&](int r, F a) {
+        for (int r = wave; r < n_local; r += kTPB / 64) {
+            const int d = __builtin_amdgcn_readfirstlane(deg[r]);
+            if (d == 0 && !idle) continue;
+            F a;
+#pragma unroll
+            for (int t = 0; t < VEC; ++t) a[t] = 0.0f;
+            for (int e = 0; e < d; ++e) {
+                const int sl = __builtin_amdgcn_readfirstlane(src[(int64_t)r * M + e]);
+                const F x = wlds[sl * 64 + lane];
+#pragma unroll
+                for (int t = 0; t < VEC; ++t) a[t] = __builtin_fmaf(alpha, x[t], a[t]);
+            }
             const F xs = wlds[r * 64 + lane];
             const float s = sw[r];
 #pragma unroll
             for (int t = 0; t < VEC; ++t) a[t] = __builtin_fmaf(s, xs[t], a[t]);
             const int64_t c = cur.col0 + (int64_t)lane * VEC;
             if (c < cur.lim) store_one<VEC, NT>(cur.ptrs[r], c, cur.lim, cur.vec_ok && c + VEC <= cur.lim, a);
-        };
-        auto slot = [&](int r, int e) {
-            return __builtin_amdgcn_readfirstlane(src[(int64_t)r * M + e]);
-        };
-        int ra = wave;
-        while (ra < n_local) {
-            while (ra < n_local && !(deg[ra] > 0 || idle)) ra += kTPB / 64;
-            if (ra >= n_local) break;
-            int rb = ra + kTPB / 64;
-            while (rb < n_local && !(deg[rb] > 0 || idle)) rb += kTPB / 64;
-            const bool two = rb < n_local;
-            const int da = __builtin_amdgcn_readfirstlane(deg[ra]);
-            const int db = two ? __builtin_amdgcn_readfirstlane(deg[rb]) : 0;
-            F a, b;
-#pragma unroll
-            for (int t = 0; t < VEC; ++t) a[t] = b[t] = 0.0f;
-            const int dmin = da < db ? da : db;
-            int e = 0;
-            for (; e < dmin; ++e) {
-                const F xa = wlds[slot(ra, e) * 64 + lane];
-                const F xb = wlds[slot(rb, e) * 64 + lane];
-#pragma unroll
-                for (int t = 0; t < VEC; ++t) {
-                    a[t] = __builtin_fmaf(alpha, xa[t], a[t]);
-                    b[t] = __builtin_fmaf(alpha, xb[t], b[t]);
-                }
-            }
-            for (int ea = e; ea < da; ++ea) {
-                const F xa = wlds[slot(ra, ea) * 64 + lane];
-#pragma unroll
-                for (int t = 0; t < VEC; ++t) a[t] = __builtin_fmaf(alpha, xa[t], a[t]);
-            }
-            for (int eb = e; eb < db; ++eb) {
-                const F xb = wlds[slot(rb, eb) * 64 + lane];
-#pragma unroll
-                for (int t = 0; t < VEC; ++t) b[t] = __builtin_fmaf(alpha, xb[t], b[t]);
-            }
-            finish(ra, a);
-            if (two) finish(rb, b);
-            ra = two ? rb + kTPB / 64 : n_local;
         }
         __syncthreads();                      // the piece is read by every wave before restaging
         cur = nxt;
