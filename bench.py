@@ -45,6 +45,8 @@ def parse():
                          "the multi-process path; never a performance number)")
     ap.add_argument("--settle-ms", type=float, default=50.0, help="diagnostic rounds (per-round HIP events) "
                     "run for at least this long between the warmup and the timed region")
+    ap.add_argument("--configs", type=int, default=1, help="also time the WRN-28-10 and CIFAR-ResNet configs' "
+                    "rounds (BASELINE configs 2-3) on the same GPUs")
     ap.add_argument("--staged", type=int, default=1, help="N = 1: also time host-resident models (the drop-in "
                     "communicators' staging path for CPU models)")
     ap.add_argument("--allreduce", type=int, default=1, help="also time all-reduce averaging (the paper's "
@@ -309,6 +311,45 @@ def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99
     return out
 
 
+def config_figures(pkg, rank, world, n, K, W, comm, dev, placement):
+    """Secondary figures: the other BASELINE configs' gossip rounds on the same GPUs -- WRN-28-10
+    (36,546,980 params per worker) under MATCHA C_b = 0.5 and full rounds, and the repo's CIFAR
+    ResNet (181,668 params, launch-bound) under MATCHA C_b = 0.5; rounds/s and, at N = 1, HBM
+    bytes / s over the algorithmic bytes of the rounds run."""
+    import torch.distributed as dist
+    out = {}
+    for name, P, budget in (("wrn28_10_matcha0.5", 36_546_980, 0.5), ("wrn28_10_full", 36_546_980, 1.0),
+                            ("resnet18_100_matcha0.5", 181_668, 0.5)):
+        np.random.seed(1234)
+        GPc = pkg.MatchaProcessor(pkg.select_graph(0), budget, rank, n, W + K, True)
+        g = pkg.VirtualWorkerGroup(GPc, numel=P, rank=rank, nranks=world, comm=comm, placement=placement)
+        for r in range(g.n_local):
+            pkg._lib.check(pkg.lib.mx_synth_fill(g.rows[r].data_ptr(), P, 1234 + g.workers[r], None))
+        for it in range(W):
+            g.step(it)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t = time.perf_counter()
+        for j in range(K):
+            g.step(W + j)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = max_over_ranks(time.perf_counter() - t, world, dev)
+        partner = np.asarray(GPc.neighbors_info, np.int32)
+        byts = 0
+        for f in np.asarray(GPc.active_flags[W:W + K], np.uint8):
+            deg = (partner[f.astype(bool)] >= 0).sum(axis=0) if f.any() else np.zeros(n, int)
+            byts += 2 * int((deg > 0).sum()) * P * 4
+        out[name] = {"params_per_worker": P, "budget": budget, "rounds_per_s": K / el, "ms_per_round": 1e3 * el / K,
+                     "hbm_TBps": byts / el / 1e12 if world == 1 else None}
+        g.close()
+        del g
+        torch.cuda.empty_cache()
+    return out
+
+
 def staged_figure(pkg, GP, n, P, K, first):
     """Secondary figure (N = 1): workers whose models stay on the host, as the reference's
     train_mpi.py keeps them -- each round the drop-in communicator's staging (communicator.py
@@ -558,6 +599,8 @@ def main():
                           placement=args.placement)
              if args.choco else None)
     staged = staged_figure(pkg, GP, n, P, 3, W) if (world == 1 and args.staged) else None
+    configs = (config_figures(pkg, rank, world, n, max(10, K), 3, comm, dev, args.placement)
+               if args.configs and P == 25_600_000 else None)
 
     flags = np.asarray(GP.active_flags[timed_first:timed_first + K], np.uint8)
     # algorithmic HBM bytes of the mixing kernel on this GPU: every local row with degree > 0 read
@@ -656,6 +699,7 @@ def main():
             "overlap": overlap,
             "choco": choco,
             "cpu_resident_models": staged,
+            "configs": configs,
         }
         if world > 1:
             lb = float(np.mean(link_bytes))
