@@ -106,9 +106,9 @@ def test_rccl_single_rank_linkage():
 
 
 def test_bench_single_gpu_line():
-    """bench.py at N = 1 on a small shape: the line's contract fields, the self-check, the
-    per-round event statistics, the host-model staging figure and both CPU baseline legs."""
-    r = subprocess.run([sys.executable, "bench.py", "--steps", "4", "--warmup", "2", "--params", "300000",
+    """bench.py at N = 1 (headline shape, few rounds): the line's contract fields, the self-check,
+    the per-round event statistics, the config and host-model figures and the CPU baseline legs."""
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "4", "--warmup", "2",
                         "--choco-params", "200000", "--cpu-seconds", "1"], cwd=ROOT, capture_output=True,
                        text=True, timeout=280, env=dict(os.environ, OMP_NUM_THREADS="2"))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
@@ -119,5 +119,7 @@ def test_bench_single_gpu_line():
     assert 0 < ru["events_min"] <= ru["events_median"]
     assert out["roofline"]["frac"] > 0 and out["roofline"]["min_launch_ms"] > 0
     assert out["cpu_resident_models"]["rounds_per_s"] > 0
+    assert set(out["configs"]) == {"wrn28_10_matcha0.5", "wrn28_10_full", "resnet18_100_matcha0.5"}
+    assert all(v["rounds_per_s"] > 0 and v["hbm_TBps"] > 0 for v in out["configs"].values())
     cb = out["cpu_baseline"]
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["pickle"]["value"] > 0 and cb["pickle"]["cores"] >= 1
