@@ -6,7 +6,6 @@ persistent Choco state x_hat and s (all [n_local, P] in HBM).  Per round:
     [N > 1] RCCL exchange of the messages   mx_exchange_round  (12 k bytes per edge direction)
     s / x_hat updates + dense x update      mx_choco_apply     (averaging, 200-230; one fused pass)
 """
-import os
 import time
 
 import numpy as np
@@ -75,8 +74,6 @@ class ChocoWorkerGroup:
         self.apply_work = torch.empty(int(lib.mx_choco_apply_work_bytes(P, self.engine.n_slots)),
                                       dtype=torch.uint8, device="cuda")
         self.gamma32 = float(np.float32(consensus_lr))
-        self.topk_streams = int(os.environ.get("MX_TOPK_STREAMS", "1"))   # row groups on their own streams
-        self._side = []
         self.iter_dev = torch.zeros(1, dtype=torch.int64, device="cuda")   # device_round's counter
 
     @property
@@ -90,40 +87,13 @@ class ChocoWorkerGroup:
         idx = self.msgs[base + 4 * self.kpad:base + 4 * self.kpad + 8 * self.k].view(torch.int64)
         return vals, idx
 
-    def _topk_rows(self, r0, nr, stream):
-        check(lib.mx_topk_abs_diff_rows(self.x.data_ptr() + 4 * r0 * self.ld, self.x_hat.data_ptr() + 4 * r0 * self.ld,
-                                        self.ld, nr, self.numel, self.k, self.msgs.data_ptr() + r0 * self.msg_ld,
-                                        self.msg_ld, 4 * self.kpad, self.bnd_off,
-                                        self.work.data_ptr() + r0 * self.work_ld, self.work_ld, stream),
-              "mx_topk_abs_diff_rows")
-
     def compress(self, it, stream=None):
         """prepare_comm_buffer (communicator.py:175-196): every local row's top-k message of
-        x - x_hat into its message slot.  With topk_streams = S > 1 the rows are split into S
-        groups whose top-k launch chains run on S streams: one group's latency-bound candidate
-        passes overlap another's streaming compaction pass."""
-        S = min(self.topk_streams, self.n_local)
-        if S <= 1:
-            self._topk_rows(0, self.n_local, stream_ptr(stream))
-            return
-        cur = stream if stream is not None else torch.cuda.current_stream()
-        while len(self._side) < S - 1:
-            self._side.append(torch.cuda.Stream())
-        fork = torch.cuda.Event()
-        fork.record(cur)
-        cuts = [self.n_local * g // S for g in range(S + 1)]
-        joins = []
-        for g in range(S):
-            s = cur if g == 0 else self._side[g - 1]
-            if g:
-                s.wait_event(fork)
-            self._topk_rows(cuts[g], cuts[g + 1] - cuts[g], s.cuda_stream)
-            if g:
-                e = torch.cuda.Event()
-                e.record(s)
-                joins.append(e)
-        for e in joins:
-            cur.wait_event(e)
+        x - x_hat into its message slot."""
+        check(lib.mx_topk_abs_diff_rows(self.x.data_ptr(), self.x_hat.data_ptr(), self.ld, self.n_local,
+                                        self.numel, self.k, self.msgs.data_ptr(), self.msg_ld, 4 * self.kpad,
+                                        self.bnd_off, self.work.data_ptr(), self.work_ld, stream_ptr(stream)),
+              "mx_topk_abs_diff_rows")
 
     def average(self, it, stream=None):
         """averaging (communicator.py:200-230): receive partner messages ([N > 1] over the
