@@ -90,7 +90,6 @@ struct Rows {
     int64_t work_ld;
     int64_t P, k;
     int64_t bnd_off;      // int32 tile bounds at out + r*out_ld + bnd_off (< 0: not written)
-    int nt;               // non-temporal loads of x / x_hat
 };
 
 struct RowView {
@@ -139,13 +138,6 @@ __device__ __forceinline__ float diff_at(const float* x, const float* xh, int64_
 }
 
 typedef float f4 __attribute__((ext_vector_type(4)));
-
-// streaming (non-temporal) or ordinary 16-byte accesses, by a block-uniform flag (knob "nt")
-__device__ __forceinline__ f4 ldv(const f4* p, bool nt) { return nt ? __builtin_nontemporal_load(p) : *p; }
-__device__ __forceinline__ void stv(const f4& v, f4* p, bool nt) {
-    if (nt) __builtin_nontemporal_store(v, p);
-    else *p = v;
-}
 
 // elements 4q .. 4q+3 of x - x_hat (16-byte non-temporal loads when the rows are aligned);
 // returns how many of them are < P
@@ -338,8 +330,8 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double
         const int64_t q0 = c * (kChunk / 4) + wave * kSubQuads + lane;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            ax[j] = ldv(x4 + q0 + j * 64, R.nt != 0);
-            ah[j] = h4 ? ldv(h4 + q0 + j * 64, R.nt != 0) : f4{0.0f, 0.0f, 0.0f, 0.0f};
+            ax[j] = __builtin_nontemporal_load(x4 + q0 + j * 64);
+            ah[j] = h4 ? __builtin_nontemporal_load(h4 + q0 + j * 64) : f4{0.0f, 0.0f, 0.0f, 0.0f};
         }
     };
     int64_t c = blockIdx.x;
@@ -665,7 +657,7 @@ __global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, floa
                                                      const int32_t* __restrict__ rec_in,
                                                      const int64_t* __restrict__ iter_dev, int64_t n_iters,
                                                      int64_t words, int n_local, int M,
-                                                     float alpha, float g, int nt) {
+                                                     float alpha, float g) {
     const int32_t* rec = round_rec(rec_in, iter_dev, n_iters, words);
     if (!rec) return;
     __shared__ float ls[kTile], lh[kTile];
@@ -685,9 +677,9 @@ __global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, floa
 #pragma unroll
         for (int j = 0; j < kQ; ++j) {
             const int q = j * kTPB + tid;
-            xv[j] = ldv(reinterpret_cast<const f4*>(xr) + q, nt & 1);
-            reinterpret_cast<f4*>(ls)[q] = ldv(reinterpret_cast<const f4*>(sr) + q, nt & 1);
-            reinterpret_cast<f4*>(lh)[q] = ldv(reinterpret_cast<const f4*>(hr) + q, nt & 1);
+            xv[j] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(xr) + q);
+            reinterpret_cast<f4*>(ls)[q] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(sr) + q);
+            reinterpret_cast<f4*>(lh)[q] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(hr) + q);
         }
     } else {
         for (int i = tid; i < len; i += kTPB) {
@@ -733,9 +725,9 @@ __global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, floa
             const f4 hv = reinterpret_cast<const f4*>(lh)[q];
 #pragma unroll
             for (int c = 0; c < 4; ++c) a[c] = __builtin_fmaf(-g, hv[c], __builtin_fmaf(g, sv[c], a[c]));
-            stv(a, reinterpret_cast<f4*>(xr) + q, nt & 2);
-            if (ds[q / (kGran / 4)]) stv(sv, reinterpret_cast<f4*>(sr) + q, nt & 2);
-            if (dh[q / (kGran / 4)]) stv(hv, reinterpret_cast<f4*>(hr) + q, nt & 2);
+            __builtin_nontemporal_store(a, reinterpret_cast<f4*>(xr) + q);
+            if (ds[q / (kGran / 4)]) __builtin_nontemporal_store(sv, reinterpret_cast<f4*>(sr) + q);
+            if (dh[q / (kGran / 4)]) __builtin_nontemporal_store(hv, reinterpret_cast<f4*>(hr) + q);
         }
     } else {
         for (int i = tid; i < len; i += kTPB) {
@@ -759,7 +751,6 @@ int g_compact_blocks = 0;     // persistent compaction blocks over all rows; 0 =
                               // row, 2048 for several (same-box sweeps: one row 1024 < 2048, 8 rows
                               // 0.667 -> 0.656 ms at 2048)
 int g_sample_pieces = 1;      // sampled 1024-element pieces per wave (sample_kernel grid)
-int g_nt = 7;                 // bit 0: non-temporal top-k loads, bit 1: apply loads, bit 2: apply stores
 int g_cand_chunks = 2;        // chunk regions per wave of cand_hist / cand_mark (fewer blocks =
                               // fewer global histogram flushes onto the same 1024 / 512 bins)
 
@@ -796,11 +787,6 @@ extern "C" int mx_topk_set(const char* key, int64_t value) {
         g_cand_chunks = (int)value;
         return MX_OK;
     }
-    if (!strcmp(key, "nt")) {
-        MX_CHECK(value >= 0 && value <= 7, "mx_topk_set: nt %lld", (long long)value);
-        g_nt = (int)value;
-        return MX_OK;
-    }
     if (!strcmp(key, "sample_pieces")) {
         MX_CHECK(value >= 1 && value <= 1024, "mx_topk_set: sample_pieces %lld", (long long)value);
         g_sample_pieces = (int)value;
@@ -814,7 +800,6 @@ extern "C" int64_t mx_topk_get(const char* key) {
     if (key && !strcmp(key, "compact_blocks")) return g_compact_blocks;
     if (key && !strcmp(key, "sample_pieces")) return g_sample_pieces;
     if (key && !strcmp(key, "cand_chunks")) return g_cand_chunks;
-    if (key && !strcmp(key, "nt")) return g_nt;
     mx::set_error("mx_topk_get: unknown key '%s'", key ? key : "(null)");
     return MX_ERR_INVALID;
 }
@@ -835,7 +820,7 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
              "mx_topk_abs_diff_rows: work must be 256-byte aligned");
     hipStream_t st = mx::as_stream(stream);
     Rows R{x, x_hat, ld, static_cast<char*>(out), out_ld_bytes, idx_off_bytes, static_cast<char*>(work),
-           work_ld_bytes, P, k, bnd_off_bytes, g_nt & 1};
+           work_ld_bytes, P, k, bnd_off_bytes};
     const int64_t nc = n_chunks(P);
     const int64_t S = sample_stride(P);
     const int64_t nsamp = (n_subs(P) + S - 1) / S;
@@ -920,8 +905,7 @@ int choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t 
     const char* m = static_cast<const char*>(msgs);
     MX_CHECK(nt <= 0x7fffffff, "mx_choco_apply: P too large");
     hipLaunchKernelGGL(apply_kernel, dim3((unsigned)nt, n_local), dim3(kTPB), 0, st, x, xhat, s, ld, P, m,
-                       msg_ld_bytes, kpad, k, rec, iter_dev, iter, words, n_local, M, alpha, gamma,
-                       ((g_nt >> 1) & 1) | (((g_nt >> 2) & 1) << 1));
+                       msg_ld_bytes, kpad, k, rec, iter_dev, iter, words, n_local, M, alpha, gamma);
     MX_LAUNCH_CHECK();
     return MX_OK;
 }
