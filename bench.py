@@ -344,6 +344,27 @@ def config_figures(pkg, rank, world, n, K, W, comm, dev, placement):
             byts += 2 * int((deg > 0).sum()) * P * 4
         out[name] = {"params_per_worker": P, "budget": budget, "rounds_per_s": K / el, "ms_per_round": 1e3 * el / K,
                      "hbm_TBps": byts / el / 1e12 if world == 1 else None}
+        if world == 1 and P < 1_000_000:
+            # launch-bound rows: the same K rounds replayed from one captured HIP graph
+            # (device_rounds: the rounds read their iteration from a device counter)
+            gr = torch.cuda.CUDAGraph()
+            cs = torch.cuda.Stream()
+            cs.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(cs):
+                with torch.cuda.graph(gr):
+                    g.device_rounds(K)
+            torch.cuda.synchronize()
+            g.iter_dev.fill_(W)
+            gr.replay()                           # warm replay of the same rounds' shapes
+            g.iter_dev.fill_(W)
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            gr.replay()
+            torch.cuda.synchronize()
+            elg = time.perf_counter() - t
+            out[name]["graph_rounds_per_s"] = K / elg
+            out[name]["graph_note"] = f"{K} rounds (iterations {W}..{W + K - 1}) replayed from one HIP graph"
+            del gr
         g.close()
         del g
         torch.cuda.empty_cache()
