@@ -139,6 +139,19 @@ __device__ __forceinline__ float diff_at(const float* x, const float* xh, int64_
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 
+// 16-byte streaming access; NT = non-temporal hint (compile-time: a runtime choice measured 24 %
+// slower whatever its value, the prefetching loops lose their schedule)
+template <bool NT>
+__device__ __forceinline__ f4 ld4(const f4* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void st4(f4 v, f4* p) {
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
 // elements 4q .. 4q+3 of x - x_hat (16-byte non-temporal loads when the rows are aligned);
 // returns how many of them are < P
 __device__ __forceinline__ int load_quad(const float* x, const float* xh, int64_t q, int64_t P, bool vec,
@@ -650,6 +663,12 @@ __device__ __forceinline__ const int32_t* round_rec(const int32_t* rec, const in
     return r[0] ? r : nullptr;
 }
 
+// NT: non-temporal accesses.  Chosen by the row count (mx_topk_set "apply_nt", -1 = auto): with
+// several rows the streams are far larger than the Infinity Cache and the hints win (8 rows
+// 0.65 ms vs 0.80 ms with ordinary accesses); a single row (config 4's share of one GPU at N = 8)
+// runs 123 -> 117 us per round with ordinary accesses, the apply pass then finding part of x /
+// x_hat the top-k pass has just read still on die (tools/choco_mall.py).
+template <bool NT>
 __global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, float* __restrict__ xh,
                                                      float* __restrict__ s, int64_t ld, int64_t P,
                                                      const char* __restrict__ msgs, int64_t msg_ld,
@@ -677,9 +696,9 @@ __global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, floa
 #pragma unroll
         for (int j = 0; j < kQ; ++j) {
             const int q = j * kTPB + tid;
-            xv[j] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(xr) + q);
-            reinterpret_cast<f4*>(ls)[q] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(sr) + q);
-            reinterpret_cast<f4*>(lh)[q] = __builtin_nontemporal_load(reinterpret_cast<const f4*>(hr) + q);
+            xv[j] = ld4<NT>(reinterpret_cast<const f4*>(xr) + q);
+            reinterpret_cast<f4*>(ls)[q] = ld4<NT>(reinterpret_cast<const f4*>(sr) + q);
+            reinterpret_cast<f4*>(lh)[q] = ld4<NT>(reinterpret_cast<const f4*>(hr) + q);
         }
     } else {
         for (int i = tid; i < len; i += kTPB) {
@@ -725,9 +744,9 @@ __global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, floa
             const f4 hv = reinterpret_cast<const f4*>(lh)[q];
 #pragma unroll
             for (int c = 0; c < 4; ++c) a[c] = __builtin_fmaf(-g, hv[c], __builtin_fmaf(g, sv[c], a[c]));
-            __builtin_nontemporal_store(a, reinterpret_cast<f4*>(xr) + q);
-            if (ds[q / (kGran / 4)]) __builtin_nontemporal_store(sv, reinterpret_cast<f4*>(sr) + q);
-            if (dh[q / (kGran / 4)]) __builtin_nontemporal_store(hv, reinterpret_cast<f4*>(hr) + q);
+            st4<NT>(a, reinterpret_cast<f4*>(xr) + q);
+            if (ds[q / (kGran / 4)]) st4<NT>(sv, reinterpret_cast<f4*>(sr) + q);
+            if (dh[q / (kGran / 4)]) st4<NT>(hv, reinterpret_cast<f4*>(hr) + q);
         }
     } else {
         for (int i = tid; i < len; i += kTPB) {
@@ -751,6 +770,7 @@ int g_compact_blocks = 0;     // persistent compaction blocks over all rows; 0 =
                               // row, 2048 for several (same-box sweeps: one row 1024 < 2048, 8 rows
                               // 0.667 -> 0.656 ms at 2048)
 int g_sample_pieces = 1;      // sampled 1024-element pieces per wave (sample_kernel grid)
+int g_apply_nt = -1;          // apply pass non-temporal accesses: -1 auto (only with several rows), 0, 1
 int g_cand_chunks = 2;        // chunk regions per wave of cand_hist / cand_mark (fewer blocks =
                               // fewer global histogram flushes onto the same 1024 / 512 bins)
 
@@ -787,6 +807,11 @@ extern "C" int mx_topk_set(const char* key, int64_t value) {
         g_cand_chunks = (int)value;
         return MX_OK;
     }
+    if (!strcmp(key, "apply_nt")) {
+        MX_CHECK(value >= -1 && value <= 1, "mx_topk_set: apply_nt %lld", (long long)value);
+        g_apply_nt = (int)value;
+        return MX_OK;
+    }
     if (!strcmp(key, "sample_pieces")) {
         MX_CHECK(value >= 1 && value <= 1024, "mx_topk_set: sample_pieces %lld", (long long)value);
         g_sample_pieces = (int)value;
@@ -800,6 +825,7 @@ extern "C" int64_t mx_topk_get(const char* key) {
     if (key && !strcmp(key, "compact_blocks")) return g_compact_blocks;
     if (key && !strcmp(key, "sample_pieces")) return g_sample_pieces;
     if (key && !strcmp(key, "cand_chunks")) return g_cand_chunks;
+    if (key && !strcmp(key, "apply_nt")) return g_apply_nt;
     mx::set_error("mx_topk_get: unknown key '%s'", key ? key : "(null)");
     return MX_ERR_INVALID;
 }
@@ -904,7 +930,9 @@ int choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t 
     const int64_t nt = n_tiles(P);
     const char* m = static_cast<const char*>(msgs);
     MX_CHECK(nt <= 0x7fffffff, "mx_choco_apply: P too large");
-    hipLaunchKernelGGL(apply_kernel, dim3((unsigned)nt, n_local), dim3(kTPB), 0, st, x, xhat, s, ld, P, m,
+    const bool nt_hint = g_apply_nt < 0 ? n_local > 1 : g_apply_nt > 0;
+    hipLaunchKernelGGL(nt_hint ? apply_kernel<true> : apply_kernel<false>, dim3((unsigned)nt, n_local), dim3(kTPB),
+                       0, st, x, xhat, s, ld, P, m,
                        msg_ld_bytes, kpad, k, rec, iter_dev, iter, words, n_local, M, alpha, gamma);
     MX_LAUNCH_CHECK();
     return MX_OK;

@@ -243,12 +243,21 @@ def _topk_case(O, P, pattern):
     elif pattern == "ties":
         x[::7] = np.float32(0.5)
         x[::11] = np.float32(-0.5)
+    elif pattern == "coarse":         # 1/128 grid: ~15.6k keys tie at the threshold
+        x[:] = np.round(x * 128) / np.float32(128)
+    elif pattern == "coarse333":      # 1/333 grid: ~6k ties, every threshold digit pass non-trivial
+        x[:] = np.round(x * 333) / np.float32(333)
+    elif pattern == "gap":            # 1 % of keys in [999, 1001): the threshold far above the
+        x[::100] += np.float32(1000.0)    # sampled floor, 20k candidates in one 12-bit bin
+    elif pattern == "spread":         # 1 % of keys spread over [2, 1002): threshold bin nearly empty
+        x[::100] = np.copysign(np.float32(2) + np.float32(1000) * np.abs(x[::100]), x[::100])
     return x
 
 
 @pytest.mark.parametrize("stride,pieces,blocks", [(0, 1, 1024), (1, 1, 1024), (16, 1, 1024), (0, 4, 2048),
                                                   (16, 3, 77), (0, 2, 4096)])
-@pytest.mark.parametrize("pattern", ["layers", "sampled_large", "constant", "ties"])
+@pytest.mark.parametrize("pattern", ["layers", "sampled_large", "constant", "ties", "coarse", "coarse333", "gap",
+                                     "spread"])
 def test_topk_sampled_floor_exact(pkg, O, stride, pieces, blocks, pattern):
     """The sampled candidate floor (and its device-side fallback) never changes the result, for any
     sampling grid (pieces per wave) or persistent compaction grid."""
@@ -289,7 +298,9 @@ def test_topk_work_reuse_and_tile_bounds(pkg, O):
 def _reuse_calls(pkg, O, work, hist_bytes):
     L = pkg.lib
     for P, ratio, pattern in [(2_000_001, 0.99, "sampled_large"), (4097, 0.5, "ties"), (300_000, 0.9, "layers"),
-                              (2_000_001, 0.99, "constant"), (2_000_001, 0.99, "sampled_large")]:
+                              (2_000_001, 0.99, "constant"), (2_000_001, 0.99, "coarse"), (2_000_001, 0.99, "gap"),
+                              (2_000_001, 0.99, "coarse333"), (2_000_001, 0.99, "spread"),
+                              (2_000_001, 0.99, "sampled_large")]:
         x = _topk_case(O, P, pattern)
         k = O.topk_k(P, ratio)
         ov, oi = O.topk_abs(x, k)
@@ -425,9 +436,20 @@ def test_mix_er_graphs_wide_configs(pkg, O, n, p, seed, P, knobs):
     assert np.array_equal(got.view(np.uint32), X.view(np.uint32))
 
 
-@pytest.mark.parametrize("P,ratio", [(14_774_436 // 16, 0.99), (545_930, 0.9)])
-def test_choco_vs_oracle_larger(pkg, O, P, ratio):
-    """Choco on 8 workers at VGG-16 / ResNet-50(10) scale slices, 3 rounds, bit-exact vs oracle."""
+@pytest.mark.parametrize("P,ratio,apply_nt", [(14_774_436 // 16, 0.99, -1), (545_930, 0.9, -1),
+                                              (14_774_436 // 16, 0.99, 0), (545_930, 0.9, 1)])
+def test_choco_vs_oracle_larger(pkg, O, P, ratio, apply_nt):
+    """Choco on 8 workers at VGG-16 / ResNet-50(10) scale slices, 3 rounds, bit-exact vs oracle;
+    the apply pass with its access hints as chosen (-1: by row count) or forced either way."""
+    saved = int(pkg.lib.mx_topk_get(b"apply_nt"))
+    pkg._lib.check(pkg.lib.mx_topk_set(b"apply_nt", apply_nt))
+    try:
+        _choco_vs_oracle_larger(pkg, O, P, ratio)
+    finally:
+        pkg.lib.mx_topk_set(b"apply_nt", saved)
+
+
+def _choco_vs_oracle_larger(pkg, O, P, ratio):
     n = 8
     gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, n, 4, True)
     flags = np.array([[1, 1, 1, 1, 1], [1, 0, 1, 0, 1], [0, 1, 1, 1, 0]], np.uint8)

@@ -1,0 +1,74 @@
+"""Choco round A/B over the apply pass's access hints (mx_topk_set "apply_nt": -1 auto, 0, 1; an
+r02 build also had compact_nt / apply_rev: tiles last-first -- neither helped): 8 rows on one GPU (the bench figure) and one row (a rank's share at N = 8, null
+transport, received messages = valid stand-ins).  Interleaved repeats, median of per-round HIP
+events.  Question asked: does the apply pass find x / x_hat in the Infinity Cache right after the
+top-k pass read them (one row: 118 MB fits; 8 rows: the tails do)?"""
+import importlib
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+pkg = importlib.import_module("270-matcha-a-matching-based-link-scheduling-strategy-to-speed-up-distributed-optimization_amd")
+from nullcomm import NullComm  # noqa: E402
+
+P = int(os.environ.get("CHOCO_P", 14_774_436))
+REPS = int(os.environ.get("REPS", 3))
+_V = os.environ.get("VARIANTS", "-1,0,1")      # apply_nt values; "none": leave the knob alone (another build)
+VARIANTS = [None] if _V == "none" else [int(v) for v in _V.split(",")]
+n = 8
+GP = pkg.MatchaProcessor(pkg.select_graph(0), 1.0, 0, n, 200, True)
+
+
+def setk(v):
+    if v is not None:
+        pkg._lib.check(pkg.lib.mx_topk_set(b"apply_nt", v))
+
+
+def time_rounds(c, it0, K=30):
+    for j in range(5):
+        c.step(it0 + j)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    for j, (a, b) in enumerate(ev):
+        a.record()
+        c.step(it0 + 5 + j)
+        b.record()
+    torch.cuda.synchronize()
+    return float(np.median([a.elapsed_time(b) for a, b in ev])) * 1e3
+
+
+groups = {}
+c8 = pkg.ChocoWorkerGroup(GP, numel=P, ratio=0.99, consensus_lr=0.1)
+for i in range(n):
+    pkg._lib.check(pkg.lib.mx_synth_fill(c8.rows[i].data_ptr(), P, 1234 + i, None))
+groups["rows8"] = c8
+c1 = pkg.ChocoWorkerGroup(GP, numel=P, ratio=0.99, consensus_lr=0.1, rank=0, nranks=8, comm=NullComm(0, 8),
+                          placement="auto")
+pkg._lib.check(pkg.lib.mx_synth_fill(c1.rows[0].data_ptr(), P, 1234 + c1.workers[0], None))
+c1.compress(0)
+torch.cuda.synchronize()
+for s in range(c1.n_local, c1.engine.n_slots):
+    c1.msgs[s * c1.msg_ld:(s + 1) * c1.msg_ld].copy_(c1.msgs[:c1.msg_ld])
+groups["row1"] = c1
+
+res = {(g, v): [] for g in groups for v in VARIANTS}
+it = 0
+for rep in range(REPS):
+    for g, c in groups.items():
+        for v in VARIANTS:
+            setk(v)
+            res[(g, v)].append(time_rounds(c, it % 150))
+            it += 40
+            print(json.dumps({"rep": rep, "group": g, "apply_nt": v,
+                              "round_us": round(res[(g, v)][-1], 2)}), flush=True)
+if VARIANTS != [None]:
+    setk(-1)
+for (g, v), xs in res.items():
+    print(json.dumps({"group": g, "apply_nt": v,
+                      "round_us_min": round(min(xs), 2), "round_us_median": round(float(np.median(xs)), 2)}))

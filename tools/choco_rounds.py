@@ -1,0 +1,33 @@
+"""K Choco rounds of one group (CHOCO_GROUP = rows8: 8 rows on one GPU; row1: one row, a rank's
+share at N = 8 with a null transport) -- a short fixed workload for rocprofv3 kernel traces."""
+import importlib
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+pkg = importlib.import_module("270-matcha-a-matching-based-link-scheduling-strategy-to-speed-up-distributed-optimization_amd")
+from nullcomm import NullComm  # noqa: E402
+
+P = int(os.environ.get("CHOCO_P", 14_774_436))
+K = int(os.environ.get("K", 30))
+GP = pkg.MatchaProcessor(pkg.select_graph(0), 1.0, 0, 8, K + 10, True)
+if os.environ.get("CHOCO_GROUP", "row1") == "rows8":
+    c = pkg.ChocoWorkerGroup(GP, numel=P, ratio=0.99, consensus_lr=0.1)
+    for i in range(8):
+        pkg._lib.check(pkg.lib.mx_synth_fill(c.rows[i].data_ptr(), P, 1234 + i, None))
+else:
+    c = pkg.ChocoWorkerGroup(GP, numel=P, ratio=0.99, consensus_lr=0.1, rank=0, nranks=8, comm=NullComm(0, 8),
+                             placement="auto")
+    pkg._lib.check(pkg.lib.mx_synth_fill(c.rows[0].data_ptr(), P, 1234 + c.workers[0], None))
+    c.compress(0)
+    torch.cuda.synchronize()
+    for s in range(c.n_local, c.engine.n_slots):
+        c.msgs[s * c.msg_ld:(s + 1) * c.msg_ld].copy_(c.msgs[:c.msg_ld])
+for it in range(K):
+    c.step(it)
+torch.cuda.synchronize()
+print("done", K)
