@@ -16,10 +16,12 @@ Reformulations used here:
     a maximum of convex quadratics in a -> a 1-D convex minimisation (bounded Brent, then a
     golden-section polish).
 
-Parity status: the SDP optimum p is not unique in general, so p cannot be
-reproduced without CVXOPT -- "parity unpinned".  Known answers that ARE checked
-(tests/test_solver.py): C_b = 1 gives p = 1 and alpha = FixedProcessor's 2/(lambda_2 +
-lambda_max); the spectral norms of ResearchReport.pdf Fig. 1(c) for graph 0.
+Parity status: the SDP optimum p is not unique in general, so p itself cannot be
+reproduced without CVXOPT -- "parity unpinned" for p.  What IS checked (tests/test_solver.py):
+the objective value -- the lambda_2 reached is within 1e-6 of an independent cutting-plane upper
+bound on the optimum for graphs 0-5 x budgets 0.1-0.8; alpha is the global minimiser of its
+convex 1-D reduction (dense grid); C_b = 1 gives p = 1 and alpha = FixedProcessor's
+2/(lambda_2 + lambda_max); the spectral norms of ResearchReport.pdf Fig. 1(c) for graph 0.
 """
 import numpy as np
 import scipy.linalg

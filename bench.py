@@ -285,7 +285,18 @@ def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99
         dist.barrier()
     el = max_over_ranks(time.perf_counter() - t, world, dev)
     out = {"config": f"P={P} (VGG-16 size by default), ratio {ratio} (k={grp.k}), gamma {gamma}, graph 0 full rounds",
-           "rounds_per_s": K / el, "ms_per_round": 1e3 * el / K, "rows_per_gpu": grp.n_local, "parity_ok": None}
+           "rounds_per_s": K / el, "ms_per_round": 1e3 * el / K, "rows_per_gpu": grp.n_local, "rounds": K,
+           "parity_ok": None}
+    if world == 1:
+        # ~6 P 4 B per worker (top-k reads x, x_hat; apply reads x, s, x_hat, writes x)
+        alg = 24 * P * grp.n_local
+        out["roofline"] = {"bound": "hbm", "alg_bytes_per_round": alg, "achieved_GBps": alg / (el / K) / 1e9,
+                           "frac_of_8TBps": alg / (el / K) / HBM_PEAK,
+                           "note": "algorithmic bytes; the passes also move the dirty 64-B granules of s / x_hat "
+                                   "and the candidate / message bytes (~3.2 GB per 8-row round by PMC, r02)"}
+        del grp
+        torch.cuda.empty_cache()
+        out["one_row_share_n8"] = choco_row_share(pkg, GP, P, ratio, gamma, K, W)
     if world > 1:
         mine = (list(grp.workers), grp.rows.cpu().numpy())
         objs = [None] * world if rank == 0 else None
@@ -306,7 +317,49 @@ def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99
             out["parity"] = "every worker's row vs a 1-GPU recompute of the same rounds, uint32"
             del ref
         dist.barrier()
-    del grp
+    if world > 1:
+        del grp
+        torch.cuda.empty_cache()
+    return out
+
+
+class _NullComm:
+    """Transport that moves nothing (the received message slots hold valid stand-ins)."""
+
+    def __init__(self, rank, nranks):
+        self.rank, self.nranks, self.handle = rank, nranks, None
+
+    def exchange_round(self, engine, it, row_ptrs, slab_ptr, slab_ld_bytes, row_bytes):
+        return int(sum(1 for op in engine.exchange_plan(it) if op[0] == 1))
+
+
+def choco_row_share(pkg, GP, P, ratio, gamma, K, W):
+    """Config 4's per-GPU work at N = 8 measured on this GPU: rank 0's single row (placement
+    "auto") with a null transport -- top-k, then the apply pass over its own and its partners'
+    messages (copies of its own as stand-ins).  What every GPU adds to the message exchange in a
+    real 8-GPU Choco round; per-round HIP events."""
+    c = pkg.ChocoWorkerGroup(GP, numel=P, ratio=ratio, consensus_lr=gamma, rank=0, nranks=8,
+                             comm=_NullComm(0, 8), placement="auto")
+    pkg._lib.check(pkg.lib.mx_synth_fill(c.rows[0].data_ptr(), P, 1234 + c.workers[0], None))
+    c.compress(0)
+    torch.cuda.synchronize()
+    for s in range(c.n_local, c.engine.n_slots):
+        c.msgs[s * c.msg_ld:(s + 1) * c.msg_ld].copy_(c.msgs[:c.msg_ld])
+    for it in range(W):
+        c.step(it)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+    for j, (a, b) in enumerate(ev):
+        a.record()
+        c.step(W + j)
+        b.record()
+    torch.cuda.synchronize()
+    us = np.array([a.elapsed_time(b) for a, b in ev]) * 1e3
+    out = {"rows": 1, "partners": int(c.engine.n_slots - c.n_local), "round_us_median": float(np.median(us)),
+           "round_us_min": float(us.min()), "rounds": K,
+           "hbm_GBps_alg": 24 * P / (np.median(us) * 1e-6) / 1e9,
+           "how": "rank 0's row of an 8-GPU layout, null transport, per-round HIP events"}
+    del c
     torch.cuda.empty_cache()
     return out
 
@@ -616,7 +669,7 @@ def main():
 
     allreduce = allreduce_figure(group, n, world, dev, max(5, K // 5), 2) if args.allreduce else None
 
-    choco = (choco_figure(pkg, GP, rank, world, max(5, K // 5), 3, comm, dev, P=args.choco_params,
+    choco = (choco_figure(pkg, GP, rank, world, max(20, K), 3, comm, dev, P=args.choco_params,
                           placement=args.placement)
              if args.choco else None)
     staged = staged_figure(pkg, GP, n, P, 3, W) if (world == 1 and args.staged) else None
