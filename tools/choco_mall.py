@@ -1,6 +1,8 @@
-"""Choco round A/B over the apply pass's access hints (mx_topk_set "apply_nt": -1 auto, 0, 1; an
-r02 build also had compact_nt / apply_rev: tiles last-first -- neither helped): 8 rows on one GPU (the bench figure) and one row (a rank's share at N = 8, null
-transport, received messages = valid stand-ins).  Interleaved repeats, median of per-round HIP
+"""Choco round A/B over mx_topk_set knob settings (VARIANTS="apply_nt=-1,apply_nt=0,compact_occ=5:
+compact_blocks=1280", ":" joins knobs of one variant; "none" leaves the knobs alone, for another build
+via MX_GOSSIP_LIB).  r02 builds also tried compact_nt / apply_rev (tiles last-first) and a
+96-VGPR compaction (5 waves per SIMD): none helped.  8 rows on one GPU (the bench figure) and one
+row (a rank's share at N = 8, null transport, received messages = valid stand-ins).  Interleaved repeats, median of per-round HIP
 events.  Question asked: does the apply pass find x / x_hat in the Infinity Cache right after the
 top-k pass read them (one row: 118 MB fits; 8 rows: the tails do)?"""
 import importlib
@@ -19,15 +21,28 @@ from nullcomm import NullComm  # noqa: E402
 
 P = int(os.environ.get("CHOCO_P", 14_774_436))
 REPS = int(os.environ.get("REPS", 3))
-_V = os.environ.get("VARIANTS", "-1,0,1")      # apply_nt values; "none": leave the knob alone (another build)
-VARIANTS = [None] if _V == "none" else [int(v) for v in _V.split(",")]
+_V = os.environ.get("VARIANTS", "apply_nt=-1,apply_nt=0,apply_nt=1")
+VARIANTS = [None] if _V == "none" else _V.split(",")
 n = 8
 GP = pkg.MatchaProcessor(pkg.select_graph(0), 1.0, 0, n, 200, True)
 
 
+DEFAULTS = {}
+
+
 def setk(v):
-    if v is not None:
-        pkg._lib.check(pkg.lib.mx_topk_set(b"apply_nt", v))
+    if v is None:
+        return
+    for kv in v.split(":"):
+        k, x = kv.split("=")
+        if k not in DEFAULTS:
+            DEFAULTS[k] = int(pkg.lib.mx_topk_get(k.encode()))
+        pkg._lib.check(pkg.lib.mx_topk_set(k.encode(), int(x)))
+
+
+def reset():
+    for k, x in DEFAULTS.items():
+        pkg._lib.check(pkg.lib.mx_topk_set(k.encode(), x))
 
 
 def time_rounds(c, it0, K=30):
@@ -62,13 +77,13 @@ it = 0
 for rep in range(REPS):
     for g, c in groups.items():
         for v in VARIANTS:
+            reset()
             setk(v)
             res[(g, v)].append(time_rounds(c, it % 150))
             it += 40
-            print(json.dumps({"rep": rep, "group": g, "apply_nt": v,
+            print(json.dumps({"rep": rep, "group": g, "variant": v,
                               "round_us": round(res[(g, v)][-1], 2)}), flush=True)
-if VARIANTS != [None]:
-    setk(-1)
+reset()
 for (g, v), xs in res.items():
-    print(json.dumps({"group": g, "apply_nt": v,
+    print(json.dumps({"group": g, "variant": v,
                       "round_us_min": round(min(xs), 2), "round_us_median": round(float(np.median(xs)), 2)}))
