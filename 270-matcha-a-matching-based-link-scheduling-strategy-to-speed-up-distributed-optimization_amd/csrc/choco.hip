@@ -597,7 +597,7 @@ __global__ __launch_bounds__(kTPB) void write_cand(Rows R, int64_t G) {
     int64_t run_out = gt + (eq < need_eq ? eq : need_eq), run_eq = eq;
     if (R.bnd_off >= 0 && lane == 0) {             // chunk c is apply tile c: its first entry
         int32_t* bnd = reinterpret_cast<int32_t*>(R.out + (int64_t)blockIdx.y * R.out_ld + R.bnd_off);
-        bnd[c] = (int32_t)run_out;
+        bnd[c] = (int32_t)(run_out < R.k ? run_out : R.k);
         if (c == nchunks - 1) bnd[nchunks] = (int32_t)R.k;
     }
     for (int64_t i0 = 0; i0 < nc; i0 += 64) {
@@ -609,9 +609,9 @@ __global__ __launch_bounds__(kTPB) void write_cand(Rows R, int64_t G) {
         const uint32_t einc = wave_incl_scan(eq ? 1u : 0u);
         const bool sel = in && (key > T || (eq && run_eq + (int64_t)einc - 1 < need_eq));
         const uint32_t sinc = wave_incl_scan(sel ? 1u : 0u);
-        if (sel) {
-            const int64_t pos = run_out + sinc - 1;
-            v.vals[pos] = d;
+        const int64_t pos = run_out + sinc - 1;
+        if (sel && pos < R.k) {                    // (< k by construction; the guard keeps a corrupted
+            v.vals[pos] = d;                       // scratch from writing outside the message)
             v.idx[pos] = c * kChunk + (i0 == 0 ? l0 : v.cloc[c * kChunk + i]);
         }
         run_out += __shfl(sinc, 63, 64);
@@ -713,9 +713,10 @@ __global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, floa
     const int32_t* src = deg + 2 * n_local + r * M;
     for (int e = 0; e < d; ++e) {              // partners, ascending matching order
         const Msg m = msg_at(msgs, msg_ld, kpad, k, src[e]);
-        const int lo = m.bnd[t], hi = m.bnd[t + 1];
-        for (int q = lo + tid; q < hi; q += kTPB) {
-            const int c = (int)(m.ix[q] - t0);
+        const int lo = max(m.bnd[t], 0), hi = min(m.bnd[t + 1], (int)k);   // clamped: a received
+        for (int q = lo + tid; q < hi; q += kTPB) {                        // message is not trusted
+            const int c = (int)(m.ix[q] - t0);                             // to stay in range
+            if ((unsigned)c >= (unsigned)len) continue;
             ls[c] = __fadd_rn(ls[c], __fmul_rn(alpha, m.v[q]));
             ds[c / kGran] = 1;
         }
@@ -724,9 +725,10 @@ __global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, floa
     {                                          // own message
         const float sw = __int_as_float(deg[n_local + r]);
         const Msg m = msg_at(msgs, msg_ld, kpad, k, r);
-        const int lo = m.bnd[t], hi = m.bnd[t + 1];
+        const int lo = max(m.bnd[t], 0), hi = min(m.bnd[t + 1], (int)k);
         for (int q = lo + tid; q < hi; q += kTPB) {
             const int c = (int)(m.ix[q] - t0);
+            if ((unsigned)c >= (unsigned)len) continue;
             const float vq = m.v[q];
             ls[c] = __fadd_rn(ls[c], __fmul_rn(sw, vq));
             lh[c] = __fadd_rn(lh[c], vq);
@@ -771,8 +773,10 @@ int g_compact_blocks = 0;     // persistent compaction blocks over all rows; 0 =
                               // 0.667 -> 0.656 ms at 2048)
 int g_sample_pieces = 1;      // sampled 1024-element pieces per wave (sample_kernel grid)
 int g_apply_nt = -1;          // apply pass non-temporal accesses: -1 auto (only with several rows), 0, 1
-int g_cand_chunks = 2;        // chunk regions per wave of cand_hist / cand_mark (fewer blocks =
-                              // fewer global histogram flushes onto the same 1024 / 512 bins)
+int g_cand_chunks = 0;        // chunk regions per wave of cand_hist / cand_mark; 0 = auto: 4 for one
+                              // row, 8 for several (fewer blocks = fewer histogram flushes: a second
+                              // flush of cand_hist<10>'s 1024 bins measured +3.7 us on one row; same-box
+                              // sweep 2 -> 4 / 8: one row 121.7 -> 119.6 us, 8 rows 655 -> 640 us)
 
 int64_t sample_stride(int64_t P) {
     const int64_t nc = n_chunks(P);
@@ -803,7 +807,7 @@ extern "C" int mx_topk_set(const char* key, int64_t value) {
         return MX_OK;
     }
     if (!strcmp(key, "cand_chunks")) {
-        MX_CHECK(value >= 1 && value <= 4096, "mx_topk_set: cand_chunks %lld", (long long)value);
+        MX_CHECK(value >= 0 && value <= 4096, "mx_topk_set: cand_chunks %lld", (long long)value);
         g_cand_chunks = (int)value;
         return MX_OK;
     }
@@ -861,7 +865,8 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
     const unsigned bgrid = clamp_grid(nc, 1, (cblocks + nrows - 1) / nrows);   // persistent
     const unsigned wgrid = (unsigned)((nc + kWaves - 1) / kWaves);          // one wave per chunk
     const unsigned sgrid = clamp_grid(nsamp, (int64_t)g_sample_pieces * kWaves, (1024 + nrows - 1) / nrows);
-    const unsigned cgrid = clamp_grid(nc, (int64_t)g_cand_chunks * kWaves, (2048 + nrows - 1) / nrows);
+    const int cchunks = g_cand_chunks > 0 ? g_cand_chunks : (nrows == 1 ? 4 : 8);
+    const unsigned cgrid = clamp_grid(nc, (int64_t)cchunks * kWaves, (2048 + nrows - 1) / nrows);
 #define MX_L(kern, grid, tpb, ...)                                                 \
     hipLaunchKernelGGL(kern, grid, dim3(tpb), 0, st, R, ##__VA_ARGS__);            \
     MX_LAUNCH_CHECK()
