@@ -102,11 +102,37 @@ class _Staging:
                     p.data = view
                 off += k
 
+    PIECE_FLOATS = 4 << 20        # staging pieces of 16 MB: the host copy of one piece overlaps
+                                  # the DMA of its neighbour (both directions)
+
     def _pinned(self):
         n = self.row.numel()
         if getattr(self, "_pin", None) is None or self._pin.numel() != n:
             self._pin = torch.empty(n, dtype=torch.float32, pin_memory=True)
         return self._pin
+
+    def _plan(self):
+        """Pieces [a, b) of the flat row and, per piece, the parameter slices it holds:
+        (param index, first, end within the parameter, offset in the row).  Non-contiguous
+        parameters are copied whole, outside the pieces."""
+        key = (self.PIECE_FLOATS, tuple(p.numel() for p in self.params))
+        if getattr(self, "_plan_key", None) != key:
+            offs = np.cumsum([0] + [p.numel() for p in self.params])
+            n, step = int(offs[-1]), max(1, int(self.PIECE_FLOATS))
+            pieces, i = [], 0
+            for a in range(0, n, step):
+                b = min(n, a + step)
+                while i < len(self.params) and offs[i + 1] <= a:
+                    i += 1
+                parts, j = [], i
+                while j < len(self.params) and offs[j] < b:
+                    lo, hi = max(a, int(offs[j])), min(b, int(offs[j + 1]))
+                    if hi > lo:
+                        parts.append((j, lo - int(offs[j]), hi - int(offs[j]), lo))
+                    j += 1
+                pieces.append((a, b, parts))
+            self._plan_key, self._plan_pieces, self._offs = key, pieces, offs
+        return self._plan_pieces
 
     def load(self):
         if self.on_gpu:
@@ -116,25 +142,43 @@ class _Staging:
                     self.adopt()
             if self.on_gpu:
                 return
-        # host model: flatten into a pinned staging buffer (comm_helpers.py:27-30's torch.cat),
-        # then one DMA to the row
+        # host model: flatten (comm_helpers.py:27-30's torch.cat) into a pinned staging buffer piece
+        # by piece, each piece's DMA to the row issued as soon as it is filled
         pin = self._pinned()
-        tensors = [p.data.reshape(-1) for p in self.params]
-        if len(tensors) > 1:
-            torch.cat(tensors, out=pin)
-        else:
-            pin.copy_(tensors[0])
-        self.row.copy_(pin, non_blocking=True)
+        for a, b, parts in self._plan():
+            for i, lo, hi, d in parts:
+                t = self.params[i].data
+                src = t.reshape(-1)[lo:hi] if t.is_contiguous() else t.contiguous().reshape(-1)[lo:hi]
+                pin[d:d + hi - lo].copy_(src)
+            self.row[a:b].copy_(pin[a:b], non_blocking=True)
 
     def store(self):
-        if not self.on_gpu:
-            pin = self._pinned()
-            pin.copy_(self.row, non_blocking=True)
-            torch.cuda.current_stream().synchronize()
-            tensors = [p.data for p in self.params]
-            with torch.no_grad():
-                for f, t in zip(unflatten_tensors(pin, tensors), tensors):
-                    t.copy_(f)
+        if self.on_gpu:
+            return
+        # every piece's DMA back is queued at once; piece i is scattered into the parameters while
+        # the later pieces are still in flight
+        pin = self._pinned()
+        pieces = self._plan()
+        events = []
+        for a, b, _ in pieces:
+            pin[a:b].copy_(self.row[a:b], non_blocking=True)
+            e = torch.cuda.Event()
+            e.record()
+            events.append(e)
+        later = set()
+        with torch.no_grad():
+            for (a, b, parts), e in zip(pieces, events):
+                e.synchronize()
+                for i, lo, hi, d in parts:
+                    t = self.params[i].data
+                    if t.is_contiguous():
+                        t.reshape(-1)[lo:hi].copy_(pin[d:d + hi - lo])
+                    else:
+                        later.add(i)
+            for i in sorted(later):                 # non-contiguous: whole-tensor copy_ (view_as)
+                t = self.params[i].data
+                o = int(self._offs[i])
+                t.copy_(pin[o:o + t.numel()].view_as(t))
 
 
 class Communicator(object):

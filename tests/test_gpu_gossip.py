@@ -503,6 +503,33 @@ def test_multirank_pipeline_loopback(pkg, O, gid, nranks, chunk):
     assert np.array_equal(got.view(np.uint32), X.view(np.uint32))
 
 
+@pytest.mark.parametrize("piece", [7, 100, 1 << 22])
+def test_host_staging_pieces(pkg, piece):
+    """Host-resident models' staging (communicator._Staging): pieces of the flat row that split
+    parameters, an empty and a non-contiguous parameter; load() gives torch.cat's layout
+    (comm_helpers.py:27-30), store() writes the row back into the same tensors (identity and
+    storage kept, communicator.py:124-131)."""
+    from importlib import import_module
+    C = import_module(pkg.__name__ + ".communicator")
+    torch.manual_seed(5)
+    ps = [torch.nn.Parameter(torch.randn(*sh)) for sh in ((13, 7), (0,), (5,), (64, 33), (1,))]
+    ps.append(torch.nn.Parameter(torch.randn(9, 6).t()))          # non-contiguous
+    n = sum(p.numel() for p in ps)
+    row = torch.zeros(n, device="cuda")
+    st = C._Staging(ps, row)
+    st.PIECE_FLOATS = piece
+    ids, ptrs = [id(p) for p in ps], [p.data_ptr() for p in ps]
+    st.load()
+    torch.cuda.synchronize()
+    assert torch.equal(row.cpu(), torch.cat([p.detach().reshape(-1) for p in ps]))
+    new = torch.randn(n, device="cuda")
+    row.copy_(new)
+    st.store()
+    assert torch.equal(torch.cat([p.detach().reshape(-1) for p in ps]), new.cpu())
+    assert [id(p) for p in ps] == ids and [p.data_ptr() for p in ps] == ptrs
+    assert not ps[-1].is_contiguous()
+
+
 @pytest.mark.parametrize("on_gpu", [True, False])
 def test_dropin_decen_communicators_per_rank(pkg, O, on_gpu):
     """The reference API one process per worker -- here 8 decenCommunicator(rank, 8, GP) objects
