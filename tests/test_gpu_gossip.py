@@ -439,8 +439,9 @@ def test_mix_er_graphs_wide_configs(pkg, O, n, p, seed, P, knobs):
 @pytest.mark.parametrize("P,ratio,apply_nt", [(14_774_436 // 16, 0.99, -1), (545_930, 0.9, -1),
                                               (14_774_436 // 16, 0.99, 0), (545_930, 0.9, 1)])
 def test_choco_vs_oracle_larger(pkg, O, P, ratio, apply_nt):
-    """Choco on 8 workers at VGG-16 / ResNet-50(10) scale slices, 3 rounds, bit-exact vs oracle;
-    the apply pass with its access hints as chosen (-1: by row count) or forced either way."""
+    """Choco on 8 workers at VGG-16 / ResNet-50(10) scale slices, 3 rounds, x / x_hat / s bit-exact
+    vs oracle; the apply pass with its access hints as chosen (-1: by row count) or forced either
+    way.  Both P leave a partial last tile."""
     saved = int(pkg.lib.mx_topk_get(b"apply_nt"))
     pkg._lib.check(pkg.lib.mx_topk_set(b"apply_nt", apply_nt))
     try:
@@ -468,6 +469,8 @@ def _choco_vs_oracle_larger(pkg, O, P, ratio):
         O.choco_round(X, XH, S, topo.neighbors_info, f, 2 / 7, k, 0.1)
         got = grp.rows.cpu().numpy()
         assert np.array_equal(got.view(np.uint32), X.view(np.uint32)), f"round {t}"
+        assert np.array_equal(grp.x_hat[:, :P].cpu().numpy().view(np.uint32), XH.view(np.uint32)), f"x_hat {t}"
+        assert np.array_equal(grp.s[:, :P].cpu().numpy().view(np.uint32), S.view(np.uint32)), f"s {t}"
 
 
 @pytest.mark.parametrize("gid,nranks,chunk", [(0, 2, None), (0, 4, None), (0, 8, None), (2, 4, None),
