@@ -768,9 +768,11 @@ unsigned clamp_grid(int64_t n, int64_t per, int64_t cap) {
 }  // namespace
 
 int g_sample_stride = 0;   // 0 = auto (about kSampleTarget sampled elements per row)
-int g_compact_blocks = 0;     // persistent compaction blocks over all rows; 0 = auto: 1024 for one
-                              // row, 2048 for several (same-box sweeps: one row 1024 < 2048, 8 rows
-                              // 0.667 -> 0.656 ms at 2048)
+int g_compact_blocks = 0;     // persistent compaction blocks over all rows; 0 = auto: 512 for one
+                              // row, 2048 for several (same-box sweeps: one row 256 / 384 / 512 / 640 /
+                              // 1024 / 2048 blocks 131 / 121 / 116.4 / 116.2 / 119 / 134 us per round,
+                              // the per-block prologue and flush outweigh the parallelism; 8 rows
+                              // 0.667 -> 0.656 ms at 2048, flat from 768 to 3072)
 int g_sample_pieces = 1;      // sampled 1024-element pieces per wave (sample_kernel grid)
 int g_apply_nt = -1;          // apply pass non-temporal accesses: -1 auto (only with several rows), 0, 1
 int g_cand_chunks = 0;        // chunk regions per wave of cand_hist / cand_mark; 0 = auto: 4 for one
@@ -861,7 +863,7 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
     }
     const double frac = (double)sampled / (double)P;
     MX_CHECK(nc <= 0x7fffffff, "mx_topk_abs_diff_rows: P too large");
-    const int cblocks = g_compact_blocks > 0 ? g_compact_blocks : (nrows == 1 ? 1024 : 2048);
+    const int cblocks = g_compact_blocks > 0 ? g_compact_blocks : (nrows == 1 ? 512 : 2048);
     const unsigned bgrid = clamp_grid(nc, 1, (cblocks + nrows - 1) / nrows);   // persistent
     const unsigned wgrid = (unsigned)((nc + kWaves - 1) / kWaves);          // one wave per chunk
     const unsigned sgrid = clamp_grid(nsamp, (int64_t)g_sample_pieces * kWaves, (1024 + nrows - 1) / nrows);
