@@ -182,6 +182,11 @@ __device__ __forceinline__ int load_quad(const float* x, const float* xh, int64_
     return n;
 }
 
+// set bits of a wave mask in the lanes below this one
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 // inclusive scan of a per-lane count over the wave
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     const int lane = threadIdx.x & 63;
@@ -401,7 +406,7 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double
                 keep |= (f ? 1u : 0u) << (4 * j + e);
                 if constexpr (BAL) {                    // ballots + mbcnt instead of a shuffle scan
                     const uint64_t b = __ballot(f);
-                    ex[j] += __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+                    ex[j] += lanes_below(b);
                     wt[j] += (uint32_t)__popcll(b);
                 } else {
                     ex[j] += f;                         // this lane's count; scanned below
@@ -620,16 +625,17 @@ __global__ __launch_bounds__(kTPB) void write_cand(Rows R, int64_t G) {
         const float d = !in ? 0.0f : i0 == 0 ? a0 : v.cval[c * kChunk + i];
         const uint32_t key = key_of(d);
         const bool eq = in && key == T;
-        const uint32_t einc = wave_incl_scan(eq ? 1u : 0u);
-        const bool sel = in && (key > T || (eq && run_eq + (int64_t)einc - 1 < need_eq));
-        const uint32_t sinc = wave_incl_scan(sel ? 1u : 0u);
-        const int64_t pos = run_out + sinc - 1;
+        const uint64_t be = __ballot(eq);          // flag ranks by ballot + mbcnt (exclusive counts)
+        const uint32_t eex = lanes_below(be);
+        const bool sel = in && (key > T || (eq && run_eq + (int64_t)eex < need_eq));
+        const uint64_t bs = __ballot(sel);
+        const int64_t pos = run_out + lanes_below(bs);
         if (sel && pos < R.k) {                    // (< k by construction; the guard keeps a corrupted
             v.vals[pos] = d;                       // scratch from writing outside the message)
             v.idx[pos] = c * kChunk + (i0 == 0 ? l0 : v.cloc[c * kChunk + i]);
         }
-        run_out += __shfl(sinc, 63, 64);
-        run_eq += __shfl(einc, 63, 64);
+        run_out += __popcll(bs);
+        run_eq += __popcll(be);
     }
 }
 
