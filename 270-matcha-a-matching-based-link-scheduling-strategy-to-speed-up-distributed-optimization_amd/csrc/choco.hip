@@ -198,12 +198,6 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
-__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
-
 // ---- S: top-digit histogram over every S-th 1024-element piece, one wave per sampled piece
 __global__ __launch_bounds__(kTPB) void sample_kernel(Rows R, int64_t S) {
     const RowView v = row_view(R);
@@ -512,19 +506,19 @@ __global__ __launch_bounds__(kTPB) void cand_mark(Rows R, int64_t G) {
     const int64_t c0 = (int64_t)blockIdx.x * G, c1 = c0 + G < nchunks ? c0 + G : nchunks;
     uint32_t wg = 0, we = 0;
     auto count = [&](int64_t c, int64_t nc, float a) {     // a = candidate `lane` (speculative)
-        uint32_t g = 0, e = 0;
-        if (lane < nc) {
+        uint32_t g = 0, e = 0;                   // wave-uniform: ballot counts per 64 candidates
+        {
+            const bool in = lane < nc;
             const uint32_t key = key_of(a);
-            g += key > T;
-            e += key == T;
+            g += (uint32_t)__popcll(__ballot(in && key > T));
+            e += (uint32_t)__popcll(__ballot(in && key == T));
         }
-        for (int64_t i = 64 + lane; i < nc; i += 64) {
-            const uint32_t key = key_of(v.cval[c * kChunk + i]);
-            g += key > T;
-            e += key == T;
+        for (int64_t i0 = 64; i0 < nc; i0 += 64) {
+            const bool in = i0 + lane < nc;
+            const uint32_t key = in ? key_of(v.cval[c * kChunk + i0 + lane]) : 0u;
+            g += (uint32_t)__popcll(__ballot(in && key > T));
+            e += (uint32_t)__popcll(__ballot(in && key == T));
         }
-        g = wave_sum(g);
-        e = wave_sum(e);
         wg += g;
         we += e;
         if (lane == 0) {
