@@ -328,7 +328,8 @@ __device__ Resolved resolve(const RowView& v, int64_t k, int stages) {
 // fallback = 1: runs only if fewer than k candidates were kept, then keeps every key.
 // BAL: a wave's output offsets from ballots + mbcnt (one row: 117.5 -> 115.5 us per round) or from
 // shuffle scans (several rows: 650 vs 655 us with ballots, whose 64-bit masks spill SGPRs)
-template <bool BAL>
+// LOOP: candidate stores in a loop over the lane's kept elements (mx_topk_set "compact_store" 1)
+template <bool BAL, bool LOOP>
 __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double frac, int fallback) {
     const RowView v = row_view(R);
     if (fallback && v.st->cand_n >= (unsigned long long)R.k) return;
@@ -423,18 +424,42 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double
         }
         float* cv = v.cval + c * kChunk;
         uint16_t* cl = v.cloc + c * kChunk;
+        if constexpr (LOOP) {
+            // one store pair per kept element of the lane, the wave looping as often as its
+            // fullest lane keeps (1-2 at 1 % density) instead of 16 masked store pairs
+            uint32_t base[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            uint32_t p = pos + ex[j];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-                if ((keep >> (4 * j + e)) & 1u) {
-                    cv[p] = d[j][e];
-                    cl[p] = (uint16_t)(kSub * wave + 4 * (64 * j + lane) + e);
-                    ++p;
-                }
+            for (int j = 0; j < 4; ++j) {
+                base[j] = pos + ex[j];
+                pos += wt[j];
             }
-            pos += wt[j];
+            for (uint32_t rem = keep; rem; rem &= rem - 1) {
+                const int b = __builtin_ctz(rem);
+                const int j = b >> 2;
+                float val = d[0][0];
+                uint32_t bj = base[0];
+#pragma unroll
+                for (int t = 1; t < 16; ++t) val = b == t ? d[t >> 2][t & 3] : val;
+#pragma unroll
+                for (int t = 1; t < 4; ++t) bj = j == t ? base[t] : bj;
+                const uint32_t p = bj + __popc(keep & ((1u << b) - 1) & (0xfu << (4 * j)));
+                cv[p] = val;
+                cl[p] = (uint16_t)(kSub * wave + 4 * (64 * j + lane) + (b & 3));
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                uint32_t p = pos + ex[j];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if ((keep >> (4 * j + e)) & 1u) {
+                        cv[p] = d[j][e];
+                        cl[p] = (uint16_t)(kSub * wave + 4 * (64 * j + lane) + e);
+                        ++p;
+                    }
+                }
+                pos += wt[j];
+            }
         }
         if (threadIdx.x == 0) {
             v.cnt[4 * c + 0] = 0;
@@ -646,7 +671,6 @@ __global__ __launch_bounds__(kTPB) void write_cand(Rows R, int64_t G) {
 // [bnd[t], bnd[t+1]) of the bounds the sender's write_cand stored after the message's indices
 // (tile t = top-k chunk t: bnd[t] is that chunk's output offset).
 constexpr int kTile = 4096;                    // elements per apply tile (16 KB of s + 16 KB of x_hat)
-constexpr int kGran = 16;                      // floats per dirty granule (64 B)
 
 __host__ __device__ inline int64_t n_tiles(int64_t P) { return (P + kTile - 1) / kTile; }
 
@@ -682,7 +706,10 @@ __device__ __forceinline__ const int32_t* round_rec(const int32_t* rec, const in
 // 0.65 ms vs 0.80 ms with ordinary accesses); a single row (config 4's share of one GPU at N = 8)
 // runs 123 -> 117 us per round with ordinary accesses, the apply pass then finding part of x /
 // x_hat the top-k pass has just read still on die (tools/choco_mall.py).
-template <bool NT>
+// GRAN: floats per dirty granule of s / x_hat written back.  16 (64 B) is the one instantiated: 32-B
+// granules measured 8 rows 639 -> 715 us per round (same-box A/B; partial non-temporal line writes),
+// one row unchanged
+template <bool NT, int GRAN>
 __global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, float* __restrict__ xh,
                                                      float* __restrict__ s, int64_t ld, int64_t P,
                                                      const char* __restrict__ msgs, int64_t msg_ld,
@@ -694,6 +721,7 @@ __global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, floa
     const int32_t* rec = round_rec(rec_in, iter_dev, n_iters, words);
     if (!rec) return;
     __shared__ float ls[kTile], lh[kTile];
+    constexpr int kGran = GRAN;
     __shared__ uint8_t ds[kTile / kGran], dh[kTile / kGran];
     const int r = blockIdx.y;
     const int64_t t = blockIdx.x;
@@ -789,6 +817,9 @@ int g_compact_blocks = 0;     // persistent compaction blocks over all rows; 0 =
                               // 0.667 -> 0.656 ms at 2048, flat from 768 to 3072)
 int g_sample_pieces = 1;      // sampled 1024-element pieces per wave (sample_kernel grid)
 int g_apply_nt = -1;          // apply pass non-temporal accesses: -1 auto (only with several rows), 0, 1
+int g_compact_store = 1;      // compaction candidate stores: 1 (default) a loop over the lane's kept elements,
+                              // 0 one masked store pair per (step, element) (same-box A/B: 8 rows 639 -> 632 us,
+                              // one row 114.4 -> 113.2 us)
 int g_cand_chunks = 0;        // chunk regions per wave of cand_hist / cand_mark; 0 = auto: 4 for one
                               // row, 8 for several (fewer blocks = fewer histogram flushes: a second
                               // flush of cand_hist<10>'s 1024 bins measured +3.7 us on one row; same-box
@@ -832,6 +863,11 @@ extern "C" int mx_topk_set(const char* key, int64_t value) {
         g_apply_nt = (int)value;
         return MX_OK;
     }
+    if (!strcmp(key, "compact_store")) {
+        MX_CHECK(value == 0 || value == 1, "mx_topk_set: compact_store %lld", (long long)value);
+        g_compact_store = (int)value;
+        return MX_OK;
+    }
     if (!strcmp(key, "sample_pieces")) {
         MX_CHECK(value >= 1 && value <= 1024, "mx_topk_set: sample_pieces %lld", (long long)value);
         g_sample_pieces = (int)value;
@@ -846,6 +882,7 @@ extern "C" int64_t mx_topk_get(const char* key) {
     if (key && !strcmp(key, "sample_pieces")) return g_sample_pieces;
     if (key && !strcmp(key, "cand_chunks")) return g_cand_chunks;
     if (key && !strcmp(key, "apply_nt")) return g_apply_nt;
+    if (key && !strcmp(key, "compact_store")) return g_compact_store;
     mx::set_error("mx_topk_get: unknown key '%s'", key ? key : "(null)");
     return MX_ERR_INVALID;
 }
@@ -887,13 +924,10 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
     hipLaunchKernelGGL(kern, grid, dim3(tpb), 0, st, R, ##__VA_ARGS__);            \
     MX_LAUNCH_CHECK()
     MX_L(sample_kernel, dim3(sgrid, nrows), kTPB, S);
-    if (nrows == 1) {
-        MX_L(compact_kernel<true>, dim3(bgrid, nrows), kTPB, S, frac, 0);
-        if (S > 1) MX_L(compact_kernel<true>, dim3(bgrid, nrows), kTPB, S, frac, 1);
-    } else {
-        MX_L(compact_kernel<false>, dim3(bgrid, nrows), kTPB, S, frac, 0);
-        if (S > 1) MX_L(compact_kernel<false>, dim3(bgrid, nrows), kTPB, S, frac, 1);
-    }
+    auto ck = nrows == 1 ? (g_compact_store ? compact_kernel<true, true> : compact_kernel<true, false>)
+                         : (g_compact_store ? compact_kernel<false, true> : compact_kernel<false, false>);
+    MX_L(ck, dim3(bgrid, nrows), kTPB, S, frac, 0);
+    if (S > 1) MX_L(ck, dim3(bgrid, nrows), kTPB, S, frac, 1);
     MX_L(cand_hist<kMidBits>, dim3(cgrid, nrows), kTPB);
     MX_L(cand_hist<kLowBits>, dim3(cgrid, nrows), kTPB);
     const int64_t G = (nc + cgrid - 1) / cgrid;    // chunks per cand_mark block
@@ -957,7 +991,8 @@ int choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t 
     const char* m = static_cast<const char*>(msgs);
     MX_CHECK(nt <= 0x7fffffff, "mx_choco_apply: P too large");
     const bool nt_hint = g_apply_nt < 0 ? n_local > 1 : g_apply_nt > 0;
-    hipLaunchKernelGGL(nt_hint ? apply_kernel<true> : apply_kernel<false>, dim3((unsigned)nt, n_local), dim3(kTPB),
+    auto kern = nt_hint ? apply_kernel<true, 16> : apply_kernel<false, 16>;
+    hipLaunchKernelGGL(kern, dim3((unsigned)nt, n_local), dim3(kTPB),
                        0, st, x, xhat, s, ld, P, m,
                        msg_ld_bytes, kpad, k, rec, iter_dev, iter, words, n_local, M, alpha, gamma);
     MX_LAUNCH_CHECK();

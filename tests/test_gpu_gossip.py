@@ -450,6 +450,34 @@ def test_choco_vs_oracle_larger(pkg, O, P, ratio, apply_nt):
         pkg.lib.mx_topk_set(b"apply_nt", saved)
 
 
+@pytest.mark.parametrize("knobs", [{"compact_store": 0}, {"compact_store": 1}, {"compact_store": 0, "apply_nt": 0}])
+def test_choco_knob_variants(pkg, O, knobs):
+    """Every Choco kernel variant selected by mx_topk_set (compaction stores looped over the kept
+    elements or one masked store pair per element; apply access hints) is bit-exact: the 8-row round (x / x_hat / s,
+    3 rounds) and the one-row top-k on the tie / far-threshold / sampled-fallback patterns."""
+    saved = {k: int(pkg.lib.mx_topk_get(k.encode())) for k in knobs}
+    for k, v in knobs.items():
+        pkg._lib.check(pkg.lib.mx_topk_set(k.encode(), v))
+    try:
+        _choco_vs_oracle_larger(pkg, O, 545_930, 0.9)
+        P, ratio = 2_000_001, 0.99
+        k = O.topk_k(P, ratio)
+        for stride, pattern in [(0, "layers"), (16, "sampled_large"), (0, "ties"), (0, "gap"), (0, "spread"),
+                                (1, "coarse333")]:
+            x = _topk_case(O, P, pattern)
+            ov, oi = O.topk_abs(x, k)
+            pkg._lib.check(pkg.lib.mx_topk_set(b"sample_stride", stride))
+            try:
+                v, i = pkg.get_top_k(torch.from_numpy(x).cuda(), ratio)
+            finally:
+                pkg.lib.mx_topk_set(b"sample_stride", 0)
+            assert np.array_equal(i.cpu().numpy(), oi), pattern
+            assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32)), pattern
+    finally:
+        for k, v in saved.items():
+            pkg.lib.mx_topk_set(k.encode(), v)
+
+
 def _choco_vs_oracle_larger(pkg, O, P, ratio):
     n = 8
     gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, n, 4, True)
