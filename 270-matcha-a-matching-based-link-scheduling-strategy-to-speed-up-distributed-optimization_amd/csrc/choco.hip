@@ -58,6 +58,16 @@ struct SelState {
     unsigned long long cand_n;   // candidates kept by the first compact_kernel pass (zero on entry)
 };
 
+// Per-chunk counters and per-block totals are 64-byte records, each written whole by one store
+// instruction (a record half-written by two kernels / two blocks is a partial-sector write).  Padding
+// the candidate regions' last lines the same way measured neutral (same-box A/B) and is not done.
+constexpr int kRec = 8;                      // int64 words per record
+// Candidate regions (one per chunk, filled from its start, ~1-6 % used) are strided 256 B beyond
+// their 16 / 8 KB so the region heads every pass touches spread over the HBM channels instead of
+// all sitting at the same offset of 16 KB-aligned windows.
+constexpr int kCvLd = kChunk + 64;           // floats per value region
+constexpr int kClLd = kChunk + 128;          // uint16 per index region
+
 struct WorkLayout {
     size_t hist, state, cnt, bt, cval, cloc, total;
 };
@@ -71,10 +81,10 @@ __host__ __device__ inline WorkLayout layout(int64_t P) {
     w.hist = 0;
     w.state = w.hist + sizeof(uint32_t) * kHistWords;
     w.cnt = w.state + 64;
-    w.bt = w.cnt + sizeof(int64_t) * 4 * (size_t)nc;              // cand_mark block totals (<= nc blocks)
-    w.cval = (w.bt + sizeof(int64_t) * 2 * (size_t)nc + 255) / 256 * 256;
-    w.cloc = w.cval + sizeof(float) * (size_t)nc * kChunk;
-    w.total = (w.cloc + sizeof(uint16_t) * (size_t)nc * kChunk + 255) / 256 * 256;
+    w.bt = w.cnt + sizeof(int64_t) * kRec * (size_t)nc;           // cand_mark block totals (<= nc blocks)
+    w.cval = (w.bt + sizeof(int64_t) * kRec * (size_t)nc + 255) / 256 * 256;
+    w.cloc = w.cval + sizeof(float) * (size_t)nc * kCvLd;
+    w.total = (w.cloc + sizeof(uint16_t) * (size_t)nc * kClLd + 255) / 256 * 256;
     return w;
 }
 
@@ -324,7 +334,7 @@ __device__ Resolved resolve(const RowView& v, int64_t k, int stages) {
 // candidate histogram.  b_lo comes from the sampled histogram (every block resolves it): S = 1 the
 // exact digit of the k-th largest key; S > 1 k scaled to the sample with a 25 % + 4 sigma margin.
 // The next chunk's x / x_hat loads are issued before the current chunk is ranked and written.
-// cnt[4c + 0..3] = {0, candidates > T, candidates == T, candidates}.
+// cnt[kRec c + 0..3] = {0, candidates > T, candidates == T, candidates}, + 4 words of padding.
 // fallback = 1: runs only if fewer than k candidates were kept, then keeps every key.
 // BAL: a wave's output offsets from ballots + mbcnt (one row: 117.5 -> 115.5 us per round) or from
 // shuffle scans (several rows: 650 vs 655 us with ballots, whose 64-bit masks spill SGPRs)
@@ -422,8 +432,8 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double
             pos += w < wave ? wtot[par][w] : 0;
             all += wtot[par][w];
         }
-        float* cv = v.cval + c * kChunk;
-        uint16_t* cl = v.cloc + c * kChunk;
+        float* cv = v.cval + c * kCvLd;
+        uint16_t* cl = v.cloc + c * kClLd;
         if constexpr (LOOP) {
             // one store pair per kept element of the lane, the wave looping as often as its
             // fullest lane keeps (1-2 at 1 % density) instead of 16 masked store pairs
@@ -461,11 +471,8 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double
                 pos += wt[j];
             }
         }
-        if (threadIdx.x == 0) {
-            v.cnt[4 * c + 0] = 0;
-            v.cnt[4 * c + 3] = all;
-            kept += all;
-        }
+        if (wave == 0 && lane < kRec) v.cnt[kRec * c + lane] = lane == 3 ? all : 0;   // the whole record
+        if (threadIdx.x == 0) kept += all;
     }
     __syncthreads();
     uint32_t* out = fallback ? v.h12f : v.h12;
@@ -499,12 +506,12 @@ __global__ __launch_bounds__(kTPB) void cand_hist(Rows R) {
     for (int64_t c = (int64_t)blockIdx.x * kWaves + wave; c < nchunks; c += 2 * stride) {
         const int64_t c2 = c + stride;
         const bool two = c2 < nchunks;
-        const int64_t n1 = v.cnt[4 * c + 3], n2 = two ? v.cnt[4 * c2 + 3] : 0;
-        const float a1 = v.cval[c * kChunk + lane], a2 = two ? v.cval[c2 * kChunk + lane] : 0.0f;
+        const int64_t n1 = v.cnt[kRec * c + 3], n2 = two ? v.cnt[kRec * c2 + 3] : 0;
+        const float a1 = v.cval[c * kCvLd + lane], a2 = two ? v.cval[c2 * kCvLd + lane] : 0.0f;
         if (lane < n1) add(a1);
-        for (int64_t i = 64 + lane; i < n1; i += 64) add(v.cval[c * kChunk + i]);
+        for (int64_t i = 64 + lane; i < n1; i += 64) add(v.cval[c * kCvLd + i]);
         if (lane < n2) add(a2);
-        for (int64_t i = 64 + lane; i < n2; i += 64) add(v.cval[c2 * kChunk + i]);
+        for (int64_t i = 64 + lane; i < n2; i += 64) add(v.cval[c2 * kCvLd + i]);
     }
     __syncthreads();
     uint32_t* out = BITS == kMidBits ? v.h10 : v.h9;
@@ -540,22 +547,19 @@ __global__ __launch_bounds__(kTPB) void cand_mark(Rows R, int64_t G) {
         }
         for (int64_t i0 = 64; i0 < nc; i0 += 64) {
             const bool in = i0 + lane < nc;
-            const uint32_t key = in ? key_of(v.cval[c * kChunk + i0 + lane]) : 0u;
+            const uint32_t key = in ? key_of(v.cval[c * kCvLd + i0 + lane]) : 0u;
             g += (uint32_t)__popcll(__ballot(in && key > T));
             e += (uint32_t)__popcll(__ballot(in && key == T));
         }
         wg += g;
         we += e;
-        if (lane == 0) {
-            v.cnt[4 * c + 1] = g;
-            v.cnt[4 * c + 2] = e;
-        }
+        if (lane < kRec) v.cnt[kRec * c + lane] = lane == 1 ? g : lane == 2 ? e : lane == 3 ? nc : 0;
     };
     for (int64_t c = c0 + wave; c < c1; c += 2 * kWaves) {    // two regions per step (as cand_hist)
         const int64_t c2 = c + kWaves;
         const bool two = c2 < c1;
-        const int64_t n1 = v.cnt[4 * c + 3], n2 = two ? v.cnt[4 * c2 + 3] : 0;
-        const float a1 = v.cval[c * kChunk + lane], a2 = two ? v.cval[c2 * kChunk + lane] : 0.0f;
+        const int64_t n1 = v.cnt[kRec * c + 3], n2 = two ? v.cnt[kRec * c2 + 3] : 0;
+        const float a1 = v.cval[c * kCvLd + lane], a2 = two ? v.cval[c2 * kCvLd + lane] : 0.0f;
         count(c, n1, a1);
         if (two) count(c2, n2, a2);
     }
@@ -564,14 +568,13 @@ __global__ __launch_bounds__(kTPB) void cand_mark(Rows R, int64_t G) {
         se[wave] = we;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < kRec) {                      // the whole 64-B record
         int64_t bg = 0, be = 0;
         for (int w = 0; w < kWaves; ++w) {
             bg += sg[w];
             be += se[w];
         }
-        v.bt[2 * blockIdx.x] = bg;
-        v.bt[2 * blockIdx.x + 1] = be;
+        v.bt[kRec * blockIdx.x + threadIdx.x] = threadIdx.x == 0 ? bg : threadIdx.x == 1 ? be : 0;
     }
 }
 
@@ -599,19 +602,19 @@ __global__ __launch_bounds__(kTPB) void write_cand(Rows R, int64_t G) {
     const int64_t c = c_first + wave;
     const int64_t nchunks = n_chunks(R.P);
     const bool live = c < nchunks;                 // this wave's region: count + first 64 candidates
-    const int64_t nc = live ? v.cnt[4 * c + 3] : 0;  // loaded up front (speculatively), in flight
-    const float a0 = live ? v.cval[c * kChunk + lane] : 0.0f;          // with the prefix loads
-    const uint32_t l0 = live ? v.cloc[c * kChunk + lane] : 0u;
+    const int64_t nc = live ? v.cnt[kRec * c + 3] : 0;  // loaded up front (speculatively), in flight
+    const float a0 = live ? v.cval[c * kCvLd + lane] : 0.0f;          // with the prefix loads
+    const uint32_t l0 = live ? v.cloc[c * kClLd + lane] : 0u;
     const int64_t J = c_first / G, nitems = J + (c_first - J * G);
     int64_t g = 0, e = 0;
     for (int64_t i = threadIdx.x; i < nitems; i += kTPB) {
         if (i < J) {
-            g += v.bt[2 * i];
-            e += v.bt[2 * i + 1];
+            g += v.bt[kRec * i];
+            e += v.bt[kRec * i + 1];
         } else {
             const int64_t cc = J * G + (i - J);
-            g += v.cnt[4 * cc + 1];
-            e += v.cnt[4 * cc + 2];
+            g += v.cnt[kRec * cc + 1];
+            e += v.cnt[kRec * cc + 2];
         }
     }
     g = wave_sum64(g);
@@ -629,8 +632,8 @@ __global__ __launch_bounds__(kTPB) void write_cand(Rows R, int64_t G) {
         eq += re[w];
     }
     for (int64_t cc = c_first; cc < c; ++cc) {
-        gt += v.cnt[4 * cc + 1];
-        eq += v.cnt[4 * cc + 2];
+        gt += v.cnt[kRec * cc + 1];
+        eq += v.cnt[kRec * cc + 2];
     }
     int64_t run_out = gt + (eq < need_eq ? eq : need_eq), run_eq = eq;
     if (R.bnd_off >= 0 && lane == 0) {             // chunk c is apply tile c: its first entry
@@ -641,7 +644,7 @@ __global__ __launch_bounds__(kTPB) void write_cand(Rows R, int64_t G) {
     for (int64_t i0 = 0; i0 < nc; i0 += 64) {
         const int64_t i = i0 + lane;
         const bool in = i < nc;
-        const float d = !in ? 0.0f : i0 == 0 ? a0 : v.cval[c * kChunk + i];
+        const float d = !in ? 0.0f : i0 == 0 ? a0 : v.cval[c * kCvLd + i];
         const uint32_t key = key_of(d);
         const bool eq = in && key == T;
         const uint64_t be = __ballot(eq);          // flag ranks by ballot + mbcnt (exclusive counts)
@@ -651,7 +654,7 @@ __global__ __launch_bounds__(kTPB) void write_cand(Rows R, int64_t G) {
         const int64_t pos = run_out + lanes_below(bs);
         if (sel && pos < R.k) {                    // (< k by construction; the guard keeps a corrupted
             v.vals[pos] = d;                       // scratch from writing outside the message)
-            v.idx[pos] = c * kChunk + (i0 == 0 ? l0 : v.cloc[c * kChunk + i]);
+            v.idx[pos] = c * kChunk + (i0 == 0 ? l0 : v.cloc[c * kClLd + i]);
         }
         run_out += __popcll(bs);
         run_eq += __popcll(be);
