@@ -197,14 +197,17 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// inclusive scan of a per-lane count over the wave
+// inclusive scan of a per-lane count over the wave, in DPP lane moves (no LDS round trips: the
+// ds_bpermute form of __shfl_up costs six dependent LDS latencies per scan): row_shr 1 / 2 / 4 / 8
+// within each 16-lane row (zeros shifted in), then row_bcast:15 / row_bcast:31 carry the row
+// totals into the rows above
 __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, true);   // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, true);   // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, true);   // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, true);   // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
     return v;
 }
 
@@ -420,7 +423,7 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double
             }
             if constexpr (!BAL) {
                 const uint32_t incl = wave_incl_scan(ex[j]);
-                wt[j] = __shfl(incl, 63, 64);
+                wt[j] = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
                 ex[j] = incl - ex[j];
             }
             tot += wt[j];
@@ -917,7 +920,7 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
     }
     const double frac = (double)sampled / (double)P;
     MX_CHECK(nc <= 0x7fffffff, "mx_topk_abs_diff_rows: P too large");
-    const int cblocks = g_compact_blocks > 0 ? g_compact_blocks : (nrows == 1 ? 512 : 2048);
+    const int cblocks = g_compact_blocks > 0 ? g_compact_blocks : (nrows == 1 ? 640 : 2560);
     const unsigned bgrid = clamp_grid(nc, 1, (cblocks + nrows - 1) / nrows);   // persistent
     const unsigned wgrid = (unsigned)((nc + kWaves - 1) / kWaves);          // one wave per chunk
     const unsigned sgrid = clamp_grid(nsamp, (int64_t)g_sample_pieces * kWaves, (1024 + nrows - 1) / nrows);
