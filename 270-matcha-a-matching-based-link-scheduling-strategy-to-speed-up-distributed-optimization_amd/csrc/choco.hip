@@ -211,6 +211,31 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v) {
     return v;
 }
 
+// the same over 64-bit counts: both halves moved by the same DPP pattern give the source lane's
+// 64-bit value
+template <int CTRL, int ROWS, bool BC>
+__device__ __forceinline__ int64_t dpp64(int64_t v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, ROWS, 0xf, BC);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)((uint64_t)v >> 32), CTRL, ROWS, 0xf, BC);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+__device__ __forceinline__ int64_t wave_incl_scan64(int64_t v) {
+    v += dpp64<0x111, 0xf, true>(v);
+    v += dpp64<0x112, 0xf, true>(v);
+    v += dpp64<0x114, 0xf, true>(v);
+    v += dpp64<0x118, 0xf, true>(v);
+    v += dpp64<0x142, 0xa, false>(v);
+    v += dpp64<0x143, 0xc, false>(v);
+    return v;
+}
+
+__device__ __forceinline__ int64_t lane63(int64_t v) {
+    const int lo = __builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+    const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), 63);
+    return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
 // ---- S: top-digit histogram over every S-th 1024-element piece, one wave per sampled piece
 __global__ __launch_bounds__(kTPB) void sample_kernel(Rows R, int64_t S) {
     const RowView v = row_view(R);
@@ -258,12 +283,7 @@ __device__ void find_bin(const uint32_t* __restrict__ hist, int64_t need, int* b
         cnt[j] = hist[NBINS - 1 - (t * kPer + j)];
         mine += cnt[j];
     }
-    int64_t incl = mine;                                 // inclusive scan over the wave
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int64_t x = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += x;
-    }
+    int64_t incl = wave_incl_scan64(mine);               // inclusive scan over the wave (DPP)
     if (lane == 63) wsum[wave] = incl;
     __syncthreads();
     int64_t base = 0, tot = 0;
@@ -581,11 +601,7 @@ __global__ __launch_bounds__(kTPB) void cand_mark(Rows R, int64_t G) {
     }
 }
 
-__device__ __forceinline__ int64_t wave_sum64(int64_t v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
-}
+__device__ __forceinline__ int64_t wave_sum64(int64_t v) { return lane63(wave_incl_scan64(v)); }
 
 // ---- C: one wave per chunk region: the candidates are already in index order, so a wave scan
 // of the tie flags ranks the ties and a wave scan of the selection flags places the output.
