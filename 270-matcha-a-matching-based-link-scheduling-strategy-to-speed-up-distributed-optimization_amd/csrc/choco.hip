@@ -504,6 +504,12 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double
     if (!fallback && threadIdx.x == 0 && kept) atomicAdd(&v.st->cand_n, (unsigned long long)kept);
 }
 
+// counts and first candidates of two chunk regions, loaded one step ahead by the candidate passes
+struct RegionPair {
+    int64_t n1, n2;
+    float a1, a2;
+};
+
 // candidate histogram of the next digit (10 bits at 9, or 9 bits at 0) among candidates matching
 // the prefix resolved so far; one wave per chunk region; LDS histogram flushed once per block
 template <int BITS>
@@ -513,28 +519,42 @@ __global__ __launch_bounds__(kTPB) void cand_hist(Rows R) {
     constexpr int stages = BITS == kMidBits ? 1 : 2;
     constexpr int shift = BITS == kMidBits ? kMidShift : 0;
     __shared__ uint32_t h[NB];
+    const int64_t nchunks = n_chunks(R.P);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // two chunk regions per step, their counts and first 64 candidates loaded together (the
+    // region is allocated whatever the count, lanes past it are ignored): one memory round trip
+    // instead of a count -> candidates chain per region -- this pass reads them cold.  The first
+    // step's loads fly while the histograms are resolved, each later step's during the one before.
+    const int64_t stride = (int64_t)gridDim.x * kWaves;
+    auto load = [&](int64_t c) {
+        RegionPair q{0, 0, 0.0f, 0.0f};
+        if (c < nchunks) {
+            q.n1 = v.cnt[kRec * c + 3];
+            q.a1 = v.cval[c * kCvLd + lane];
+        }
+        if (c + stride < nchunks) {
+            q.n2 = v.cnt[kRec * (c + stride) + 3];
+            q.a2 = v.cval[(c + stride) * kCvLd + lane];
+        }
+        return q;
+    };
+    int64_t c = (int64_t)blockIdx.x * kWaves + wave;
+    RegionPair cur = load(c);
     const Resolved z = resolve(v, R.k, stages);
     for (int i = threadIdx.x; i < NB; i += kTPB) h[i] = 0;
     __syncthreads();
-    const int64_t nchunks = n_chunks(R.P);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     auto add = [&](float d) {
         const uint32_t key = key_of(d);
         if ((key & z.mask) == z.prefix) atomicAdd(&h[(key >> shift) & (NB - 1)], 1u);
     };
-    // two chunk regions per step, their counts and first 64 candidates loaded together (the
-    // region is allocated whatever the count, lanes past it are ignored): one memory round trip
-    // instead of a count -> candidates chain per region -- this pass reads them cold
-    const int64_t stride = (int64_t)gridDim.x * kWaves;
-    for (int64_t c = (int64_t)blockIdx.x * kWaves + wave; c < nchunks; c += 2 * stride) {
+    for (; c < nchunks; c += 2 * stride) {
+        const RegionPair nx = load(c + 2 * stride);
         const int64_t c2 = c + stride;
-        const bool two = c2 < nchunks;
-        const int64_t n1 = v.cnt[kRec * c + 3], n2 = two ? v.cnt[kRec * c2 + 3] : 0;
-        const float a1 = v.cval[c * kCvLd + lane], a2 = two ? v.cval[c2 * kCvLd + lane] : 0.0f;
-        if (lane < n1) add(a1);
-        for (int64_t i = 64 + lane; i < n1; i += 64) add(v.cval[c * kCvLd + i]);
-        if (lane < n2) add(a2);
-        for (int64_t i = 64 + lane; i < n2; i += 64) add(v.cval[c2 * kCvLd + i]);
+        if (lane < cur.n1) add(cur.a1);
+        for (int64_t i = 64 + lane; i < cur.n1; i += 64) add(v.cval[c * kCvLd + i]);
+        if (lane < cur.n2) add(cur.a2);
+        for (int64_t i = 64 + lane; i < cur.n2; i += 64) add(v.cval[c2 * kCvLd + i]);
+        cur = nx;
     }
     __syncthreads();
     uint32_t* out = BITS == kMidBits ? v.h10 : v.h9;
@@ -549,6 +569,22 @@ __global__ __launch_bounds__(kTPB) void cand_hist(Rows R) {
 // (no separate scan launch).
 __global__ __launch_bounds__(kTPB) void cand_mark(Rows R, int64_t G) {
     const RowView v = row_view(R);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t nchunks = n_chunks(R.P);
+    const int64_t c0 = (int64_t)blockIdx.x * G, c1 = c0 + G < nchunks ? c0 + G : nchunks;
+    auto load = [&](int64_t c) {                 // two regions per step (as cand_hist), one step ahead
+        RegionPair q{0, 0, 0.0f, 0.0f};
+        if (c < c1) {
+            q.n1 = v.cnt[kRec * c + 3];
+            q.a1 = v.cval[c * kCvLd + lane];
+        }
+        if (c + kWaves < c1) {
+            q.n2 = v.cnt[kRec * (c + kWaves) + 3];
+            q.a2 = v.cval[(c + kWaves) * kCvLd + lane];
+        }
+        return q;
+    };
+    RegionPair cur = load(c0 + wave);            // in flight while the three histograms are resolved
     const Resolved z = resolve(v, R.k, 3);
     const uint32_t T = z.prefix;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -556,9 +592,6 @@ __global__ __launch_bounds__(kTPB) void cand_mark(Rows R, int64_t G) {
         v.st->need = z.need;
     }
     __shared__ uint32_t sg[kWaves], se[kWaves];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t nchunks = n_chunks(R.P);
-    const int64_t c0 = (int64_t)blockIdx.x * G, c1 = c0 + G < nchunks ? c0 + G : nchunks;
     uint32_t wg = 0, we = 0;
     auto count = [&](int64_t c, int64_t nc, float a) {     // a = candidate `lane` (speculative)
         uint32_t g = 0, e = 0;                   // wave-uniform: ballot counts per 64 candidates
@@ -578,13 +611,11 @@ __global__ __launch_bounds__(kTPB) void cand_mark(Rows R, int64_t G) {
         we += e;
         if (lane < kRec) v.cnt[kRec * c + lane] = lane == 1 ? g : lane == 2 ? e : lane == 3 ? nc : 0;
     };
-    for (int64_t c = c0 + wave; c < c1; c += 2 * kWaves) {    // two regions per step (as cand_hist)
-        const int64_t c2 = c + kWaves;
-        const bool two = c2 < c1;
-        const int64_t n1 = v.cnt[kRec * c + 3], n2 = two ? v.cnt[kRec * c2 + 3] : 0;
-        const float a1 = v.cval[c * kCvLd + lane], a2 = two ? v.cval[c2 * kCvLd + lane] : 0.0f;
-        count(c, n1, a1);
-        if (two) count(c2, n2, a2);
+    for (int64_t c = c0 + wave; c < c1; c += 2 * kWaves) {
+        const RegionPair nx = load(c + 2 * kWaves);
+        count(c, cur.n1, cur.a1);
+        if (c + kWaves < c1) count(c + kWaves, cur.n2, cur.a2);
+        cur = nx;
     }
     if (lane == 0) {
         sg[wave] = wg;
