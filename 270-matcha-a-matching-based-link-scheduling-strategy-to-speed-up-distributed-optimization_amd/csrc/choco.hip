@@ -763,19 +763,12 @@ __device__ __forceinline__ const int32_t* round_rec(const int32_t* rec, const in
 // granules measured 8 rows 639 -> 715 us per round (same-box A/B; partial non-temporal line writes),
 // one row unchanged
 template <bool NT, int GRAN>
-__global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, float* __restrict__ xh,
-                                                     float* __restrict__ s, int64_t ld, int64_t P,
-                                                     const char* __restrict__ msgs, int64_t msg_ld,
-                                                     int64_t kpad, int64_t k,
-                                                     const int32_t* __restrict__ rec_in,
-                                                     const int64_t* __restrict__ iter_dev, int64_t n_iters,
-                                                     int64_t words, int n_local, int M,
-                                                     float alpha, float g) {
-    const int32_t* rec = round_rec(rec_in, iter_dev, n_iters, words);
-    if (!rec) return;
-    __shared__ float ls[kTile], lh[kTile];
+__device__ __forceinline__ void apply_tile(float* __restrict__ x, float* __restrict__ xh, float* __restrict__ s,
+                                           int64_t ld, int64_t P, const char* __restrict__ msgs, int64_t msg_ld,
+                                           int64_t kpad, int64_t k, const int32_t* __restrict__ rec, int n_local,
+                                           int M, float alpha, float g, float* ls, float* lh, uint8_t* ds,
+                                           uint8_t* dh) {
     constexpr int kGran = GRAN;
-    __shared__ uint8_t ds[kTile / kGran], dh[kTile / kGran];
     const int r = blockIdx.y;
     const int64_t t = blockIdx.x;
     const int64_t t0 = t * kTile;
@@ -854,6 +847,150 @@ __global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, floa
     }
 }
 
+template <bool NT, int GRAN>
+__global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, float* __restrict__ xh,
+                                                     float* __restrict__ s, int64_t ld, int64_t P,
+                                                     const char* __restrict__ msgs, int64_t msg_ld,
+                                                     int64_t kpad, int64_t k,
+                                                     const int32_t* __restrict__ rec_in,
+                                                     const int64_t* __restrict__ iter_dev, int64_t n_iters,
+                                                     int64_t words, int n_local, int M,
+                                                     float alpha, float g) {
+    const int32_t* rec = round_rec(rec_in, iter_dev, n_iters, words);
+    if (!rec) return;
+    __shared__ float ls[kTile], lh[kTile];
+    __shared__ uint8_t ds[kTile / GRAN], dh[kTile / GRAN];
+    apply_tile<NT, GRAN>(x, xh, s, ld, P, msgs, msg_ld, kpad, k, rec, n_local, M, alpha, g, ls, lh, ds, dh);
+}
+
+// The same pass with the message phase's global reads moved under the tile's stream: the plan
+// record and every message's tile bounds are wave-uniform (scalar loads, their own counter), and
+// the first kTPB entries of up to kPfMsgs messages are loaded per thread right after the x / s /
+// x_hat loads and before s / x_hat are staged into LDS, so the ordered LDS updates then run
+// without a memory round trip per message (the plain kernel pays two per message: bounds, then
+// entries).  Entries past the first kTPB of a message in this tile, and messages past kPfMsgs,
+// are loaded as in the plain kernel.  Same order of updates, same results.
+constexpr int kPfMsgs = 8;
+
+template <bool NT>
+__global__ __launch_bounds__(kTPB) void apply_kernel_pf(float* __restrict__ x, float* __restrict__ xh,
+                                                        float* __restrict__ s, int64_t ld, int64_t P,
+                                                        const char* __restrict__ msgs, int64_t msg_ld,
+                                                        int64_t kpad, int64_t k,
+                                                        const int32_t* __restrict__ rec_in,
+                                                        const int64_t* __restrict__ iter_dev, int64_t n_iters,
+                                                        int64_t words, int n_local, int M,
+                                                        float alpha, float g) {
+    const int32_t* rec = round_rec(rec_in, iter_dev, n_iters, words);
+    if (!rec) return;
+    constexpr int kGran = 16;
+    const int r = blockIdx.y;
+    const int64_t t = blockIdx.x;
+    const int64_t t0 = t * kTile;
+    const int len = (int)(P - t0 < kTile ? P - t0 : kTile);
+    float* xr = x + (int64_t)r * ld + t0;
+    float* sr = s + (int64_t)r * ld + t0;
+    float* hr = xh + (int64_t)r * ld + t0;
+    __shared__ float ls[kTile], lh[kTile];
+    __shared__ uint8_t ds[kTile / kGran], dh[kTile / kGran];
+    if (!(len == kTile && (((uintptr_t)xr | (uintptr_t)sr | (uintptr_t)hr) & 15) == 0)) {   // partial /
+        apply_tile<NT, 16>(x, xh, s, ld, P, msgs, msg_ld, kpad, k, rec, n_local, M, alpha, g, ls, lh, ds, dh);
+        return;                                                                         // unaligned tile
+    }
+    // from here on the whole-tile path is branch-free up to the message phase, so the waitcnt pass
+    // can count the loads in flight exactly (a merge of two paths makes it wait for all of them)
+    const int tid = threadIdx.x;
+    constexpr int kQ = kTile / 4 / kTPB;       // quads per lane
+    const int32_t* deg = rec + mx::kPlanHeader;
+    const int d = deg[r];
+    const int nm = d + 1;                      // partners in matching order, then the own message
+    const int32_t* src = deg + 2 * n_local + r * M;
+    const float sw = __int_as_float(deg[n_local + r]);
+    // lane e < kPfMsgs of every wave: message e's slot, then its bounds in this tile -- two small
+    // vector loads issued BEFORE the tile stream (vector loads return in order), so the entry
+    // loads that need them can be issued right behind the stream
+    const int lane = tid & 63;
+    int my_lo = 0, my_hi = 0, my_sl = r;
+    {
+        const int e = lane < kPfMsgs ? lane : 0;
+        const int sl = lane < kPfMsgs && e < d ? src[e] : r;
+        my_sl = sl;
+        const Msg m = msg_at(msgs, msg_ld, kpad, k, sl);
+        if (lane < kPfMsgs && e < nm) {
+            my_lo = max(m.bnd[t], 0);              // clamped: a received message is not trusted
+            my_hi = min(m.bnd[t + 1], (int)k);     // to stay in range
+        }
+    }
+    f4 xv[kQ], sv[kQ], hv[kQ];
+#pragma unroll
+    for (int j = 0; j < kQ; ++j) {
+        const int q = j * kTPB + tid;
+        xv[j] = ld4<NT>(reinterpret_cast<const f4*>(xr) + q);
+        sv[j] = ld4<NT>(reinterpret_cast<const f4*>(sr) + q);
+        hv[j] = ld4<NT>(reinterpret_cast<const f4*>(hr) + q);
+    }
+    int plo[kPfMsgs], phi[kPfMsgs];
+    int64_t pix[kPfMsgs];
+    float pv[kPfMsgs];
+#pragma unroll
+    for (int e = 0; e < kPfMsgs; ++e) {
+        plo[e] = __builtin_amdgcn_readlane(my_lo, e);
+        phi[e] = __builtin_amdgcn_readlane(my_hi, e);
+        const int q = plo[e] + tid < phi[e] ? plo[e] + tid : 0;     // clamped: loads stay unconditional
+        const Msg m = msg_at(msgs, msg_ld, kpad, k, __builtin_amdgcn_readlane(my_sl, e));
+        pix[e] = m.ix[q];
+        pv[e] = m.v[q];
+    }
+#pragma unroll
+    for (int j = 0; j < kQ; ++j) {
+        const int q = j * kTPB + tid;
+        reinterpret_cast<f4*>(ls)[q] = sv[j];
+        reinterpret_cast<f4*>(lh)[q] = hv[j];
+    }
+    for (int i = tid; i < kTile / kGran; i += kTPB) ds[i] = dh[i] = 0;
+    __syncthreads();
+    auto upd = [&](bool own, int64_t ix, float vq) {
+        const int c = (int)(ix - t0);
+        if ((unsigned)c >= (unsigned)len) return;
+        ls[c] = __fadd_rn(ls[c], __fmul_rn(own ? sw : alpha, vq));
+        ds[c / kGran] = 1;
+        if (own) {
+            lh[c] = __fadd_rn(lh[c], vq);
+            dh[c / kGran] = 1;
+        }
+    };
+#pragma unroll
+    for (int e = 0; e < kPfMsgs; ++e) {
+        if (e >= nm) break;
+        const bool own = e == d;
+        if (plo[e] + tid < phi[e]) upd(own, pix[e], pv[e]);
+        if (phi[e] - plo[e] > kTPB) {
+            const Msg m = msg_at(msgs, msg_ld, kpad, k, __builtin_amdgcn_readlane(my_sl, e));
+            for (int q = plo[e] + kTPB + tid; q < phi[e]; q += kTPB) upd(own, m.ix[q], m.v[q]);
+        }
+        __syncthreads();                       // a later message may touch the same element
+    }
+    for (int e = kPfMsgs; e < nm; ++e) {
+        const bool own = e == d;
+        const Msg m = msg_at(msgs, msg_ld, kpad, k, own ? r : src[e]);
+        const int lo = max(m.bnd[t], 0), hi = min(m.bnd[t + 1], (int)k);
+        for (int q = lo + tid; q < hi; q += kTPB) upd(own, m.ix[q], m.v[q]);
+        __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < kQ; ++j) {
+        const int q = j * kTPB + tid;
+        f4 a = xv[j];
+        const f4 s4 = reinterpret_cast<const f4*>(ls)[q];
+        const f4 h4 = reinterpret_cast<const f4*>(lh)[q];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) a[c] = __builtin_fmaf(-g, h4[c], __builtin_fmaf(g, s4[c], a[c]));
+        st4<NT>(a, reinterpret_cast<f4*>(xr) + q);
+        if (ds[q / (kGran / 4)]) st4<NT>(s4, reinterpret_cast<f4*>(sr) + q);
+        if (dh[q / (kGran / 4)]) st4<NT>(h4, reinterpret_cast<f4*>(hr) + q);
+    }
+}
+
 unsigned clamp_grid(int64_t n, int64_t per, int64_t cap) {
     int64_t g = (n + per - 1) / per;
     if (g > cap) g = cap;
@@ -869,6 +1006,7 @@ int g_compact_blocks = 0;     // persistent compaction blocks over all rows; 0 =
                               // the per-block prologue and flush outweigh the parallelism; 8 rows
                               // 0.667 -> 0.656 ms at 2048, flat from 768 to 3072)
 int g_sample_pieces = 1;      // sampled 1024-element pieces per wave (sample_kernel grid)
+int g_apply_pf = 1;           // apply pass: 1 message entries prefetched under the tile stream, 0 plain
 int g_apply_nt = -1;          // apply pass non-temporal accesses: -1 auto (only with several rows), 0, 1
 int g_compact_store = 1;      // compaction candidate stores: 1 (default) a loop over the lane's kept elements,
                               // 0 one masked store pair per (step, element) (same-box A/B: 8 rows 639 -> 632 us,
@@ -916,6 +1054,11 @@ extern "C" int mx_topk_set(const char* key, int64_t value) {
         g_apply_nt = (int)value;
         return MX_OK;
     }
+    if (!strcmp(key, "apply_pf")) {
+        MX_CHECK(value == 0 || value == 1, "mx_topk_set: apply_pf %lld", (long long)value);
+        g_apply_pf = (int)value;
+        return MX_OK;
+    }
     if (!strcmp(key, "compact_store")) {
         MX_CHECK(value == 0 || value == 1, "mx_topk_set: compact_store %lld", (long long)value);
         g_compact_store = (int)value;
@@ -936,6 +1079,7 @@ extern "C" int64_t mx_topk_get(const char* key) {
     if (key && !strcmp(key, "cand_chunks")) return g_cand_chunks;
     if (key && !strcmp(key, "apply_nt")) return g_apply_nt;
     if (key && !strcmp(key, "compact_store")) return g_compact_store;
+    if (key && !strcmp(key, "apply_pf")) return g_apply_pf;
     mx::set_error("mx_topk_get: unknown key '%s'", key ? key : "(null)");
     return MX_ERR_INVALID;
 }
@@ -1044,7 +1188,8 @@ int choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t 
     const char* m = static_cast<const char*>(msgs);
     MX_CHECK(nt <= 0x7fffffff, "mx_choco_apply: P too large");
     const bool nt_hint = g_apply_nt < 0 ? n_local > 1 : g_apply_nt > 0;
-    auto kern = nt_hint ? apply_kernel<true, 16> : apply_kernel<false, 16>;
+    auto kern = g_apply_pf ? (nt_hint ? apply_kernel_pf<true> : apply_kernel_pf<false>)
+                           : (nt_hint ? apply_kernel<true, 16> : apply_kernel<false, 16>);
     hipLaunchKernelGGL(kern, dim3((unsigned)nt, n_local), dim3(kTPB),
                        0, st, x, xhat, s, ld, P, m,
                        msg_ld_bytes, kpad, k, rec, iter_dev, iter, words, n_local, M, alpha, gamma);

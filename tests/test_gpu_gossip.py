@@ -450,10 +450,12 @@ def test_choco_vs_oracle_larger(pkg, O, P, ratio, apply_nt):
         pkg.lib.mx_topk_set(b"apply_nt", saved)
 
 
-@pytest.mark.parametrize("knobs", [{"compact_store": 0}, {"compact_store": 1}, {"compact_store": 0, "apply_nt": 0}])
+@pytest.mark.parametrize("knobs", [{"compact_store": 0}, {"compact_store": 1}, {"compact_store": 0, "apply_nt": 0},
+                                   {"apply_pf": 0}, {"apply_pf": 0, "apply_nt": 1}])
 def test_choco_knob_variants(pkg, O, knobs):
     """Every Choco kernel variant selected by mx_topk_set (compaction stores looped over the kept
-    elements or one masked store pair per element; apply access hints) is bit-exact: the 8-row round (x / x_hat / s,
+    elements or one masked store pair per element; apply access hints; apply with or without the
+    message entries prefetched under the tile stream) is bit-exact: the 8-row round (x / x_hat / s,
     3 rounds) and the one-row top-k on the tie / far-threshold / sampled-fallback patterns."""
     saved = {k: int(pkg.lib.mx_topk_get(k.encode())) for k in knobs}
     for k, v in knobs.items():
@@ -476,6 +478,54 @@ def test_choco_knob_variants(pkg, O, knobs):
     finally:
         for k, v in saved.items():
             pkg.lib.mx_topk_set(k.encode(), v)
+
+
+@pytest.mark.parametrize("apply_pf", [1, 0])
+@pytest.mark.parametrize("case", ["concentrated", "high_degree"])
+def test_choco_apply_message_shapes(pkg, O, case, apply_pf):
+    """The apply pass on message shapes the synthetic rows never make: tiles where a message holds
+    thousands of entries (a contiguous block of large updates -> whole tiles selected, more than
+    the kTPB entries the prefetching kernel loads up front) and rows with more partners than it
+    prefetches (ER(12, 0.9): up to 11 partners + the own message).  3 rounds, x / x_hat / s bit-exact,
+    with and without the prefetching kernel; both P leave a partial last tile."""
+    import random as pyrandom
+    if case == "concentrated":
+        n, P, ratio = 8, 300_001, 0.9
+        gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, n, 4, True)
+    else:
+        pyrandom.seed(0)
+        n, P, ratio = 12, 70_001, 0.95
+        gp = pkg.GraphProcessor(pkg.erdos_renyi(n, 0.9, 3), 1.0, 0, n, 4, False)
+    M = len(gp.neighbors_info)
+    deg = (np.asarray(gp.neighbors_info) >= 0).sum(0)
+    if case == "high_degree":
+        assert deg.max() + 1 > 8
+    flags = np.ones((3, M), np.uint8)
+    flags[1, ::2] = 0
+    alpha = 1.0 / (deg.max() + 1)
+    topo = Topo(gp.neighbors_info, alpha, flags)
+    saved = int(pkg.lib.mx_topk_get(b"apply_pf"))
+    pkg._lib.check(pkg.lib.mx_topk_set(b"apply_pf", apply_pf))
+    try:
+        grp = pkg.ChocoWorkerGroup(topo, numel=P, ratio=ratio, consensus_lr=0.1)
+        X = np.stack([O.synth(700 + i, P) for i in range(n)])
+        if case == "concentrated":
+            X[:, 50_000:90_000] *= np.float32(1000.0)
+        XH, S = np.zeros_like(X), np.zeros_like(X)
+        grp.rows.copy_(torch.from_numpy(X))
+        k = O.topk_k(P, ratio)
+        for t, f in enumerate(flags):
+            if t:
+                D = np.stack([np.float32(0.01) * O.synth(9100 + 31 * t + i, P) for i in range(n)])
+                X += D
+                grp.rows.add_(torch.from_numpy(D).cuda())
+            grp.communicate()
+            O.choco_round(X, XH, S, topo.neighbors_info, f, alpha, k, 0.1)
+            assert np.array_equal(grp.rows.cpu().numpy().view(np.uint32), X.view(np.uint32)), f"round {t}"
+            assert np.array_equal(grp.x_hat[:, :P].cpu().numpy().view(np.uint32), XH.view(np.uint32)), t
+            assert np.array_equal(grp.s[:, :P].cpu().numpy().view(np.uint32), S.view(np.uint32)), t
+    finally:
+        pkg.lib.mx_topk_set(b"apply_pf", saved)
 
 
 def _choco_vs_oracle_larger(pkg, O, P, ratio):
