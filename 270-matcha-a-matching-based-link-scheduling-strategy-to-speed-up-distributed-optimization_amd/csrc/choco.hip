@@ -385,6 +385,7 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double
     };
     int64_t c = blockIdx.x;
     if (c < nc && whole(c)) issue(c);              // the first chunk flies while b_lo is resolved
+
     uint32_t b_lo = 0;
     if (!fallback) {
         int64_t want = R.k;
@@ -403,23 +404,12 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double
     for (int i = h0 + threadIdx.x; i < kTopBins; i += kTPB) h[i] = 0;
     uint32_t kept = 0;                             // this block's candidates (thread 0)
     __syncthreads();                               // h zeroed
-    for (int par = 0; c < nc; c += gridDim.x, par ^= 1) {
-        float d[4][4];
-        int n[4];
-        if (whole(c)) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-#pragma unroll
-                for (int e = 0; e < 4; ++e) d[j][e] = h4 ? __fsub_rn(ax[j][e], ah[j][e]) : ax[j][e];
-                n[j] = 4;
-            }
-        } else {
-            const int64_t q0 = c * (kChunk / 4) + wave * kSubQuads;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) n[j] = load_quad(v.x, v.xh, q0 + j * 64 + lane, R.P, vec, d[j]);
-        }
-        const int64_t cn = c + gridDim.x;
-        if (cn < nc && whole(cn)) issue(cn);
+    // whole chunks (prefetched one ahead in registers) and the partial / unaligned ones run in two
+    // separate loops over the same per-chunk step: one loop holding both load paths made the
+    // waitcnt pass wait for the next chunk's loads in the middle of every iteration
+    const int64_t nfull = vec ? R.P / kChunk : 0;  // chunks whole(c) holds for: [0, nfull)
+    int par = 0;
+    auto step = [&](int64_t c, float (&d)[4][4], const int (&n)[4]) {
         uint32_t keep = 0;                           // bit 4j + e: element e of step j is kept
         uint32_t ex[4], wt[4];                       // kept in lower lanes / in the wave, per step
         uint32_t tot = 0;
@@ -496,6 +486,25 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double
         }
         if (wave == 0 && lane < kRec) v.cnt[kRec * c + lane] = lane == 3 ? all : 0;   // the whole record
         if (threadIdx.x == 0) kept += all;
+        par ^= 1;
+    };
+    for (; c < nfull; c += gridDim.x) {
+        float d[4][4];
+        const int n[4] = {4, 4, 4, 4};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) d[j][e] = h4 ? __fsub_rn(ax[j][e], ah[j][e]) : ax[j][e];
+        if (c + gridDim.x < nfull) issue(c + gridDim.x);
+        step(c, d, n);
+    }
+    for (; c < nc; c += gridDim.x) {
+        float d[4][4];
+        int n[4];
+        const int64_t q0 = c * (kChunk / 4) + wave * kSubQuads;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) n[j] = load_quad(v.x, v.xh, q0 + j * 64 + lane, R.P, vec, d[j]);
+        step(c, d, n);
     }
     __syncthreads();
     uint32_t* out = fallback ? v.h12f : v.h12;

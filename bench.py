@@ -126,6 +126,17 @@ def pmc_traffic(kernel_prefix="mix_kernel"):
     return (max(vals) if vals else None), os.path.relpath(files[-1], ROOT)
 
 
+def guarded(name, fn):
+    """A secondary figure (after the timed region): an exception is reported in the line as
+    {"error": ...} instead of losing the headline line; traceback to stderr."""
+    try:
+        return fn()
+    except Exception as e:                       # noqa: BLE001 -- reported, not swallowed
+        import traceback
+        traceback.print_exc()
+        return {"error": f"{name}: {type(e).__name__}: {e}"}
+
+
 def max_over_ranks(x, world, dev):
     import torch.distributed as dist
     if world == 1:
@@ -673,13 +684,15 @@ def main():
                   "skipped_rounds": int((fl.sum(1) == 0).sum())}
         del gm
 
-    allreduce = allreduce_figure(group, n, world, dev, max(5, K // 5), 2) if args.allreduce else None
+    allreduce = (guarded("allreduce", lambda: allreduce_figure(group, n, world, dev, max(5, K // 5), 2))
+                 if args.allreduce else None)
 
-    choco = (choco_figure(pkg, GP, rank, world, max(20, K), 3, comm, dev, P=args.choco_params,
-                          placement=args.placement)
+    choco = (guarded("choco", lambda: choco_figure(pkg, GP, rank, world, max(20, K), 3, comm, dev,
+                                                    P=args.choco_params, placement=args.placement))
              if args.choco else None)
-    staged = staged_figure(pkg, GP, n, P, 3, W) if (world == 1 and args.staged) else None
-    configs = (config_figures(pkg, rank, world, n, max(10, K), 3, comm, dev, args.placement)
+    staged = guarded("staged", lambda: staged_figure(pkg, GP, n, P, 3, W)) if (world == 1 and args.staged) else None
+    configs = (guarded("configs", lambda: config_figures(pkg, rank, world, n, max(10, K), 3, comm, dev,
+                                                          args.placement))
                if args.configs and P == 25_600_000 else None)
 
     flags = np.asarray(GP.active_flags[timed_first:timed_first + K], np.uint8)
@@ -722,8 +735,11 @@ def main():
     avg_ms = float(step_ms.mean())
     exch_s = exch_per = probe = None
     if world > 1:             # (with --transport gloo: the same code over host staging, tests only)
-        exch_s, exch_per = exchange_only(group, timed_first, K, world, dev)
-        probe = p2p_probe(rank, world, P * 4, dev)
+        xo = guarded("exchange_only", lambda: exchange_only(group, timed_first, K, world, dev))
+        exch_s, exch_per = xo if isinstance(xo, tuple) else (None, None)
+        probe = guarded("p2p_probe", lambda: p2p_probe(rank, world, P * 4, dev))
+        if "error" in probe:
+            probe = None
     mix_avg_ms = float(mix_ms.mean())
     mix_bytes = float(np.mean(hbm_bytes))
     achieved = mix_bytes / (mix_avg_ms * 1e-3)
