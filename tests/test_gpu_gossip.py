@@ -279,6 +279,23 @@ def test_topk_sampled_floor_exact(pkg, O, stride, pieces, blocks, pattern):
     assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32))
 
 
+@pytest.mark.parametrize("pattern", ["layers", "ties", "gap"])
+def test_topk_unaligned_input(pkg, O, pattern):
+    """A tensor view 4 bytes off 16-byte alignment takes the compaction's element-load path for
+    every chunk (no prefetched whole chunks): same index set and values as the oracle."""
+    P, ratio = 300_001, 0.99
+    x = _topk_case(O, P, pattern)
+    k = O.topk_k(P, ratio)
+    ov, oi = O.topk_abs(x, k)
+    big = torch.zeros(P + 1, dtype=torch.float32, device="cuda")
+    big[1:] = torch.from_numpy(x).cuda()
+    xv = big[1:]
+    assert xv.data_ptr() % 16 != 0
+    v, i = pkg.get_top_k(xv, ratio)
+    assert np.array_equal(i.cpu().numpy(), oi)
+    assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32))
+
+
 def test_topk_work_reuse_and_tile_bounds(pkg, O):
     """One zero-filled scratch serves a sequence of calls of different P / k / patterns (incl. the
     fallback pass): each call leaves its histograms and counters zero (no zeroing launch runs),
