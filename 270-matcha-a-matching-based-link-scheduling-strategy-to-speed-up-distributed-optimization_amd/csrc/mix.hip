@@ -737,9 +737,9 @@ struct Tune {
                          // 1 = 9-64 slots only (<= 8: register-indexed / LDS-column), 0 = never
     int split = 0;       // row kernel sub-tiles per layout tile: 0 = auto (enough work items for
                          // the persistent grid), 1 / 2 / 4 = forced (capped by the geometry)
-    int flat_small = 1;  // row kernel: rounds of at most 4 x the persistent grid's work items launch
-                         // one workgroup per item instead (a second pass over the persistent grid
-                         // is a second memory round trip on latency-bound short rows)
+    int flat_small = 128;  // row kernel: rounds of at most flat_small x the persistent grid's work items
+                         // launch one workgroup per item instead (a second pass over the persistent
+                         // grid is a second memory round trip on latency-bound short rows); 0 = never
 };
 Tune g_tune;
 
@@ -799,7 +799,7 @@ int launch_rows(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* t
                 const uint8_t* seg_vec, int nseg, int n_slots, const int32_t* plan, int64_t iter, const int64_t* iter_dev,
                 int n_local, int M, float alpha, int64_t total_tiles, hipStream_t st) {
     const int64_t work = total_tiles * SPLIT;
-    const int64_t grid = (g_tune.flat_small && g_tune.grid == 0 && work <= 4 * grid_target()) ? work : grid_for(work);
+    const int64_t grid = (g_tune.flat_small > 0 && g_tune.grid == 0 && work <= (int64_t)g_tune.flat_small * grid_target()) ? work : grid_for(work);
     hipLaunchKernelGGL((mix_kernel_rows<NS, TW, NT, SPLIT>), dim3((unsigned)grid), dim3(kTPB),
                        0, st, seg_ptrs, seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan,
                        iter, iter_dev, n_local, M, alpha);
@@ -860,7 +860,7 @@ extern "C" int mx_mix_set(const char* key, int value) {
         MX_CHECK(value == 0 || value == 1 || value == 2 || value == 4, "mx_mix_set: split %d", value);
         slot = &g_tune.split;
     } else if (!strcmp(key, "flat_small")) {
-        MX_CHECK(value == 0 || value == 1, "mx_mix_set: flat_small %d", value);
+        MX_CHECK(value >= 0 && value <= 4096, "mx_mix_set: flat_small %d", value);
         slot = &g_tune.flat_small;
     }
     MX_CHECK(slot, "mx_mix_set: unknown key '%s'", key);

@@ -388,6 +388,18 @@ def test_mix_row_kernel_for_eight_slots(pkg, O, bpc, nt, u, sp):
         pkg.engine.set_mix_tuning(**saved)
 
 
+@pytest.mark.parametrize("flat,bpc", [(0, 2), (0, 1), (128, 2)])
+def test_mix_persistent_and_flat_grids(pkg, O, flat, bpc):
+    """The row kernel's grid: persistent workgroups striding over the tiles (flat_small = 0, several
+    tiles per workgroup) and one workgroup per work item -- bit-exact on the same layouts."""
+    saved = pkg.engine.mix_tuning()
+    try:
+        pkg.engine.set_mix_tuning(flat_small=flat, blocks_per_cu=bpc, rows=2)
+        _layouts_bit_exact(pkg, O)
+    finally:
+        pkg.engine.set_mix_tuning(**saved)
+
+
 def _layouts_bit_exact(pkg, O):
     """flat arena, ragged multi-segment layouts (graph 0) and an unaligned 16-slot graph, 3 rounds"""
     for gid, lens in ((0, [1, 3, 1024, 1027, 5, 4096 + 3, 0, 77, 10_000]), (2, [1, 3, 1027, 5, 9000]),
