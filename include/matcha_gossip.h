@@ -121,6 +121,9 @@ int mx_mix_tile(int n_slots);
  *   split          row kernel: sub-tiles of 256+ columns per layout tile, so short rows still
  *                  give every persistent workgroup work: 0 = auto (default), 1 / 2 / 4 = forced
  *                  (capped at 4 for 8/16 slots, 2 for 32, 1 for 64); layouts are unaffected
+ *   flat_small     row kernel: rounds of at most flat_small x (CUs x blocks_per_cu) work items
+ *                  launch one workgroup per item instead of the persistent grid (default 128;
+ *                  0 = always persistent; ignored when grid > 0)
  * "unroll" changes the tile size: rebuild layouts (mx_mix_layout) after setting it.
  * mx_mix_get returns the current value (negative on an unknown key).
  * mx_mix_kernel_name: the kernel mx_gossip_mix launches for n_slots under the current knobs
@@ -177,10 +180,18 @@ int mx_scatter(float* const* ptrs_dev, const int64_t* off_dev, int nseg, int64_t
 size_t mx_topk_work_bytes(int64_t P);
 /* Top-k knobs: "sample_stride" = sample every S-th 1024-element chunk for the candidate floor
  * (0 = auto, about 2^18 sampled elements per row; 1 = exact full histogram, no sampling);
- * "compact_blocks" = persistent workgroups of the full pass, over all rows (0 = auto: 1024 for
- * one row, 2048 for several);
+ * "compact_blocks" = persistent workgroups of the full pass, over all rows (0 = auto: 640 for
+ * one row, 2560 for several);
  * "sample_pieces" = sampled 1024-element pieces per wave of the sampling pass (default 1);
- * "cand_chunks" = candidate regions per wave of the candidate-histogram / mark passes (default 2). */
+ * "cand_chunks" = candidate regions per wave of the candidate-histogram / mark passes (0 = auto:
+ * 4 for one row, 8 for several);
+ * "compact_store" = 1 (default): candidate stores looped over each lane's kept elements, 0: one
+ * masked store pair per element;
+ * "apply_nt" = mx_choco_apply's access hints: -1 (default) non-temporal with several rows only,
+ * 0 / 1 forced;
+ * "apply_pf" = 1 (default): mx_choco_apply prefetches every message's tile bounds and first entries
+ * under the tile stream, 0: the plain kernel (bounds and entries loaded per message).
+ * Knobs tune speed only, never results. */
 int mx_topk_set(const char* key, int64_t value);
 int64_t mx_topk_get(const char* key);
 int mx_topk_abs_diff(const float* x, const float* x_hat, int64_t P, int64_t k, float* vals,
