@@ -737,7 +737,7 @@ struct Tune {
                          // 1 = 9-64 slots only (<= 8: register-indexed / LDS-column), 0 = never
     int split = 0;       // row kernel sub-tiles per layout tile: 0 = auto (enough work items for
                          // the persistent grid), 1 / 2 / 4 = forced (capped by the geometry)
-    int flat_small = 128;  // row kernel: rounds of at most flat_small x the persistent grid's work items
+    int flat_small = 256;  // row kernel: rounds of at most flat_small x the persistent grid's work items
                          // launch one workgroup per item instead (a second pass over the persistent
                          // grid is a second memory round trip on latency-bound short rows); 0 = never
 };
@@ -779,6 +779,12 @@ int row_split(int ns, int64_t total_tiles) {
     if (g_tune.split > 0) return g_tune.split < cap ? g_tune.split : cap;
     int s = 1;
     while (s < cap && 2 * total_tiles * s < 3 * grid_target()) s *= 2;
+    // with one workgroup per work item (flat_small), 512-column sub-tiles beat whole 1024-column
+    // tiles at every size measured for 8 slots (2M-36.5M params: -1 to -6 %; headline 283.8 ->
+    // 272.3 us, tools/split_sweep.py); persistent grids keep whole tiles (split 2 was slower there)
+    if (s < 2 && ns <= 16 && g_tune.flat_small > 0 && g_tune.grid == 0 &&
+        2 * total_tiles <= (int64_t)g_tune.flat_small * grid_target())
+        s = 2;
     return s;
 }
 

@@ -119,10 +119,11 @@ int mx_mix_tile(int n_slots);
  *                  partner lists): 2 = every slot count (default; <= 8 slots needs unroll 1 or 2),
  *                  1 = 9-64 slots only, 0 = never
  *   split          row kernel: sub-tiles of 256+ columns per layout tile, so short rows still
- *                  give every persistent workgroup work: 0 = auto (default), 1 / 2 / 4 = forced
+ *                  give every persistent workgroup work, and 2 for 8-16 slots on flat grids:
+ *                  0 = auto (default), 1 / 2 / 4 = forced
  *                  (capped at 4 for 8/16 slots, 2 for 32, 1 for 64); layouts are unaffected
  *   flat_small     row kernel: rounds of at most flat_small x (CUs x blocks_per_cu) work items
- *                  launch one workgroup per item instead of the persistent grid (default 128;
+ *                  launch one workgroup per item instead of the persistent grid (default 256;
  *                  0 = always persistent; ignored when grid > 0)
  * "unroll" changes the tile size: rebuild layouts (mx_mix_layout) after setting it.
  * mx_mix_get returns the current value (negative on an unknown key).
