@@ -30,7 +30,9 @@ def trace_gaps(path, K=20):
     replay = [i for i, nm in enumerate(names) if "mix_kernel_rows<8, 256" in nm]
     timed = None
     if replay:
-        head = [r for r in allrows[:replay[0]] if "mix_kernel_rows<8, 1024" in r["Kernel_Name"]][-K:]
+        before = [r for r in allrows[:replay[0]] if "mix_kernel" in r["Kernel_Name"]]
+        hk = before[-1]["Kernel_Name"] if before else None      # the timed rounds' kernel (whatever split)
+        head = [r for r in before if r["Kernel_Name"] == hk][-K:]
         if len(head) == K:
             st = np.array([int(r["Start_Timestamp"]) for r in head], np.int64)
             en = np.array([int(r["End_Timestamp"]) for r in head], np.int64)
