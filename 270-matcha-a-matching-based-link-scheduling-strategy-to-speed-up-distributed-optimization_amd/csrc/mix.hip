@@ -805,7 +805,10 @@ int launch_rows(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* t
                 const uint8_t* seg_vec, int nseg, int n_slots, const int32_t* plan, int64_t iter, const int64_t* iter_dev,
                 int n_local, int M, float alpha, int64_t total_tiles, hipStream_t st) {
     const int64_t work = total_tiles * SPLIT;
-    const int64_t grid = (g_tune.flat_small > 0 && g_tune.grid == 0 && work <= (int64_t)g_tune.flat_small * grid_target()) ? work : grid_for(work);
+    // one workgroup per item only for 8-16 slots: with 32 / 64 slots (narrower tiles, longer partner
+    // walks) the persistent grid stays faster (ER(32): 286 vs 350 us, ER(64): 324 vs 426 us)
+    const int64_t grid = (NS <= 16 && g_tune.flat_small > 0 && g_tune.grid == 0 &&
+                          work <= (int64_t)g_tune.flat_small * grid_target()) ? work : grid_for(work);
     hipLaunchKernelGGL((mix_kernel_rows<NS, TW, NT, SPLIT>), dim3((unsigned)grid), dim3(kTPB),
                        0, st, seg_ptrs, seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan,
                        iter, iter_dev, n_local, M, alpha);

@@ -122,7 +122,7 @@ int mx_mix_tile(int n_slots);
  *                  give every persistent workgroup work, and 2 for 8-16 slots on flat grids:
  *                  0 = auto (default), 1 / 2 / 4 = forced
  *                  (capped at 4 for 8/16 slots, 2 for 32, 1 for 64); layouts are unaffected
- *   flat_small     row kernel: rounds of at most flat_small x (CUs x blocks_per_cu) work items
+ *   flat_small     row kernel, 8-16 slots: rounds of at most flat_small x (CUs x blocks_per_cu) work items
  *                  launch one workgroup per item instead of the persistent grid (default 256;
  *                  0 = always persistent; ignored when grid > 0)
  * "unroll" changes the tile size: rebuild layouts (mx_mix_layout) after setting it.

@@ -1,4 +1,4 @@
-"""Row kernel sub-tiles (split 1 / 2) x grid (persistent: flat_small 0 / one workgroup per item:
+"""Row kernel sub-tiles (split 1 / 2) x grid (GRAPH = topology id: 0 = 8 workers, 2 = 16) (persistent: flat_small 0 / one workgroup per item:
 flat_small 256) on 8 workers x P, graph 0, every matching active.  Mixing kernel HIP events,
 median of 60, 3 interleaved repeats."""
 import importlib
@@ -15,11 +15,19 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 pkg = importlib.import_module("270-matcha-a-matching-based-link-scheduling-strategy-to-speed-up-distributed-optimization_amd")
 from conftest import Topo  # noqa: E402
 
-n = 8
-gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, n, 4, True)
-topo = Topo(gp.neighbors_info, 2 / 7, np.ones((8, 5), np.uint8))
+GRAPH = os.environ.get("GRAPH", "0")
+if GRAPH.startswith("er"):               # er<n>: ER(n, 0.1), host decomposition (widebench's graphs)
+    import random
+    random.seed(0)
+    n = int(GRAPH[2:])
+    gp = pkg.GraphProcessor(pkg.erdos_renyi(n, 0.1, 1234), 1.0, 0, n, 4, False)
+else:
+    n = pkg.GRAPH_SIZES[int(GRAPH)]
+    gp = pkg.GraphProcessor(pkg.select_graph(int(GRAPH)), 1.0, 0, n, 4, True)
+M = len(gp.neighbors_info)
+topo = Topo(gp.neighbors_info, 1.0 / (M + 1), np.ones((8, M), np.uint8))
 sizes = [int(x) for x in os.environ.get("SIZES", "2000000,4000000,8000000,25600000,36546980").split(",")]
-variants = [(1, 0), (1, 256), (2, 0), (2, 256)]
+variants = [tuple(int(y) for y in v.split(":")) for v in os.environ.get("VARIANTS", "1:0,1:256,2:0,2:256").split(",")]
 
 
 def kernel_us(grp, reps=60):
@@ -48,7 +56,7 @@ for P in sizes:
     pkg.engine.set_mix_tuning(**saved)
     for (sp, fl), xs in res.items():
         us = float(np.median(xs))
-        print(json.dumps({"P": P, "split": sp, "flat_small": fl, "kernel_us": round(us, 1),
+        print(json.dumps({"graph": GRAPH, "P": P, "split": sp, "flat_small": fl, "kernel_us": round(us, 1),
                           "TBps": round(2 * n * P * 4 / us / 1e6, 3)}), flush=True)
     del grp
     torch.cuda.empty_cache()
