@@ -727,7 +727,8 @@ Cfg pick(int n_slots) {
 struct Tune {
     int blocks_per_cu = 2;
     int unroll = 1;      // 1, 2 or 4 accesses per lane per row per tile (NS = 8 configs only; LDS kernel <= 2)
-    int nontemporal = 1;
+    int nontemporal = 2;  // 1 / 0: streaming hints on / off; 2 = auto (row kernel: off for rows of
+                          // 32-320 MB, about the Infinity Cache; every other kernel: on)
     int prefetch = 0;
     int regidx = 1;      // 1: register-indexed kernel (n_slots <= 8; wider spills), 0: LDS-column kernel
     int chunked = 0;     // single-segment layouts: 1 = equal contiguous chunk per workgroup, 0 = tile stride
@@ -846,7 +847,7 @@ extern "C" int mx_mix_set(const char* key, int value) {
         slot = &g_tune.unroll;
     } else if (!strcmp(key, "nontemporal")) {
         slot = &g_tune.nontemporal;
-        value = value ? 1 : 0;
+        value = value == 2 ? 2 : (value ? 1 : 0);
     } else if (!strcmp(key, "prefetch")) {
         slot = &g_tune.prefetch;
         value = value ? 1 : 0;
@@ -1022,7 +1023,14 @@ int gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev, const int
         default: return launch_reg<N, U, true, U == 1>(MX_ARGS);              \
     }
     if ((g_tune.rows && c.ns >= 16) || (g_tune.rows == 2 && unroll_for(8) <= 2)) {
-        const bool nt = g_tune.nontemporal != 0;
+        // auto: rows of 32-320 MB (about the 256 MB Infinity Cache) keep ordinary (cacheable)
+        // accesses -- back-to-back rounds then find them on die (8 x 2M params 25.1 -> 23.7 us,
+        // 8 x 8M 90.3 -> 75.2 us, 8 x 10M 111.5 -> 107.7 us); above, the streaming hints win
+        // (8 x 12M 138.9 -> 130.8 us, headline 294 -> 272 us), and below, where the rows fit in the
+        // L2s, too (8 x 181k / 666k: 5-7 % slower with ordinary accesses; tools/sessions/r2_s80.sh)
+        const int64_t ws = total_tiles * (int64_t)mx_mix_tile(n_slots) * n_slots * 4;
+        const bool nt = g_tune.nontemporal == 2 ? (ws <= ((int64_t)32 << 20) || ws > ((int64_t)320 << 20))
+                                                : g_tune.nontemporal != 0;
         if (c.ns == 8 && unroll_for(8) == 2)
             return nt ? launch_rows<8, 2048, true>(MX_ARGS) : launch_rows<8, 2048, false>(MX_ARGS);
         const int sp = row_split(c.ns, total_tiles);

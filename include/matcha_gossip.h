@@ -108,7 +108,8 @@ int mx_mix_tile(int n_slots);
  *   blocks_per_cu  persistent workgroups per CU (grid = CUs x this, capped by the tile count)
  *   unroll         16-byte accesses per lane per slot per iteration, n_slots <= 8: 1, 2 or 4
  *                  (register-indexed kernel), 1 or 2 (LDS kernel)
- *   nontemporal    streaming (non-temporal) load/store hints
+ *   nontemporal    streaming (non-temporal) load/store hints: 1 on, 0 off, 2 = auto (default: the row
+ *                  kernel drops them for rows of 32-320 MB, about the Infinity Cache)
  *   prefetch       issue the next iteration's loads before mixing/storing the current one
  *   regidx         register-indexed kernel (no LDS) instead of the LDS-column one, n_slots <= 8
  *   chunked        single-segment layouts: equal contiguous chunk per workgroup (1) or tile stride (0)

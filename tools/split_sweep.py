@@ -28,6 +28,7 @@ M = len(gp.neighbors_info)
 topo = Topo(gp.neighbors_info, 1.0 / (M + 1), np.ones((8, M), np.uint8))
 sizes = [int(x) for x in os.environ.get("SIZES", "2000000,4000000,8000000,25600000,36546980").split(",")]
 variants = [tuple(int(y) for y in v.split(":")) for v in os.environ.get("VARIANTS", "1:0,1:256,2:0,2:256").split(",")]
+NT = [int(x) for x in os.environ.get("NT", "1").split(",")]   # nontemporal hint settings to cross with
 
 
 def kernel_us(grp, reps=60):
@@ -48,15 +49,15 @@ for P in sizes:
     grp = pkg.VirtualWorkerGroup(topo, numel=P)
     for i in range(n):
         pkg.lib.mx_synth_fill(grp.rows[i].data_ptr(), P, 1234 + i, None)
-    res = {v: [] for v in variants}
+    res = {(v, nt): [] for v in variants for nt in NT}
     for rep in range(3):
-        for sp, fl in variants:
-            pkg.engine.set_mix_tuning(split=sp, flat_small=fl)
-            res[(sp, fl)].append(kernel_us(grp))
+        for (sp, fl), nt in res:
+            pkg.engine.set_mix_tuning(split=sp, flat_small=fl, nontemporal=nt)
+            res[((sp, fl), nt)].append(kernel_us(grp))
     pkg.engine.set_mix_tuning(**saved)
-    for (sp, fl), xs in res.items():
+    for ((sp, fl), nt), xs in res.items():
         us = float(np.median(xs))
-        print(json.dumps({"graph": GRAPH, "P": P, "split": sp, "flat_small": fl, "kernel_us": round(us, 1),
+        print(json.dumps({"graph": GRAPH, "P": P, "split": sp, "flat_small": fl, "nontemporal": nt, "kernel_us": round(us, 1),
                           "TBps": round(2 * n * P * 4 / us / 1e6, 3)}), flush=True)
     del grp
     torch.cuda.empty_cache()
