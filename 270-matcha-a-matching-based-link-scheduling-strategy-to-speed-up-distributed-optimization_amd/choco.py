@@ -12,7 +12,7 @@ import numpy as np
 import torch
 
 from ._lib import check, lib, require_device, stream_ptr
-from .engine import GossipEngine, ROW_ALIGN, default_comm, owner_table, partition
+from .engine import GossipEngine, PullTransport, ROW_ALIGN, default_comm, owner_table, partition
 
 
 def topk_count(P, ratio):
@@ -33,6 +33,9 @@ class ChocoWorkerGroup:
         self.workers = block_workers(self.placement, self.row_base, self.n_local)
         if nranks > 1 and comm is None:
             comm = default_comm()
+        if isinstance(comm, PullTransport):
+            raise TypeError("ChocoWorkerGroup: PullTransport carries whole-row rounds only "
+                            "(VirtualWorkerGroup); Choco messages need the RCCL transport")
         self.engine = GossipEngine(topology, self.row_base, self.n_local, comm=comm,
                                    owner=owner_table(n, nranks))
         self.topology = topology

@@ -181,6 +181,15 @@ class _Staging:
                 t.copy_(pin[o:o + t.numel()].view_as(t))
 
 
+def _refuse_pull(transport, who):
+    """The pull transport serves whole-row gossip only (VirtualWorkerGroup): Choco messages and
+    the centralized all-gather need a transport that moves buffers."""
+    from .engine import PullTransport
+    if isinstance(transport, PullTransport):
+        raise TypeError(f"{who}: PullTransport carries decentralized whole-row rounds only "
+                        "(decenCommunicator / VirtualWorkerGroup); use the RCCL transport (transport=None)")
+
+
 class Communicator(object):
     """communicator.py:10-43 -- communicate(model) -> seconds spent averaging.
 
@@ -228,12 +237,30 @@ class decenCommunicator(Communicator):
             # same size (e.g. parameters re-created): adopt the new tensors into the same row
             self._stage = _Staging(params, self._group.rows[0])
         else:
+            # a new parameter count: a new row.  The old group's transport buffers are released
+            # first (under PullTransport this re-bind is collective: every rank must re-bind in the
+            # same call, as every rank's model changes size together in data-parallel training)
+            self.close()
             on_gpu = all(p.device.type == "cuda" for p in params)
             self._group = VirtualWorkerGroup(self.topology, [model] if on_gpu else None,
                                              numel=None if on_gpu else n, rank=self.rank,
                                              nranks=self.size, comm=self._comm(), idle_rows=self.idle_rows)
             self._stage = _Staging(params, self._group.rows[0])
         self._model_params = params
+
+    def close(self):
+        """Release the worker group (and the pull transport's shared buffers, if any)."""
+        if self._group is not None:
+            self._group.close()
+            self._group = None
+            self._stage = None
+            self._model_params = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:                        # interpreter teardown: nothing left to release
+            pass
 
     def communicate(self, model):
         active_flags = self.topology.active_flags[self.iter]
@@ -257,6 +284,7 @@ class ChocoCommunicator(Communicator):
     """communicator.py:161-268 -- top-k compressed gossip with persistent x_hat / s."""
 
     def __init__(self, rank, size, topology, ratio, consensus_lr, *, transport=None):
+        _refuse_pull(transport, "ChocoCommunicator")
         super(ChocoCommunicator, self).__init__(rank, size, transport=transport)
         self.topology = topology
         self.neighbor_weight = topology.neighbor_weight
@@ -320,15 +348,20 @@ class centralizedCommunicator(Communicator):
     """communicator.py:46-76 -- all-reduce averaging: x = allreduce_sum(x) / size.
 
     order -- how the ranks' vectors are summed:
-      "tree" (default): bit-identical to the reference's comm.allreduce(obj, op=MPI.SUM) under
-          mpi4py's default object reduction (a binomial tree to rank 0, then a broadcast):
-          every vector is all-gathered over RCCL and each rank sums them in that order on its GPU
-          (mx_allreduce_mean_ordered / mx_mean_rows) before the division of communicator.py:62;
+      "tree" (default): the order of the reference's comm.allreduce(obj, op=MPI.SUM) under
+          mpi4py's default object reduction (a binomial tree to rank 0, then a broadcast), as
+          restated from mpi4py's published algorithm (tests/reforder.py; mpi4py is not installed
+          here, so parity against mpi4py itself is unpinned): every vector is all-gathered over
+          RCCL and each rank sums them in that order on its GPU (mx_allreduce_mean_ordered /
+          mx_mean_rows, any world size) before the division of communicator.py:62;
       "sequential": the same with a rank-order left fold (mpi4py with rc.fast_reduce off);
-      "ring": RCCL's own all-reduce + division (mx_allreduce_mean) -- less traffic per rank, equal
-          to the reference within fp32 reassociation only."""
+      "ring": RCCL's own all-reduce + division (mx_allreduce_mean) -- less traffic and memory per
+          rank, equal to the reference within fp32 reassociation only.
+    Memory: "tree" / "sequential" keep a gather buffer of size x P floats per rank (the all-gather
+    target; e.g. 8 ranks x 25.6M params = 819 MB), "ring" none."""
 
     def __init__(self, rank, size, *, transport=None, order="tree"):
+        _refuse_pull(transport, "centralizedCommunicator")
         super(centralizedCommunicator, self).__init__(rank, size, transport=transport)
         if order not in ORDERS and order != "ring":
             raise ValueError(f"order must be 'tree', 'sequential' or 'ring', not {order!r}")

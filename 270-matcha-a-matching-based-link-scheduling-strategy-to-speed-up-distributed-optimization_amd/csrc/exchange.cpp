@@ -17,6 +17,10 @@
 // receives from one peer pair up in posting order, as RCCL point-to-point requires.
 #include <rccl/rccl.h>
 
+#include <atomic>
+#include <chrono>
+#include <cstdlib>
+#include <thread>
 #include <vector>
 
 #include "mx_common.h"
@@ -40,20 +44,116 @@ extern "C" int mx_rccl_unique_id(void* id_out) {
     return MX_OK;
 }
 
-extern "C" int mx_rccl_init(const void* id, int nranks, int rank, void** comm_out) {
-    MX_CHECK(id && comm_out, "mx_rccl_init: null pointer");
-    MX_CHECK(nranks >= 1 && rank >= 0 && rank < nranks, "mx_rccl_init: rank %d of %d", rank, nranks);
+// ---------------------------------------------------------------------------------- deadlines
+// A peer that never arrives (a dead rank, a rank that skipped a collective) must not hang the
+// process: the communicator is created NON-blocking (ncclConfig_t.blocking = 0), so
+// ncclCommInitRankConfig, ncclGroupEnd and the collectives return at once (ncclInProgress) and
+// wait_comm() polls ncclCommGetAsyncError against a deadline.  On expiry the call returns
+// MX_ERR_RCCL ("timed out"); a timed-out init is aborted here, a timed-out operation leaves the
+// communicator to the caller (mx_rccl_abort).  The deadline is the init call's timeout_ms, kept
+// per process (MX_RCCL_TIMEOUT_S or 300 s for mx_rccl_init).
+namespace {
+std::atomic<int64_t> g_op_timeout_ms{300000};
+
+int64_t env_timeout_ms() {
+    const char* e = getenv("MX_RCCL_TIMEOUT_S");
+    if (e && *e) {
+        const double s = atof(e);
+        if (s > 0) return (int64_t)(s * 1000.0);
+    }
+    return 300000;
+}
+
+// ncclSuccess once every operation issued on `comm` is enqueued (non-blocking communicators), the
+// async error if one occurred, ncclInProgress if the deadline passed first.
+ncclResult_t wait_comm(ncclComm_t comm, int64_t timeout_ms) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int spin = 0;; ++spin) {
+        ncclResult_t st = ncclSuccess;
+        const ncclResult_t r = ncclCommGetAsyncError(comm, &st);
+        if (r != ncclSuccess) return r;
+        if (st != ncclInProgress) return st;
+        const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+        if (ms >= timeout_ms) return ncclInProgress;
+        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(spin > 4096 ? 1000 : 20));
+    }
+}
+
+// `r` is what an RCCL call on `comm` returned: wait for ncclInProgress to resolve.
+int finish(ncclComm_t comm, ncclResult_t r, const char* what) {
+    if (r == ncclInProgress) r = wait_comm(comm, g_op_timeout_ms.load());
+    if (r == ncclInProgress) {
+        mx::set_error("%s: timed out after %lld ms (a peer rank never joined)", what, (long long)g_op_timeout_ms.load());
+        return MX_ERR_RCCL;
+    }
+    if (r != ncclSuccess) {
+        mx::set_error("%s -> %s", what, ncclGetErrorString(r));
+        return MX_ERR_RCCL;
+    }
+    return MX_OK;
+}
+}  // namespace
+
+#define MX_NCCL_ON(comm, call)                                   \
+    do {                                                         \
+        int rc_ = finish((comm), (call), #call);                 \
+        if (rc_ != MX_OK) return rc_;                            \
+    } while (0)
+
+extern "C" int mx_rccl_init_timeout(const void* id, int nranks, int rank, int64_t timeout_ms, void** comm_out,
+                                    int* nonblocking_out) {
+    MX_CHECK(id && comm_out, "mx_rccl_init_timeout: null pointer");
+    MX_CHECK(nranks >= 1 && rank >= 0 && rank < nranks, "mx_rccl_init_timeout: rank %d of %d", rank, nranks);
+    MX_CHECK(timeout_ms > 0, "mx_rccl_init_timeout: timeout_ms %lld", (long long)timeout_ms);
     ncclUniqueId uid;
     memcpy(&uid, id, sizeof(uid));
     ncclComm_t comm = nullptr;
-    MX_NCCL(ncclCommInitRank(&comm, nranks, uid, rank));
-    *comm_out = comm;
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclResult_t r = ncclCommInitRankConfig(&comm, nranks, uid, rank, &cfg);
+    if (r == ncclInProgress || (r == ncclSuccess && comm)) {
+        r = wait_comm(comm, timeout_ms);
+        if (r != ncclSuccess) {
+            (void)ncclCommAbort(comm);
+            if (r == ncclInProgress)
+                mx::set_error("mx_rccl_init: rank %d of %d: no complete communicator within %lld ms (a peer rank "
+                              "never joined)", rank, nranks, (long long)timeout_ms);
+            else
+                mx::set_error("mx_rccl_init: ncclCommInitRankConfig -> %s", ncclGetErrorString(r));
+            return MX_ERR_RCCL;
+        }
+        g_op_timeout_ms.store(timeout_ms);
+        if (nonblocking_out) *nonblocking_out = 1;
+        *comm_out = comm;
+        return MX_OK;
+    }
+    mx::set_error("mx_rccl_init: ncclCommInitRankConfig(blocking = 0) -> %s", ncclGetErrorString(r));
+    return MX_ERR_RCCL;
+}
+
+extern "C" int mx_rccl_init(const void* id, int nranks, int rank, void** comm_out) {
+    return mx_rccl_init_timeout(id, nranks, rank, env_timeout_ms(), comm_out, nullptr);
+}
+
+extern "C" int mx_rccl_abort(void* comm) {
+    if (!comm) return MX_OK;
+    MX_NCCL(ncclCommAbort(reinterpret_cast<ncclComm_t>(comm)));
     return MX_OK;
 }
 
-extern "C" int mx_rccl_destroy(void* comm) {
-    if (!comm) return MX_OK;
-    MX_NCCL(ncclCommDestroy(reinterpret_cast<ncclComm_t>(comm)));
+extern "C" int mx_rccl_destroy(void* comm_v) {
+    if (!comm_v) return MX_OK;
+    ncclComm_t comm = reinterpret_cast<ncclComm_t>(comm_v);
+    // drain what is still queued, then release; a communicator whose peers are gone is aborted
+    if (finish(comm, ncclCommFinalize(comm), "ncclCommFinalize") != MX_OK) {
+        (void)ncclCommAbort(comm);
+        return MX_ERR_RCCL;
+    }
+    const ncclResult_t r = ncclCommDestroy(comm);       // local once finalized
+    if (r != ncclSuccess && r != ncclInProgress) {
+        mx::set_error("ncclCommDestroy -> %s", ncclGetErrorString(r));
+        return MX_ERR_RCCL;
+    }
     return MX_OK;
 }
 
@@ -134,13 +234,13 @@ extern "C" int mx_exchange_post(void* comm_v, const int32_t* ops, int n_ops, voi
             r = ncclRecv(static_cast<char*>(slab) + (int64_t)o[2] * slab_ld_bytes, count, ncclFloat32,
                          o[1], comm, st);
         }
-        if (r != ncclSuccess) {
-            ncclGroupEnd();
+        if (r != ncclSuccess && r != ncclInProgress) {
+            (void)finish(comm, ncclGroupEnd(), "ncclGroupEnd");
             mx::set_error("%s: %s", o[0] == 0 ? "ncclSend" : "ncclRecv", ncclGetErrorString(r));
             return MX_ERR_RCCL;
         }
     }
-    MX_NCCL(ncclGroupEnd());
+    MX_NCCL_ON(comm, ncclGroupEnd());
     return MX_OK;
 }
 
@@ -179,15 +279,43 @@ __global__ void div_kernel(float* __restrict__ x, int64_t n, float d) {
 //   TREE = 0  rank order ((x0 + x1) + x2) + ... (mpi4py with fast_reduce off: allgather, then
 //             functools-style left fold)
 // MAXR bounds nrows; the tree runs over a register array with compile-time indices.
+//   TREE = 2  the same binomial tree for any nrows, row by row: a binary counter of partial sums
+//             (stack[l] = the sum of the last complete block of 2^l rows; pushing a row merges
+//             stack[l] + carry while bit l of the count is set) and a right-to-left fold of the
+//             stack at the end -- ((x0 + x1) + (x2 + x3)) + ((x4 + x5) + x6) for 7 rows, exactly
+//             the mask loop's order (checked against it for 1..300 rows in tests/reforder.py).
 template <int TREE, int MAXR>
 __global__ __launch_bounds__(256) void mean_rows_kernel(const float* rows, int nrows, int64_t ld,
                                                         int64_t count, float size, float* out) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x) {
         float acc;
-        if (TREE) {
+        if (TREE == 2) {
+            constexpr int L = 24;                         // up to 2^24 rows
+            float stack[L];
+#pragma unroll
+            for (int l = 0; l < L; ++l) stack[l] = 0.0f;
+            for (int r = 0; r < nrows; ++r) {
+                float p = rows[(int64_t)r * ld + i];
+                bool carry = true;
+#pragma unroll
+                for (int l = 0; l < L; ++l) {
+                    const bool set = (r >> l) & 1;
+                    if (carry && set) p = stack[l] + p;
+                    else if (carry) { stack[l] = p; carry = false; }
+                }
+            }
+            bool have = false;
+            acc = 0.0f;
+#pragma unroll
+            for (int l = 0; l < L; ++l)
+                if ((nrows >> l) & 1) {
+                    acc = have ? stack[l] + acc : stack[l];
+                    have = true;
+                }
+        } else if (TREE) {
             float v[MAXR];
 #pragma unroll
-            for (int r = 0; r < MAXR; ++r) v[r] = r < nrows ? rows[r * ld + i] : 0.0f;
+            for (int r = 0; r < MAXR; ++r) v[r] = r < nrows ? rows[(int64_t)r * ld + i] : 0.0f;
 #pragma unroll
             for (int m = 1; m < MAXR; m <<= 1)
 #pragma unroll
@@ -196,7 +324,7 @@ __global__ __launch_bounds__(256) void mean_rows_kernel(const float* rows, int n
             acc = v[0];
         } else {
             acc = rows[i];
-            for (int r = 1; r < nrows; ++r) acc = acc + rows[r * ld + i];
+            for (int r = 1; r < nrows; ++r) acc = acc + rows[(int64_t)r * ld + i];
         }
         out[i] = acc / size;
     }
@@ -212,8 +340,8 @@ extern "C" int mx_allreduce_mean(void* comm_v, float* buf, int64_t count, int nr
     MX_CHECK(comm_v && (buf || count == 0) && nranks >= 1, "mx_allreduce_mean: bad arguments");
     if (count == 0) return MX_OK;
     hipStream_t st = mx::as_stream(stream);
-    MX_NCCL(ncclAllReduce(buf, buf, (size_t)count, ncclFloat32, ncclSum,
-                          reinterpret_cast<ncclComm_t>(comm_v), st));
+    ncclComm_t comm = reinterpret_cast<ncclComm_t>(comm_v);
+    MX_NCCL_ON(comm, ncclAllReduce(buf, buf, (size_t)count, ncclFloat32, ncclSum, comm, st));
     hipLaunchKernelGGL(div_kernel, dim3(grid_of(count)), dim3(256), 0, st, buf, count, (float)nranks);
     MX_LAUNCH_CHECK();
     return MX_OK;
@@ -221,8 +349,8 @@ extern "C" int mx_allreduce_mean(void* comm_v, float* buf, int64_t count, int nr
 
 extern "C" int mx_mean_rows(const float* rows, int nrows, int64_t ld, int64_t count, int order, float* out,
                             void* stream) {
-    MX_CHECK(rows && out && nrows >= 1 && nrows <= 64 && ld >= count && count >= 0,
-             "mx_mean_rows: nrows=%d (1..64) ld=%lld count=%lld", nrows, (long long)ld, (long long)count);
+    MX_CHECK(rows && out && nrows >= 1 && nrows <= (1 << 24) && ld >= count && count >= 0,
+             "mx_mean_rows: nrows=%d (1..2^24) ld=%lld count=%lld", nrows, (long long)ld, (long long)count);
     MX_CHECK(order == 0 || order == 1, "mx_mean_rows: order %d (0 tree, 1 rank order)", order);
     if (count == 0) return MX_OK;
     hipStream_t st = mx::as_stream(stream);
@@ -233,8 +361,11 @@ extern "C" int mx_mean_rows(const float* rows, int nrows, int64_t ld, int64_t co
     } else if (nrows <= 8) {
         hipLaunchKernelGGL((mean_rows_kernel<1, 8>), dim3(grid_of(count)), dim3(256), 0, st, rows, nrows, ld, count, d,
                            out);
-    } else {
+    } else if (nrows <= 64) {
         hipLaunchKernelGGL((mean_rows_kernel<1, 64>), dim3(grid_of(count)), dim3(256), 0, st, rows, nrows, ld, count, d,
+                           out);
+    } else {
+        hipLaunchKernelGGL((mean_rows_kernel<2, 1>), dim3(grid_of(count)), dim3(256), 0, st, rows, nrows, ld, count, d,
                            out);
     }
     MX_LAUNCH_CHECK();
@@ -244,8 +375,8 @@ extern "C" int mx_mean_rows(const float* rows, int nrows, int64_t ld, int64_t co
 extern "C" int mx_allgather(void* comm_v, const float* send, int64_t count, float* gather, void* stream) {
     MX_CHECK(comm_v && count >= 0 && (count == 0 || (send && gather)), "mx_allgather: bad arguments");
     if (count == 0) return MX_OK;
-    MX_NCCL(ncclAllGather(send, gather, (size_t)count, ncclFloat32, reinterpret_cast<ncclComm_t>(comm_v),
-                          mx::as_stream(stream)));
+    ncclComm_t comm = reinterpret_cast<ncclComm_t>(comm_v);
+    MX_NCCL_ON(comm, ncclAllGather(send, gather, (size_t)count, ncclFloat32, comm, mx::as_stream(stream)));
     return MX_OK;
 }
 

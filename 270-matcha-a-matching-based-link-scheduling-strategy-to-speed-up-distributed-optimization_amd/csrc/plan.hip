@@ -20,7 +20,7 @@ constexpr int kMaxRemote = 156;                // the mixing kernels take at mos
 __global__ __launch_bounds__(256) void plan_kernel(const uint8_t* __restrict__ flags, int64_t T,
                                                    int M, const int32_t* __restrict__ partner,
                                                    int n, int row_base, int n_local, double alpha,
-                                                   int32_t* __restrict__ plan) {
+                                                   int32_t* __restrict__ plan, int32_t* __restrict__ any_overflow) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= T) return;
     const int64_t W = mx::plan_words(n_local, M);
@@ -63,6 +63,7 @@ __global__ __launch_bounds__(256) void plan_kernel(const uint8_t* __restrict__ f
     rec[1] = remote;
     rec[2] = 0;                                // idle rows skipped (mx_plan_set_idle)
     rec[3] = overflow;
+    if (overflow) atomicOr(any_overflow, 1);   // read back by mx_plan_build
     for (int r = 0; r < n_local; ++r) {
         const double s = 1.0 - (double)deg[r] * alpha;  // Python float arithmetic, then f32
         const float s32 = (float)s;
@@ -101,8 +102,25 @@ extern "C" int mx_plan_build(const uint8_t* flags_dev, int64_t T, int M, const i
              "mx_plan_build: local block [%d, %d) outside [0, %d)", row_base, row_base + n_local, n_global);
     if (T == 0) return MX_OK;
     const int64_t grid = (T + 255) / 256;
-    hipLaunchKernelGGL(plan_kernel, dim3((unsigned)grid), dim3(256), 0, mx::as_stream(stream),
-                       flags_dev, T, M, partner_dev, n_global, row_base, n_local, alpha, plan_dev);
-    MX_LAUNCH_CHECK();
+    hipStream_t st = mx::as_stream(stream);
+    int32_t* ovf = nullptr;                    // one word: did any iteration overflow kMaxRemote?
+    MX_HIP(hipMalloc(&ovf, sizeof(int32_t)));
+    int32_t host_ovf = 0;
+    hipError_t e = hipMemsetAsync(ovf, 0, sizeof(int32_t), st);
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(plan_kernel, dim3((unsigned)grid), dim3(256), 0, st, flags_dev, T, M, partner_dev,
+                           n_global, row_base, n_local, alpha, plan_dev, ovf);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = hipMemcpyAsync(&host_ovf, ovf, sizeof(int32_t), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipFree(ovf);
+    if (e != hipSuccess) {
+        mx::set_error("mx_plan_build: %s", hipGetErrorString(e));
+        return MX_ERR_HIP;
+    }
+    MX_CHECK(!host_ovf, "mx_plan_build: a round has more than %d distinct remote partners for the block "
+             "[%d, %d) -- more than any mixing kernel takes; spread the workers over more GPUs",
+             kMaxRemote, row_base, row_base + n_local);
     return MX_OK;
 }

@@ -93,13 +93,22 @@ def max_incoming_remote(partner, row_base, n_local):
 
 class RcclComm:
     """An RCCL communicator owned by the C library (one per process), bootstrapped through
-    torch.distributed (which must be initialised; any backend) for the unique-id broadcast."""
+    torch.distributed (which must be initialised; any backend) for the unique-id broadcast.
 
-    def __init__(self, group=None):
+    The communicator is non-blocking with a deadline (mx_rccl_init_timeout): if a peer never
+    joins -- the init, or any later exchange / all-reduce of the process -- the call raises
+    MXError ("timed out") after `timeout_s` (default $MX_RCCL_TIMEOUT_S or 300 s) instead of
+    hanging; abort() then releases the communicator."""
+
+    def __init__(self, group=None, timeout_s=None):
+        import os
         import torch.distributed as dist
         require_device()
         self.rank = dist.get_rank(group)
         self.nranks = dist.get_world_size(group)
+        if timeout_s is None:
+            timeout_s = float(os.environ.get("MX_RCCL_TIMEOUT_S") or 300.0)
+        self.timeout_s = float(timeout_s)
         uid = (ctypes.c_char * 128)()
         if self.rank == 0:
             check(lib.mx_rccl_unique_id(ctypes.cast(uid, ctypes.c_void_p)), "mx_rccl_unique_id")
@@ -107,14 +116,24 @@ class RcclComm:
         dist.broadcast_object_list(obj, src=0, group=group)
         buf = (ctypes.c_char * 128).from_buffer_copy(obj[0])
         h = ctypes.c_void_p()
-        check(lib.mx_rccl_init(ctypes.cast(buf, ctypes.c_void_p), self.nranks, self.rank,
-                               ctypes.byref(h)), "mx_rccl_init")
+        nb = ctypes.c_int(0)
+        check(lib.mx_rccl_init_timeout(ctypes.cast(buf, ctypes.c_void_p), self.nranks, self.rank,
+                                       int(self.timeout_s * 1000), ctypes.byref(h), ctypes.byref(nb)),
+              "mx_rccl_init_timeout")
         self.handle = h
+        self.nonblocking = bool(nb.value)
+
+    def abort(self):
+        """Release a communicator whose peers are gone (ncclCommAbort; after a timed-out call)."""
+        if self.handle:
+            lib.mx_rccl_abort(self.handle)
+            self.handle = None
 
     def close(self):
         if self.handle:
-            lib.mx_rccl_destroy(self.handle)
+            rc = lib.mx_rccl_destroy(self.handle)
             self.handle = None
+            check(rc, "mx_rccl_destroy")
 
 
 class PullTransport:

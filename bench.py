@@ -9,11 +9,23 @@ mixing + unflatten, fused: communicator.py:133-158).  Workload: full rounds (eve
 active -- the worst case, 2 * 8 * P * 4 bytes of HBM traffic per round on one GPU); inputs are
 synthetic (splitmix64 uniform[-1,1)) and resident in HBM before timing starts.  Rank 0 prints
 one JSON line.
+
+Parity: after the timed region every figure is checked against the CPU oracle (oracle/, the
+restatement pinned to the reference's own outputs) -- the oracle is the checker only, loaded
+after the measurements, never timed and never on the measured path.
+
+Secondary figures (MATCHA C_b = 0.5, all-reduce, ChocoSGD, host-resident models, the WRN-28-10 /
+CIFAR-ResNet configs, the ER(64) budget sweep) each run under a watchdog deadline
+(--figure-timeout) and a total budget (--figures-budget): a figure that hangs (e.g. a peer rank
+gone) makes rank 0 print the line measured so far with an "error" field and every rank exit,
+instead of losing the headline.
 """
 import argparse
 import json
 import os
+import random
 import sys
+import threading
 import time
 
 import numpy as np
@@ -25,6 +37,7 @@ PKG_NAME = "270-matcha-a-matching-based-link-scheduling-strategy-to-speed-up-dis
 
 HBM_PEAK = 8.0e12          # bytes/s, MI355X spec (MI355X_MICROARCH.md)
 XGMI_LINK_PEAK = 153e9     # bytes/s per direction per link
+METRIC = "gossip rounds/sec (8 workers x 25.6M fp32 params, graph 0, full MATCHA round)"
 
 
 def parse():
@@ -47,6 +60,14 @@ def parse():
                     "run for at least this long between the warmup and the timed region")
     ap.add_argument("--configs", type=int, default=1, help="also time the WRN-28-10 and CIFAR-ResNet configs' "
                     "rounds (BASELINE configs 2-3) on the same GPUs")
+    ap.add_argument("--wrn-params", type=int, default=36_546_980, help="config 3 row size (WRN-28-10)")
+    ap.add_argument("--resnet-params", type=int, default=181_668, help="config 2 row size (ResNet(18,100))")
+    ap.add_argument("--er", type=int, default=1, help="also run config 5: the ER(64, 0.1, 1234) MATCHA budget "
+                    "sweep 0.1 .. 1.0 (1e9 params per worker where memory allows)")
+    ap.add_argument("--er-params", type=float, default=1e9, help="config 5 row size (reduced to what fits, "
+                    "recorded in the line)")
+    ap.add_argument("--er-rounds", type=int, default=3, help="timed rounds per budget of the ER sweep")
+    ap.add_argument("--er-budgets", default="0.1,0.2,0.3,0.4,0.5,0.6,0.7,0.8,0.9,1.0")
     ap.add_argument("--staged", type=int, default=1, help="N = 1: also time host-resident models (the drop-in "
                     "communicators' staging path for CPU models)")
     ap.add_argument("--allreduce", type=int, default=1, help="also time all-reduce averaging (the paper's "
@@ -62,14 +83,124 @@ def parse():
     ap.add_argument("--placement", choices=("auto", "contiguous"), default="auto",
                     help="N > 1: which workers share a GPU -- auto (placement.best_placement, fewest rows "
                          "over the busiest xGMI pair) or contiguous id blocks")
+    ap.add_argument("--figure-timeout", type=float, default=300.0, help="watchdog deadline per secondary "
+                    "figure (s): past it rank 0 prints the line so far with an error and every rank exits")
+    ap.add_argument("--figures-budget", type=float, default=900.0, help="total wall time for the secondary "
+                    "figures (s); the ones left when it is spent are skipped")
+    ap.add_argument("--headline-timeout", type=float, default=900.0, help="watchdog deadline of the headline "
+                    "measurement (s)")
+    ap.add_argument("--pg-timeout", type=float, default=1800.0, help="torch.distributed timeout (s), above "
+                    "the watchdog's")
+    ap.add_argument("--debug-skip", default="", help="test hook FIGURE:RANK -- that rank skips that figure "
+                    "(its peers then wait in the figure's collectives: exercises the watchdog)")
     return ap.parse_args()
 
 
+# ----------------------------------------------------------------------------------- the checker
+def _oracle():
+    """The CPU oracle (oracle/oracle.py over liboracle.so) -- the checker.  Loaded only by the
+    parity checks and the CPU baseline, after the GPU measurements."""
+    p = os.path.join(ROOT, "oracle")
+    if p not in sys.path:
+        sys.path.insert(0, p)
+    import oracle as O
+    return O
+
+
+def synth_columns(workers, cols, seed0=1234):
+    """{worker: its synthetic row (mx_synth_fill(seed0 + worker)) at `cols`} from the oracle's
+    counter-based generator -- the columns before any round, without a device read."""
+    O = _oracle()
+    return {int(w): O.synth_at(seed0 + int(w), cols) for w in workers}
+
+
+def oracle_column_parity(topology, init, final, applied):
+    """Every worker's sampled columns after the rounds `applied` (iterations, in order) vs the
+    oracle's decenCommunicator round (communicator.py:92-122) run on the same columns from the
+    same initial values.  A gossip round mixes each column on its own, so the columns alone are
+    a complete check of those columns.  uint32 compare."""
+    O = _oracle()
+    n = int(topology.size)
+    flags = np.asarray(topology.active_flags, np.uint8)
+    partner = np.asarray(topology.neighbors_info, np.int32).reshape(-1, n)[:flags.shape[1]]
+    X = np.ascontiguousarray(np.stack([init[w] for w in range(n)]).astype(np.float32))
+    for it in applied:
+        if flags[it].any():
+            X = O.decen_round(X, partner, flags[it], topology.neighbor_weight)
+    got = np.stack([final[w] for w in range(n)])
+    return bool(np.array_equal(got.view(np.uint32), X.view(np.uint32)))
+
+
+# ----------------------------------------------------------------------------------- watchdog
+class Watchdog:
+    """Deadline on a phase of the run.  When the armed deadline passes (a collective whose peer
+    never arrives, a hang), rank 0 prints the line built so far with an "error" field and every
+    rank leaves with os._exit(0) -- an exit, never an exec; a zero status so the launcher does not
+    tear down rank 0 before it has printed."""
+
+    def __init__(self, rank, emit):
+        self.rank, self.emit = rank, emit
+        self.lock = threading.Lock()
+        self.name = self.deadline = self.seconds = None
+        t = threading.Thread(target=self._run, daemon=True)
+        t.start()
+
+    def arm(self, name, seconds):
+        with self.lock:
+            self.name, self.seconds, self.deadline = name, seconds, time.monotonic() + seconds
+
+    def disarm(self):
+        with self.lock:
+            self.deadline = None
+
+    def _run(self):
+        while True:
+            time.sleep(0.25)
+            with self.lock:
+                fire = self.deadline is not None and time.monotonic() > self.deadline
+                name, secs = self.name, self.seconds
+            if fire:
+                msg = (f"{name}: no progress within {secs:.0f} s on rank {self.rank} (a peer rank did not take "
+                       f"part or hung); the figures after it were not run")
+                sys.stderr.write(f"[bench watchdog] {msg}\n")
+                sys.stderr.flush()
+                if self.rank == 0:
+                    self.emit(msg)
+                os._exit(0)
+
+
+class Line:
+    """The one JSON line rank 0 prints (once: normally at the end, or by the watchdog)."""
+
+    def __init__(self, rank):
+        self.rank = rank
+        self.out = {"metric": METRIC, "value": None, "unit": "rounds/s"}
+        self.lock = threading.Lock()
+        self.printed = False
+
+    def emit(self, error=None):
+        with self.lock:
+            if self.printed or self.rank != 0:
+                return
+            out = dict(self.out)
+            if error:
+                out["error"] = error
+            try:
+                s = json.dumps(out)
+            except (TypeError, ValueError) as e:          # a figure mid-update: keep the headline
+                s = json.dumps({k: out[k] for k in out if isinstance(out[k], (int, float, str, type(None)))}
+                               | {"error": f"{error}; line not serialisable: {e}"})
+            print(s, flush=True)
+            self.printed = True
+
+
+# ----------------------------------------------------------------------------------- helpers
 def pickle_leg(partner, alpha, P, seconds):
     """The reference's per-rank sequence with its pickled transport (oracle/pickle_ranks.py): one
     process per worker pinned to its own core, torch.cat flatten, pickle.dumps -> pipe ->
     pickle.loads per active edge, add_(alpha), copy_ back -- what mpirun's 8 ranks spend per
     round (pickling dominates).  Full rounds; bounded by `seconds`."""
+    _oracle()
     import pickle_ranks as PR
     flags1 = np.ones((1, partner.shape[0]), np.uint8)
     one, cores, _ = PR.run(partner, flags1, alpha, P)
@@ -82,12 +213,11 @@ def pickle_leg(partner, alpha, P, seconds):
                       f"pinned per core (nproc {os.cpu_count()})"}
 
 
-def cpu_baseline(pkg, partner, alpha, n, P, seconds):
+def cpu_baseline(partner, alpha, n, P, seconds):
     """The oracle's port of the reference per-rank sequence (cat-flatten, sendrecv copy, add_
     FMA chain, copy_ back), one OpenMP thread per worker, on this box's host cores; beside it the
     same sequence with the reference's pickled transport, one process per worker."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O
+    O = _oracle()
     threads = min(n, os.cpu_count() or 1)
     rows = [[O.synth(1234 + i, P)] for i in range(n)]
     flags = np.ones((1, partner.shape[0]), np.uint8)
@@ -127,8 +257,8 @@ def pmc_traffic(kernel_prefix="mix_kernel"):
 
 
 def guarded(name, fn):
-    """A secondary figure (after the timed region): an exception is reported in the line as
-    {"error": ...} instead of losing the headline line; traceback to stderr."""
+    """A secondary figure: an exception is reported in the line as {"error": ...} instead of
+    losing the headline line; traceback to stderr."""
     try:
         return fn()
     except Exception as e:                       # noqa: BLE001 -- reported, not swallowed
@@ -144,6 +274,24 @@ def max_over_ranks(x, world, dev):
     t = torch.tensor([x], device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+
+
+def timed_loop(fn, first, K, world, dev):
+    """K calls fn(first + j) between synchronize + barrier on both sides; seconds, max over ranks."""
+    torch.cuda.synchronize()
+    barrier(world)
+    t = time.perf_counter()
+    for j in range(K):
+        fn(first + j)
+    torch.cuda.synchronize()
+    barrier(world)
+    return max_over_ranks(time.perf_counter() - t, world, dev)
 
 
 def exchange_only(group, first, K, world, dev):
@@ -189,20 +337,46 @@ def gather_columns(g, cols_dev, world, dev):
     return out
 
 
-def replay_parity(pkg, GP, n, init, final, applied):
-    """The rounds one group went through (its iteration list, in order), recomputed on ONE GPU
-    by a single-process VirtualWorkerGroup over just the sampled columns (a gossip round mixes
-    each column on its own), compared bit for bit with what the timed group holds."""
-    P = init[0].shape[0]
-    ref = pkg.VirtualWorkerGroup(GP, numel=P)
-    ref.rows.copy_(torch.from_numpy(np.stack([init[w] for w in range(n)])))
-    for it in applied:
-        ref.step(it)
-    got = ref.rows.cpu().numpy()
-    want = np.stack([final[w] for w in range(n)])
-    ok = bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
-    del ref
-    return ok
+def fill_synth(pkg, g, seed0=1234):
+    for r in range(g.n_local):
+        pkg._lib.check(pkg.lib.mx_synth_fill(g.rows[r].data_ptr(), g.numel, seed0 + g.workers[r], None))
+
+
+def round_bytes(partner, owner, flags_rows, rank, row_base, n_local, P):
+    """Per round: (this GPU's algorithmic HBM bytes of the mixing kernel, busiest directed link
+    bytes, busiest GPU pair both directions, all link bytes).  HBM: every local row with degree > 0
+    read and written once, every received slab row read once; links: a row crosses to a GPU at
+    most once per round (mx_exchange_plan)."""
+    n = partner.shape[1]
+    hbm, link, pair_b, total = [], [], [], []
+    for f in flags_rows:
+        deg = np.zeros(n, int)
+        for g in range(len(f)):
+            if f[g]:
+                deg += partner[g] >= 0
+        act = sum(1 for i in range(row_base, row_base + n_local) if deg[i] > 0)
+        moved = set()
+        for g in range(len(f)):
+            if not f[g]:
+                continue
+            for p in range(n):
+                q = partner[g, p]
+                if q >= 0 and owner[p] != owner[q]:
+                    moved.add((p, int(owner[q])))
+        links = {}
+        for p, b in moved:
+            a = int(owner[p])
+            links[(a, b)] = links.get((a, b), 0) + P * 4
+        remote = sum(1 for p, b in moved if b == rank)
+        hbm.append(2 * act * P * 4 + remote * P * 4)
+        link.append(max(links.values()) if links else 0)
+        total.append(sum(links.values()))
+        pr = {}
+        for (a, b), v in links.items():
+            k = (min(a, b), max(a, b))
+            pr[k] = pr.get(k, 0) + v
+        pair_b.append(max(pr.values()) if pr else 0)
+    return hbm, link, pair_b, total
 
 
 def p2p_probe(rank, world, nbytes, dev, reps=5):
@@ -238,6 +412,31 @@ def p2p_probe(rank, world, nbytes, dev, reps=5):
     return res
 
 
+# ----------------------------------------------------------------------------------- figures
+def matcha_figure(pkg, args, rank, world, n, P, K, W, comm, dev):
+    """The headline shape under a MATCHA C_b = 0.5 schedule (random matching subsets per round);
+    oracle column parity over every round run."""
+    np.random.seed(1234)
+    GPm = pkg.MatchaProcessor(pkg.select_graph(args.graph), 0.5, rank, n, W + K, True)
+    gm = pkg.VirtualWorkerGroup(GPm, numel=P, rank=rank, nranks=world, comm=comm, placement=args.placement)
+    fill_synth(pkg, gm)
+    for it in range(W):
+        gm.step(it)
+    el = timed_loop(gm.step, W, K, world, dev)
+    fl = np.asarray(GPm.active_flags[W:W + K])
+    cols = sample_columns(P)
+    final = gather_columns(gm, torch.from_numpy(cols).cuda(), world, dev)
+    gm.close()
+    del gm
+    torch.cuda.empty_cache()
+    out = {"budget": 0.5, "rounds_per_s": K / el, "probabilities": [round(float(x), 6) for x in GPm.probabilities],
+           "alpha": GPm.neighbor_weight, "mean_active_matchings": float(fl.sum(1).mean()),
+           "skipped_rounds": int((fl.sum(1) == 0).sum())}
+    if rank == 0:
+        out["parity_ok"] = oracle_column_parity(GPm, synth_columns(range(n), cols), final, range(W + K))
+    return out
+
+
 def allreduce_figure(group, n, world, dev, K, W):
     """Context figure: the all-reduce averaging the paper compares gossip against
     (centralizedCommunicator, communicator.py:46-76 / sync_allreduce): every worker's row becomes
@@ -246,7 +445,7 @@ def allreduce_figure(group, n, world, dev, K, W):
     import torch.distributed as dist
     rows = group.rows
 
-    def one():
+    def one(_):
         acc = rows.sum(0)
         if world > 1:
             if dev == "cpu":                     # gloo test transport: host staging
@@ -257,47 +456,70 @@ def allreduce_figure(group, n, world, dev, K, W):
                 dist.all_reduce(acc)
         rows.copy_((acc / n).expand_as(rows))
 
-    for _ in range(W):
-        one()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t = time.perf_counter()
-    for _ in range(K):
-        one()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = max_over_ranks(time.perf_counter() - t, world, dev)
+    for j in range(W):
+        one(j)
+    el = timed_loop(one, 0, K, world, dev)
     return {"rounds_per_s": K / el, "ms_per_round": 1e3 * el / K,
             "how": "row sum + torch.distributed all_reduce (RCCL at N > 1) + / n + copy back; torch ops"}
 
 
-def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99, gamma=0.1, placement=None):
-    """Secondary figure: ChocoSGD rounds (BASELINE config: VGG-16 size, top-1 %, graph 0, every
-    matching active) on the same GPUs -- top-k compress + [N > 1] message exchange + fused apply.
-    At N > 1 every worker's final row is gathered to rank 0 and compared bit for bit with the
-    same rounds recomputed by one single-GPU ChocoWorkerGroup (parity_ok)."""
+def _choco_state(grp):
+    P = grp.numel
+    return {int(w): (grp.x[i, :P].cpu().numpy(), grp.x_hat[i, :P].cpu().numpy(), grp.s[i, :P].cpu().numpy())
+            for i, w in enumerate(grp.workers)}
+
+
+def choco_oracle_round(pkg, grp, GP, it, ratio, gamma, rank, world):
+    """One more Choco round (iteration `it`, untimed) checked against the oracle's
+    ChocoCommunicator round (communicator.py:175-268, compressors.py:3-19) from the same state:
+    x, x_hat and s of every worker gathered before and after, uint32 compare on rank 0."""
     import torch.distributed as dist
+    before = _choco_state(grp)
+    grp.step(it)
+    torch.cuda.synchronize()
+    after = _choco_state(grp)
+    if world > 1:
+        objs = [None] * world if rank == 0 else None
+        dist.gather_object((before, after), objs, dst=0)
+        if rank == 0:
+            before, after = {}, {}
+            for b, a in objs:
+                before.update(b)
+                after.update(a)
+    if rank != 0:
+        return None
+    O = _oracle()
+    n = int(GP.size)
+    X = np.ascontiguousarray(np.stack([before[w][0] for w in range(n)]))
+    XH = np.ascontiguousarray(np.stack([before[w][1] for w in range(n)]))
+    S = np.ascontiguousarray(np.stack([before[w][2] for w in range(n)]))
+    flags = np.asarray(GP.active_flags, np.uint8)
+    partner = np.asarray(GP.neighbors_info, np.int32).reshape(-1, n)[:flags.shape[1]]
+    if flags[it].any():
+        O.choco_round(X, XH, S, partner, flags[it], GP.neighbor_weight, grp.k, gamma)
+    ok = True
+    for w in range(n):
+        for a, b in zip(after[w], (X[w], XH[w], S[w])):
+            ok &= bool(np.array_equal(a.view(np.uint32), b.view(np.uint32)))
+    return ok
+
+
+def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99, gamma=0.1, placement=None):
+    """Secondary figure: ChocoSGD rounds (BASELINE config 4: VGG-16 size, top-1 %, graph 0, every
+    matching active) on the same GPUs -- top-k compress + [N > 1] message exchange + fused apply.
+    Parity: one more round after the timed ones, x / x_hat / s of every worker vs the oracle's
+    round from the same state (choco_oracle_round)."""
     grp = pkg.ChocoWorkerGroup(GP, numel=P, ratio=ratio, consensus_lr=gamma, rank=rank, nranks=world,
                                comm=comm, placement=placement)
-    for r in range(grp.n_local):
-        pkg._lib.check(pkg.lib.mx_synth_fill(grp.rows[r].data_ptr(), P, 1234 + grp.workers[r], None))
+    fill_synth(pkg, grp)
     for it in range(W):
         grp.step(it)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t = time.perf_counter()
-    for j in range(K):
-        grp.step(W + j)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = max_over_ranks(time.perf_counter() - t, world, dev)
+    el = timed_loop(grp.step, W, K, world, dev)
     out = {"config": f"P={P} (VGG-16 size by default), ratio {ratio} (k={grp.k}), gamma {gamma}, graph 0 full rounds",
-           "rounds_per_s": K / el, "ms_per_round": 1e3 * el / K, "rows_per_gpu": grp.n_local, "rounds": K,
-           "parity_ok": None}
+           "rounds_per_s": K / el, "ms_per_round": 1e3 * el / K, "rows_per_gpu": grp.n_local, "rounds": K}
+    out["parity_ok"] = choco_oracle_round(pkg, grp, GP, W + K, ratio, gamma, rank, world)
+    out["parity"] = (f"round {W + K} (after the {W} warmup + {K} timed rounds) of every worker: x, x_hat, s vs the "
+                     f"oracle's Choco round from the same state, uint32")
     if world == 1:
         # SURVEY.md §8(d): ~6 P 4 B per worker (top-k reads x, x_hat; apply reads x, s, x_hat, writes x)
         alg = 24 * P * grp.n_local
@@ -305,32 +527,10 @@ def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99
                            "frac_of_8TBps": alg / (el / K) / HBM_PEAK,
                            "note": "algorithmic bytes; the passes also move the dirty 64-B granules of s / x_hat "
                                    "and the candidate / message bytes (~3.2 GB per 8-row round by PMC, r02)"}
-        del grp
-        torch.cuda.empty_cache()
+    del grp
+    torch.cuda.empty_cache()
+    if world == 1:
         out["one_row_share_n8"] = choco_row_share(pkg, GP, P, ratio, gamma, K, W)
-    if world > 1:
-        mine = (list(grp.workers), grp.rows.cpu().numpy())
-        objs = [None] * world if rank == 0 else None
-        dist.gather_object(mine, objs, dst=0)
-        if rank == 0:
-            n = int(GP.size) if hasattr(GP, "size") else len(GP.neighbors_info[0])
-            ref = pkg.ChocoWorkerGroup(GP, numel=P, ratio=ratio, consensus_lr=gamma)
-            for r in range(n):
-                pkg._lib.check(pkg.lib.mx_synth_fill(ref.rows[r].data_ptr(), P, 1234 + r, None))
-            for it in range(W + K):
-                ref.step(it)
-            want = ref.rows.cpu().numpy()
-            ok = True
-            for ws, blk in objs:
-                for i, w in enumerate(ws):
-                    ok &= bool(np.array_equal(blk[i].view(np.uint32), want[w].view(np.uint32)))
-            out["parity_ok"] = ok
-            out["parity"] = "every worker's row vs a 1-GPU recompute of the same rounds, uint32"
-            del ref
-        dist.barrier()
-    if world > 1:
-        del grp
-        torch.cuda.empty_cache()
     return out
 
 
@@ -375,32 +575,23 @@ def choco_row_share(pkg, GP, P, ratio, gamma, K, W):
     return out
 
 
-def config_figures(pkg, rank, world, n, K, W, comm, dev, placement):
+def config_figures(pkg, args, rank, world, n, K, W, comm, dev):
     """Secondary figures: the other BASELINE configs' gossip rounds on the same GPUs -- WRN-28-10
     (36,546,980 params per worker) under MATCHA C_b = 0.5 and full rounds, and the repo's CIFAR
-    ResNet (181,668 params, launch-bound) under MATCHA C_b = 0.5; rounds/s and, at N = 1, HBM
-    bytes / s over the algorithmic bytes of the rounds run."""
-    import torch.distributed as dist
+    ResNet (181,668 params, launch-bound) under MATCHA C_b = 0.5; rounds/s, at N = 1 HBM bytes / s
+    over the algorithmic bytes of the rounds run, and oracle parity of every worker's 64 sampled
+    columns over every round the group ran (eager and graph-replayed)."""
     out = {}
-    for name, P, budget in (("wrn28_10_matcha0.5", 36_546_980, 0.5), ("wrn28_10_full", 36_546_980, 1.0),
-                            ("resnet18_100_matcha0.5", 181_668, 0.5)):
+    for name, P, budget in (("wrn28_10_matcha0.5", args.wrn_params, 0.5), ("wrn28_10_full", args.wrn_params, 1.0),
+                            ("resnet18_100_matcha0.5", args.resnet_params, 0.5)):
         np.random.seed(1234)
         GPc = pkg.MatchaProcessor(pkg.select_graph(0), budget, rank, n, W + K, True)
-        g = pkg.VirtualWorkerGroup(GPc, numel=P, rank=rank, nranks=world, comm=comm, placement=placement)
-        for r in range(g.n_local):
-            pkg._lib.check(pkg.lib.mx_synth_fill(g.rows[r].data_ptr(), P, 1234 + g.workers[r], None))
+        g = pkg.VirtualWorkerGroup(GPc, numel=P, rank=rank, nranks=world, comm=comm, placement=args.placement)
+        fill_synth(pkg, g)
+        applied = list(range(W + K))
         for it in range(W):
             g.step(it)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t = time.perf_counter()
-        for j in range(K):
-            g.step(W + j)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        el = max_over_ranks(time.perf_counter() - t, world, dev)
+        el = timed_loop(g.step, W, K, world, dev)
         partner = np.asarray(GPc.neighbors_info, np.int32)
         byts = 0
         for f in np.asarray(GPc.active_flags[W:W + K], np.uint8):
@@ -426,12 +617,141 @@ def config_figures(pkg, rank, world, n, K, W, comm, dev, placement):
             gr.replay()
             torch.cuda.synchronize()
             elg = time.perf_counter() - t
+            applied += list(range(W, W + K)) * 2
             out[name]["graph_rounds_per_s"] = K / elg
             out[name]["graph_note"] = f"{K} rounds (iterations {W}..{W + K - 1}) replayed from one HIP graph"
             del gr
+        cols = sample_columns(P)
+        final = gather_columns(g, torch.from_numpy(cols).cuda(), world, dev)
         g.close()
         del g
         torch.cuda.empty_cache()
+        if rank == 0:
+            out[name]["parity_ok"] = oracle_column_parity(GPc, synth_columns(range(n), cols), final, applied)
+    if rank == 0:
+        out["parity"] = ("every worker's 64 sampled columns after every round the group ran vs the oracle's "
+                         "decen rounds on the same columns, uint32")
+    return out
+
+
+def er_figure(pkg, args, rank, world, comm, dev):
+    """BASELINE config 5: a 64-worker Erdos-Renyi(0.1, seed 1234) topology decomposed on the host,
+    P params per worker (1e9 by default, reduced to what fits this GPU -- the P run is recorded),
+    MATCHA budget sweep.  At N > 1 the workers are placed over the GPUs ("auto") and every exchange
+    form that fits at that P (plain / column-pipelined RCCL, pull) is calibrated ONE AT A TIME at
+    budget 1.0 (only one form's buffers are alive at once); the fastest runs the sweep.  Per
+    budget: rounds/s (max over ranks), per-rank slot count, busiest-link bytes per round, the
+    exchange alone (RCCL forms), and oracle parity of every worker's 64 sampled columns."""
+    from importlib import import_module
+    E = import_module(PKG_NAME + ".engine")
+    PL = import_module(PKG_NAME + ".placement")
+    n, seed = 64, 1234
+    budgets = [float(b) for b in args.er_budgets.split(",") if b]
+    Ker, Wer, R = max(1, args.er_rounds), 1, 1
+    T = Wer + Ker + 2 * R + 2
+    random.seed(0)
+    base = pkg.erdos_renyi(n, 0.1, seed)
+    np.random.seed(seed)
+    GP0 = pkg.MatchaProcessor(base, 1.0, rank, n, T, False)
+    sub = GP0.subGraphs
+    topo0, perm = PL.place(GP0, world, args.placement if world > 1 else None)
+    row_base, n_local = E.partition(n, world)[rank]
+    part0 = np.asarray(topo0.neighbors_info, np.int32).reshape(-1, n)
+    max_remote = E.max_incoming_remote(part0, row_base, n_local)
+    # bytes per parameter column on this GPU for each exchange form
+    forms = {"local": n_local} if world == 1 else {}
+    if world > 1:
+        forms["rccl"] = n_local + max_remote
+        forms["rccl_chunked"] = n_local + 2 * max_remote / 4.0 if max_remote else n_local
+        if args.pull != "off":
+            forms["pull"] = 3 * n_local
+    torch.cuda.empty_cache()
+    free, total = torch.cuda.mem_get_info()
+    reserve = 4 << 30
+    P_req = int(args.er_params)
+    fit = {k: int((free - reserve) / (4 * v)) // 64 * 64 for k, v in forms.items()}
+    P = min(P_req, max(fit.values()))
+    P = int(-max_over_ranks(-float(P), world, dev))            # every rank runs the same P
+    if P < 1024:
+        raise RuntimeError(f"ER(64) leg: only {free / 2**30:.1f} GiB free on rank {rank}")
+    cand = [k for k in forms if fit[k] >= P]
+    cols = sample_columns(P)
+    cols_dev = torch.from_numpy(cols).cuda()
+    init = synth_columns(range(n), cols)
+
+    def make(GPb, form):
+        kw = dict(numel=P, rank=rank, nranks=world, placement=perm if world > 1 else None)
+        if form == "rccl":
+            g = pkg.VirtualWorkerGroup(GPb, comm=comm, **kw)
+        elif form == "rccl_chunked":
+            g = pkg.VirtualWorkerGroup(GPb, comm=comm, chunk_cols=((P + 3) // 4 + 63) // 64 * 64, **kw)
+        elif form == "pull":
+            g = pkg.VirtualWorkerGroup(GPb, comm=pkg.PullTransport(), **kw)
+        else:
+            g = pkg.VirtualWorkerGroup(GPb, **kw)
+        fill_synth(pkg, g)
+        return g
+
+    calib = {}
+    chosen = cand[0]
+    if len(cand) > 1:
+        for form in cand:                         # one form alive at a time
+            try:
+                g = make(GP0, form)
+            except pkg.MXError as e:
+                calib[form] = f"unavailable: {e}"
+                continue
+            g.step(0)
+            calib[form] = 1e3 * timed_loop(g.step, 1, R, world, dev) / R
+            g.close()
+            del g
+            torch.cuda.empty_cache()
+        timed = {k: v for k, v in calib.items() if isinstance(v, float)}
+        chosen = min(timed, key=timed.get)
+    sweep = []
+    for b in budgets:
+        np.random.seed(seed)
+        GPb = pkg.MatchaProcessor(sub, b, rank, n, T, True)       # same matchings, budget b
+        g = make(GPb, chosen)
+        applied = list(range(Wer))
+        for it in range(Wer):
+            g.step(it)
+        el = timed_loop(g.step, Wer, Ker, world, dev)
+        applied += list(range(Wer, Wer + Ker))
+        flags = np.asarray(GPb.active_flags, np.uint8)[Wer:Wer + Ker]
+        eng = g.engine
+        hbm, link, _, _ = round_bytes(eng.partner, eng.owner, flags, rank, g.row_base, g.n_local, P)
+        xo = None
+        if world > 1 and chosen == "rccl" and flags.any():        # whole rows into the slab: plain form only
+            xo = exchange_only(g, Wer, Ker, world, dev)[0]
+        slots = [None] * world
+        if world > 1:
+            import torch.distributed as dist
+            dist.all_gather_object(slots, int(eng.n_slots))
+        else:
+            slots = [int(eng.n_slots)]
+        final = gather_columns(g, cols_dev, world, dev)
+        g.close()
+        del g
+        torch.cuda.empty_cache()
+        row = {"budget": b, "rounds_per_s": Ker / el, "ms_per_round": 1e3 * el / Ker,
+               "mean_active_matchings": float(flags.sum(1).mean()), "skipped_rounds": int((flags.sum(1) == 0).sum()),
+               "alpha": GPb.neighbor_weight, "slots_per_rank": slots,
+               "hbm_TBps_rank0": (float(np.sum(hbm)) / el / 1e12) if world == 1 else None,
+               "max_link_bytes_per_round": float(np.mean(link)) if world > 1 else None,
+               "busiest_link_GBps": (float(np.mean(link)) / (el / Ker) / 1e9) if world > 1 else None,
+               "exchange_only_ms": 1e3 * xo if xo else None}
+        if rank == 0:
+            row["parity_ok"] = oracle_column_parity(GPb, init, final, applied)
+        sweep.append(row)
+    out = {"graph": f"ER({n}, 0.1, seed {seed})", "matchings": len(sub), "edges": int(sum(len(m) for m in sub)),
+           "params_per_worker": P, "params_requested": P_req, "rows_per_gpu": n_local,
+           "max_remote_partners_rank0": max_remote, "form": chosen, "calib_ms": calib or None,
+           "rounds_per_budget": Ker, "sweep": sweep}
+    if rank == 0:
+        out["parity_ok"] = all(r.get("parity_ok") for r in sweep)
+        out["parity"] = ("every worker's 64 sampled columns after every round of each budget vs the oracle's "
+                         "decen rounds on the same columns (initial values from the oracle's generator), uint32")
     return out
 
 
@@ -484,6 +804,7 @@ def timed_rounds(run, group, first, K):
     return ev
 
 
+# ----------------------------------------------------------------------------------- main
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -491,15 +812,21 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    line = Line(rank)
+    wd = Watchdog(rank, line.emit)
+    wd.arm("startup (process group / RCCL communicator)", args.headline_timeout)
+    import datetime
     import torch.distributed as dist
     gloo = args.transport == "gloo"
     if gloo:
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
+    pg_timeout = datetime.timedelta(seconds=args.pg_timeout)
     if world > 1 and gloo:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=pg_timeout)
     elif world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local),
+                                timeout=pg_timeout)
     dev = "cpu" if gloo else "cuda"
     import importlib
     pkg = importlib.import_module(PKG_NAME)
@@ -510,7 +837,8 @@ def main():
             from gloo_transport import GlooTransport
             comm = GlooTransport(pkg)
         else:
-            comm = pkg.engine.default_comm()
+            comm = pkg.engine.RcclComm(timeout_s=min(args.figure_timeout, args.headline_timeout) * 0.8)
+    wd.arm("headline", args.headline_timeout)
 
     n, P = args.workers, args.params
     K, W = args.steps, args.warmup
@@ -520,11 +848,10 @@ def main():
     GP = pkg.MatchaProcessor(pkg.select_graph(args.graph), args.budget, rank, n,
                              W + DMAX + 2 * K + (R + 1 if world > 1 else 0), True)
     group = pkg.VirtualWorkerGroup(GP, numel=P, rank=rank, nranks=world, comm=comm, placement=args.placement)
-    for r in range(group.n_local):
-        pkg._lib.check(pkg.lib.mx_synth_fill(group.rows[r].data_ptr(), P, 1234 + group.workers[r], None))
+    fill_synth(pkg, group)
     torch.cuda.synchronize()
-    cols = torch.from_numpy(sample_columns(P)).cuda()
-    init_cols = gather_columns(group, cols, world, dev)      # self-check: the columns before any round
+    cols = sample_columns(P)
+    cols_dev = torch.from_numpy(cols).cuda()
     applied = {}                                             # group -> iterations it ran, in order
 
     def run(g, it):
@@ -538,14 +865,14 @@ def main():
     any_remote = world > 1 and max_over_ranks(float(group.engine.max_remote), world, dev) > 0   # collective
     base_it = W + DMAX + 2 * K
     forms = {"rccl": group}
+    C = None
     if any_remote and args.overlap != "off":
         # column pipelining: chunk c+1 of every exchanged row travels on a side stream while chunk c
         # is mixed (bit-identical results)
         C = args.chunk_cols or ((P + 3) // 4 + 63) // 64 * 64
         gchunk = pkg.VirtualWorkerGroup(GP, numel=P, rank=rank, nranks=world, comm=comm, placement=args.placement,
                                         chunk_cols=C)
-        for r in range(gchunk.n_local):
-            pkg._lib.check(pkg.lib.mx_synth_fill(gchunk.rows[r].data_ptr(), P, 1234 + gchunk.workers[r], None))
+        fill_synth(pkg, gchunk)
         for it in range(W):
             run(gchunk, it)
         run(gchunk, base_it)                     # first chunked round (side stream, events) untimed
@@ -557,8 +884,7 @@ def main():
         try:
             gpull = pkg.VirtualWorkerGroup(GP, numel=P, rank=rank, nranks=world, comm=pkg.PullTransport(),
                                            placement=args.placement)
-            for r in range(gpull.n_local):
-                pkg._lib.check(pkg.lib.mx_synth_fill(gpull.rows[r].data_ptr(), P, 1234 + gpull.workers[r], None))
+            fill_synth(pkg, gpull)
             for it in range(W):
                 run(gpull, it)
             forms["pull"] = gpull
@@ -567,17 +893,8 @@ def main():
     if len(forms) > 1:
         # every form runs R untimed rounds; the fastest (max over ranks, so every rank picks the
         # same) is the one timed -- unless one is forced (--overlap on / --pull on)
-        def calib(g, first):
-            torch.cuda.synchronize()
-            dist.barrier()
-            t = time.perf_counter()
-            for j in range(R):
-                run(g, first + j)
-            torch.cuda.synchronize()
-            dist.barrier()
-            return max_over_ranks((time.perf_counter() - t) / R, world, dev)
-
-        calib_ms = {name: 1e3 * calib(g, base_it + 1) for name, g in forms.items()}
+        calib_ms = {name: 1e3 * timed_loop(lambda it, g=g: run(g, it), base_it + 1, R, world, dev) / R
+                    for name, g in forms.items()}
         if args.pull == "on" and "pull" in forms:
             chosen = "pull"
         elif args.overlap == "on" and "rccl_chunked" in forms:
@@ -616,23 +933,18 @@ def main():
             break
     diag_rounds = it - W
     step_ms = np.array(step_ms)
-    if world > 1:
-        dist.barrier()
+    barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for j in range(K):                           # the timed rounds: back to back, nothing else
         run(timed, it + j)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    barrier(world)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     elapsed = max_over_ranks(elapsed, world, dev)
     timed_first = it
-    # self-check: every worker's sampled columns vs the same rounds recomputed on one GPU
-    final_cols = gather_columns(timed, cols, world, dev)
-    parity_ok = (replay_parity(pkg, GP, n, init_cols, final_cols, applied[id(timed)])
-                 if rank == 0 else None)
+    final_cols = gather_columns(timed, cols_dev, world, dev)
     # mixing kernel alone (N > 1: without the RCCL exchange, so rows go stale) -> its HBM roofline
     stream = torch.cuda.current_stream()
     mev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
@@ -658,183 +970,162 @@ def main():
         torch.cuda.synchronize()
         ref_copy_ms = float(np.mean([a.elapsed_time(b) for a, b in cev]))
         del src_t, dst_t
-    # secondary figure: a MATCHA C_b = 0.5 schedule on the same workers (random subsets per round)
-    matcha = None
-    if args.budget >= 1.0:
-        np.random.seed(1234)
-        GPm = pkg.MatchaProcessor(pkg.select_graph(args.graph), 0.5, rank, n, W + K, True)
-        gm = pkg.VirtualWorkerGroup(GPm, numel=P, rank=rank, nranks=world, comm=comm, placement=args.placement)
-        for r in range(gm.n_local):
-            pkg._lib.check(pkg.lib.mx_synth_fill(gm.rows[r].data_ptr(), P, 1234 + gm.workers[r], None))
-        for it in range(W):
-            gm.step(it)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        t1 = time.perf_counter()
-        for j in range(K):
-            gm.step(W + j)
-        torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
-        el = max_over_ranks(time.perf_counter() - t1, world, dev)
-        fl = np.asarray(GPm.active_flags[W:W + K])
-        matcha = {"budget": 0.5, "rounds_per_s": K / el, "probabilities": [round(float(x), 6) for x in GPm.probabilities],
-                  "alpha": GPm.neighbor_weight, "mean_active_matchings": float(fl.sum(1).mean()),
-                  "skipped_rounds": int((fl.sum(1) == 0).sum())}
-        del gm
-
-    allreduce = (guarded("allreduce", lambda: allreduce_figure(group, n, world, dev, max(5, K // 5), 2))
-                 if args.allreduce else None)
-
-    choco = (guarded("choco", lambda: choco_figure(pkg, GP, rank, world, max(20, K), 3, comm, dev,
-                                                    P=args.choco_params, placement=args.placement))
-             if args.choco else None)
-    staged = guarded("staged", lambda: staged_figure(pkg, GP, n, P, 3, W)) if (world == 1 and args.staged) else None
-    configs = (guarded("configs", lambda: config_figures(pkg, rank, world, n, max(10, K), 3, comm, dev,
-                                                          args.placement))
-               if args.configs and P == 25_600_000 else None)
-
     flags = np.asarray(GP.active_flags[timed_first:timed_first + K], np.uint8)
-    # algorithmic HBM bytes of the mixing kernel on this GPU: every local row with degree > 0 read
-    # and written once, every received slab row read once (positions of the engine's table: with a
-    # placement, worker group.workers[i] sits at position row_base + i)
     eng = group.engine
     partner = eng.partner
-    hbm_bytes = []
-    link_bytes = []
-    pair_bytes = []
-    total_bytes = []
-    for f in flags:
-        deg = np.zeros(n, int)
-        for g in range(len(f)):
-            if f[g]:
-                deg += partner[g] >= 0
-        act = sum(1 for i in range(group.row_base, group.row_base + group.n_local) if deg[i] > 0)
-        moved = set()                  # (worker, destination GPU): each row crosses a link once
-        for g in range(len(f)):
-            if not f[g]:
-                continue
-            for p in range(n):
-                q = partner[g, p]
-                if q >= 0 and eng.owner[p] != eng.owner[q]:
-                    moved.add((p, int(eng.owner[q])))
-        links = {}
-        for p, b in moved:
-            a = int(eng.owner[p])
-            links[(a, b)] = links.get((a, b), 0) + P * 4     # p's row travels a -> b
-        remote = sum(1 for p, b in moved if b == rank)
-        hbm_bytes.append(2 * act * P * 4 + remote * P * 4)
-        link_bytes.append(max(links.values()) if links else 0)
-        total_bytes.append(sum(links.values()))
-        pair = {}
-        for (a, b), v in links.items():
-            key = (min(a, b), max(a, b))
-            pair[key] = pair.get(key, 0) + v
-        pair_bytes.append(max(pair.values()) if pair else 0)
+    hbm_bytes, link_bytes, pair_bytes, total_bytes = round_bytes(partner, eng.owner, flags, rank, group.row_base,
+                                                                 group.n_local, P)
     avg_ms = float(step_ms.mean())
-    exch_s = exch_per = probe = None
-    if world > 1:             # (with --transport gloo: the same code over host staging, tests only)
-        xo = guarded("exchange_only", lambda: exchange_only(group, timed_first, K, world, dev))
-        exch_s, exch_per = xo if isinstance(xo, tuple) else (None, None)
-        probe = guarded("p2p_probe", lambda: p2p_probe(rank, world, P * 4, dev))
-        if "error" in probe:
-            probe = None
     mix_avg_ms = float(mix_ms.mean())
     mix_bytes = float(np.mean(hbm_bytes))
     achieved = mix_bytes / (mix_avg_ms * 1e-3)
     traffic, traffic_src = pmc_traffic()
-
-    if rank == 0:
-        out = {
-            "metric": "gossip rounds/sec (8 workers x 25.6M fp32 params, graph 0, full MATCHA round)",
-            "value": K / elapsed,
-            "unit": "rounds/s",
-            "n_gpus": world,
-            "steps": K,
-            "warmup": W,
-            "ms_per_step": 1e3 * elapsed / K,
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic (splitmix64 uniform[-1,1), resident in HBM)",
-            "config": {"workload": f"graph {args.graph} ({n} workers), P={P} fp32 per worker, "
-                                   f"budget {args.budget} ({'every matching active' if args.budget >= 1 else 'MATCHA schedule'})",
-                       "workers": n, "params_per_worker": P, "graph": args.graph, "budget": args.budget,
-                       "parallelism": f"{n} workers over {world} GPU(s)" +
-                                      (f", placement {args.placement}" if world > 1 else "") +
-                                      (f", exchange form {overlap['chosen_form']}" if overlap and
-                                       overlap.get("chosen_form") else ""),
-                       "placement": group.placement if world > 1 else None,
-                       "transport": args.transport if world > 1 else None},
-            "parity_ok": parity_ok,
-            "parity": (f"every worker's {len(sample_columns(P))} sampled columns after all "
-                       f"{len(applied[id(timed)])} rounds this run applied, vs the same rounds recomputed on one "
-                       f"GPU by a single-process VirtualWorkerGroup (uint32 compare)"),
-            "round_us": {"events_min": 1e3 * float(step_ms.min()), "events_median": 1e3 * float(np.median(step_ms)),
-                         "events_mean": 1e3 * avg_ms, "events_last_block_mean": 1e3 * float(step_ms[-K:].mean()),
-                         "events_first_block_mean": 1e3 * float(step_ms[:K].mean()),
-                         "diag_rounds": int(diag_rounds), "timed_mean": 1e6 * elapsed / K,
-                         "note": f"per-round HIP events of {diag_rounds} untimed rounds (blocks of K, >= "
-                                 f"{args.settle_ms} ms) run between the warmup and the timed region (rank 0)"},
-            "roofline": {"bound": "hbm", "kernel": f"{pkg.engine.mix_kernel_name(eng.n_slots)} (mx_gossip_mix)",
-                         "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK, "traffic": traffic,
-                         "traffic_source": traffic_src, "bytes_per_launch": mix_bytes,
-                         "avg_launch_ms": mix_avg_ms, "min_launch_ms": float(mix_ms.min()),
-                         "median_launch_ms": float(np.median(mix_ms)),
-                         "frac_timed_region": (mix_bytes / (elapsed / K)) / HBM_PEAK if world == 1 else None,
-                         "same_box_torch_copy_ms": ref_copy_ms,
-                         "vs_same_box_copy": (ref_copy_ms / mix_avg_ms) if ref_copy_ms else None,
-                         "tuning": pkg.engine.mix_tuning(),
-                         "note": "achieved = algorithmic bytes (2 x active rows x P x 4 [+ slab rows]) / "
-                                 "mean per-launch duration, HIP events on the launch stream"},
-            "matcha_schedule": matcha,
-            "allreduce_baseline": allreduce,
-            "overlap": overlap,
-            "choco": choco,
-            "cpu_resident_models": staged,
-            "configs": configs,
-        }
-        if world > 1:
-            lb = float(np.mean(link_bytes))
-            pb = float(np.mean(pair_bytes))
-            round_s = elapsed / K
-            out["xgmi"] = {"max_link_bytes_per_round": lb, "achieved": lb / round_s / 1e9,
-                           "peak": XGMI_LINK_PEAK / 1e9, "unit": "GB/s",
-                           "frac": lb / round_s / XGMI_LINK_PEAK,
-                           "max_pair_bytes_both_directions": pb,
-                           "achieved_both_directions": pb / round_s / 1e9,
-                           "frac_both_directions": pb / round_s / XGMI_LINK_PEAK,
-                           "aggregate_bytes_per_round": float(np.mean(total_bytes)),
-                           "aggregate_achieved": float(np.mean(total_bytes)) / round_s / 1e9,
-                           "round_ms": 1e3 * round_s, "round_ms_events_rank0": avg_ms,
-                           "exchange_only_ms": 1e3 * exch_s if exch_s else None,
-                           "exchange_only_ms_per_rank": [1e3 * x for x in exch_per] if exch_per else None,
-                           "exchange_only_busiest_link_GBps": lb / exch_s / 1e9 if exch_s else None,
-                           "exchange_only_busiest_pair_both_directions_GBps": pb / exch_s / 1e9 if exch_s else None,
-                           "p2p_probe": ({"bytes": P * 4, "uni_ms": 1e3 * probe["uni"],
-                                          "uni_GBps": P * 4 / probe["uni"] / 1e9, "bi_ms": 1e3 * probe["bi"],
-                                          "bi_GBps_both_directions": 2 * P * 4 / probe["bi"] / 1e9,
-                                          "how": "torch.distributed batch_isend_irecv (RCCL), ranks 0 and 1, "
-                                                 "median of 5 after one untimed transfer"}
-                                         if probe else None),
-                           "note": "busiest GPU pair: bytes that cross it per round (one direction, and "
-                                   "both directions summed) / whole-job round time (exchange + mix), "
-                                   "against the 153 GB/s per-link figure of SURVEY.md §8d"}
-        if world == 1 and args.cpu_seconds > 0:
-            out["cpu_baseline"] = cpu_baseline(pkg, partner, GP.neighbor_weight, n, P, args.cpu_seconds)
-        else:
-            out["cpu_baseline"] = None
-        print(json.dumps(out))
+    # the headline line (filled in further as the figures complete)
+    out = line.out
+    out.update({
+        "metric": METRIC,
+        "value": K / elapsed,
+        "unit": "rounds/s",
+        "n_gpus": world,
+        "steps": K,
+        "warmup": W,
+        "ms_per_step": 1e3 * elapsed / K,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (splitmix64 uniform[-1,1), resident in HBM)",
+        "config": {"workload": f"graph {args.graph} ({n} workers), P={P} fp32 per worker, "
+                               f"budget {args.budget} ({'every matching active' if args.budget >= 1 else 'MATCHA schedule'})",
+                   "workers": n, "params_per_worker": P, "graph": args.graph, "budget": args.budget,
+                   "parallelism": f"{n} workers over {world} GPU(s)" +
+                                  (f", placement {args.placement}" if world > 1 else "") +
+                                  (f", exchange form {overlap['chosen_form']}" if overlap and
+                                   overlap.get("chosen_form") else ""),
+                   "placement": group.placement if world > 1 else None,
+                   "transport": args.transport if world > 1 else None},
+        "parity_ok": None,
+        "round_us": {"events_min": 1e3 * float(step_ms.min()), "events_median": 1e3 * float(np.median(step_ms)),
+                     "events_mean": 1e3 * avg_ms, "events_last_block_mean": 1e3 * float(step_ms[-K:].mean()),
+                     "events_first_block_mean": 1e3 * float(step_ms[:K].mean()),
+                     "diag_rounds": int(diag_rounds), "timed_mean": 1e6 * elapsed / K,
+                     "note": f"per-round HIP events of {diag_rounds} untimed rounds (blocks of K, >= "
+                             f"{args.settle_ms} ms) run between the warmup and the timed region (rank 0)"},
+        "roofline": {"bound": "hbm", "kernel": f"{pkg.engine.mix_kernel_name(eng.n_slots)} (mx_gossip_mix)",
+                     "achieved": achieved / 1e9, "peak": HBM_PEAK / 1e9, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK, "traffic": traffic,
+                     "traffic_source": traffic_src, "bytes_per_launch": mix_bytes,
+                     "avg_launch_ms": mix_avg_ms, "min_launch_ms": float(mix_ms.min()),
+                     "median_launch_ms": float(np.median(mix_ms)),
+                     "frac_timed_region": (mix_bytes / (elapsed / K)) / HBM_PEAK if world == 1 else None,
+                     "same_box_torch_copy_ms": ref_copy_ms,
+                     "vs_same_box_copy": (ref_copy_ms / mix_avg_ms) if ref_copy_ms else None,
+                     "tuning": pkg.engine.mix_tuning(),
+                     "note": "achieved = algorithmic bytes (2 x active rows x P x 4 [+ slab rows]) / "
+                             "mean per-launch duration, HIP events on the launch stream"},
+        "overlap": overlap,
+    })
     if world > 1:
+        lb = float(np.mean(link_bytes))
+        pb = float(np.mean(pair_bytes))
+        round_s = elapsed / K
+        out["xgmi"] = {"max_link_bytes_per_round": lb, "achieved": lb / round_s / 1e9,
+                       "peak": XGMI_LINK_PEAK / 1e9, "unit": "GB/s",
+                       "frac": lb / round_s / XGMI_LINK_PEAK,
+                       "max_pair_bytes_both_directions": pb,
+                       "achieved_both_directions": pb / round_s / 1e9,
+                       "frac_both_directions": pb / round_s / XGMI_LINK_PEAK,
+                       "aggregate_bytes_per_round": float(np.mean(total_bytes)),
+                       "aggregate_achieved": float(np.mean(total_bytes)) / round_s / 1e9,
+                       "round_ms": 1e3 * round_s, "round_ms_events_rank0": avg_ms,
+                       "exchange_only_ms": None, "exchange_only_ms_per_rank": None, "p2p_probe": None,
+                       "note": "busiest GPU pair: bytes that cross it per round (one direction, and "
+                               "both directions summed) / whole-job round time (exchange + mix), "
+                               "against the 153 GB/s per-link figure of SURVEY.md §8d"}
+    wd.disarm()
+    # self-check: every worker's sampled columns after every round the timed group ran vs the
+    # oracle's rounds on the same columns from the synthetic initial values (checker, untimed)
+    if rank == 0:
+        out["parity_ok"] = oracle_column_parity(GP, synth_columns(range(n), cols), final_cols, applied[id(timed)])
+        out["parity"] = (f"every worker's {len(cols)} sampled columns after all {len(applied[id(timed)])} rounds "
+                         f"this run applied, vs the CPU oracle's decen rounds (oracle/matcha_oracle.c) on the "
+                         f"same columns from the same synthetic initial values (uint32 compare)")
+
+    # ------------------------------------------------------------------ secondary figures
+    t_fig = time.monotonic()
+    skip = {}
+    if args.debug_skip:
+        nm, rk = args.debug_skip.split(":")
+        skip = {nm: int(rk)}
+
+    def figure(name, fn, enabled=True):
+        if not enabled:
+            return None
+        over = time.monotonic() - t_fig > args.figures_budget
+        if world > 1:
+            wd.arm(f"{name} (budget check)", args.figure_timeout)
+            over = max_over_ranks(float(over), world, dev) > 0
+            wd.disarm()
+        if over:
+            return {"skipped": f"figures budget of {args.figures_budget:.0f} s spent"}
+        if skip.get(name) == rank:
+            return {"skipped": "--debug-skip"}
+        wd.arm(name, args.figure_timeout)
+        res = guarded(name, fn)
+        wd.disarm()
+        return res
+
+    if world > 1:
+        def _xo():
+            s, per = exchange_only(group, timed_first, K, world, dev)
+            out["xgmi"].update({"exchange_only_ms": 1e3 * s, "exchange_only_ms_per_rank": [1e3 * x for x in per],
+                                "exchange_only_busiest_link_GBps": float(np.mean(link_bytes)) / s / 1e9,
+                                "exchange_only_busiest_pair_both_directions_GBps":
+                                    float(np.mean(pair_bytes)) / s / 1e9})
+            return True
+        xo = figure("exchange_only", _xo)
+        if isinstance(xo, dict):
+            out["xgmi"]["exchange_only_error"] = xo
+        probe = figure("p2p_probe", lambda: p2p_probe(rank, world, P * 4, dev))
+        if probe and "uni" in probe:
+            out["xgmi"]["p2p_probe"] = {"bytes": P * 4, "uni_ms": 1e3 * probe["uni"],
+                                        "uni_GBps": P * 4 / probe["uni"] / 1e9, "bi_ms": 1e3 * probe["bi"],
+                                        "bi_GBps_both_directions": 2 * P * 4 / probe["bi"] / 1e9,
+                                        "how": "torch.distributed batch_isend_irecv (RCCL), ranks 0 and 1, "
+                                               "median of 5 after one untimed transfer"}
+        elif probe:
+            out["xgmi"]["p2p_probe"] = probe
+    out["cpu_baseline"] = None
+    if world == 1 and args.cpu_seconds > 0 and rank == 0:
+        out["cpu_baseline"] = guarded("cpu_baseline", lambda: cpu_baseline(partner, GP.neighbor_weight, n, P,
+                                                                           args.cpu_seconds))
+    out["matcha_schedule"] = figure("matcha", lambda: matcha_figure(pkg, args, rank, world, n, P, K, W, comm, dev),
+                                    args.budget >= 1.0)
+    out["allreduce_baseline"] = figure("allreduce", lambda: allreduce_figure(group, n, world, dev, max(5, K // 5), 2),
+                                       bool(args.allreduce))
+    # the headline groups are done: release them before the large figures
+    for g in {id(g): g for g in (timed, group)}.values():
+        g.close()
+    forms.clear()
+    del timed, group
+    torch.cuda.empty_cache()
+    out["choco"] = figure("choco", lambda: choco_figure(pkg, GP, rank, world, max(20, K), 3, comm, dev,
+                                                        P=args.choco_params, placement=args.placement),
+                          bool(args.choco))
+    out["cpu_resident_models"] = figure("staged", lambda: staged_figure(pkg, GP, n, P, 3, W),
+                                        world == 1 and bool(args.staged))
+    out["configs"] = figure("configs", lambda: config_figures(pkg, args, rank, world, n, max(10, K), 3, comm, dev),
+                            bool(args.configs))
+    out["er64_sweep"] = figure("er64", lambda: er_figure(pkg, args, rank, world, comm, dev), bool(args.er))
+    out["figures_s"] = time.monotonic() - t_fig
+    line.emit()
+    if world > 1:
+        wd.arm("teardown", args.figure_timeout)
         dist.barrier()
-        timed.close()                            # the pull transport's shared buffers, if any
-        group.close()
         if not gloo:
             comm.close()
         dist.destroy_process_group()
+        wd.disarm()
 
 
 if __name__ == "__main__":

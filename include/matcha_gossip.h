@@ -64,8 +64,9 @@ int mx_flags_binomial_sequential(const uint32_t* key_in, int pos_in, const doubl
  *   owner_dev    int32 [n_global]      rank owning each worker; NULL = all local
  *   plan_dev     int32 [T][mx_plan_words(n_local, M)]
  * Plan record layout (int32 words): [0] any flag set, [1] n_remote, [2] idle-row mode
- *   (mx_plan_set_idle; 0 after mx_plan_build), [3] 1 if the round has more than 155 distinct
- *   remote partners (not representable; callers size n_slots <= 156 beforehand),
+ *   (mx_plan_set_idle; 0 after mx_plan_build), [3] 1 if the round has more than 156 distinct
+ *   remote partners (not representable: mx_plan_build then returns MX_ERR_INVALID after one
+ *   4-byte read-back and a stream synchronize at build time),
  *   [4, 4+n_local) degree, [4+n_local, 4+2n_local) selfweight (f32 bits),
  *   [4+2n_local + r*M + e] source slot of row r's e-th partner (slot < n_local: local row,
  *   slot >= n_local: receive slab row slot - n_local).
@@ -252,6 +253,18 @@ int mx_choco_apply_at(float* x, float* x_hat, float* s, int64_t ld, int64_t P, i
  */
 int mx_rccl_unique_id(void* id_out /* 128 bytes */);
 int mx_rccl_init(const void* id /* 128 bytes */, int nranks, int rank, void** comm_out);
+/* The communicator is NON-blocking (ncclConfig_t.blocking = 0) and every RCCL call the library
+ * makes on it waits for its enqueue against a deadline: a peer rank that never joins (dead, or
+ * skipped the call) turns into MX_ERR_RCCL "timed out" instead of a hang.  mx_rccl_init uses
+ * $MX_RCCL_TIMEOUT_S (default 300 s); mx_rccl_init_timeout takes it explicitly (the deadline then
+ * applies to the init and to every later operation of the process).  An init that times out is
+ * aborted before returning; *nonblocking_out (optional) = 1.  Replaces the mpi4py COMM_WORLD set
+ * up at train_mpi.py:237-239. */
+int mx_rccl_init_timeout(const void* id, int nranks, int rank, int64_t timeout_ms, void** comm_out,
+                         int* nonblocking_out);
+/* ncclCommAbort: release a communicator whose peers are gone (after a timed-out operation). */
+int mx_rccl_abort(void* comm);
+/* ncclCommFinalize (waited for with the deadline; aborted on expiry) + ncclCommDestroy. */
 int mx_rccl_destroy(void* comm);
 /* The ordered operations mx_exchange_round posts for this rank, host only (no GPU, no RCCL):
  * ops[4i..4i+3] = {kind (0 send / 1 recv), peer rank, local row (send) or slab slot (recv),
@@ -293,7 +306,8 @@ int mx_allreduce_mean_ordered(void* comm, float* buf, int64_t count, float* gath
 /* ncclAllGather of `count` floats per rank into gather[nranks][count] (rank order). */
 int mx_allgather(void* comm, const float* send, int64_t count, float* gather, void* stream);
 /* out[i] = (rows[0][i] + ... + rows[nrows-1][i] in the given order) / nrows for i < count; rows
- * are nrows x ld floats (device), 1 <= nrows <= 64; out may be rows[0].  The division step of
+ * are nrows x ld floats (device), 1 <= nrows <= 2^24 (the tree order for any count: a binary counter
+ * of partial sums); out may be rows[0].  The division step of
  * the centralized communicator (communicator.py:61-62) and of sync_allreduce (train_mpi.py:46-55),
  * callable after any transport's gather. */
 int mx_mean_rows(const float* rows, int nrows, int64_t ld, int64_t count, int order, float* out, void* stream);

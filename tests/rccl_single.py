@@ -26,7 +26,7 @@ def main():
     pkg = importlib.import_module(PKG)
     import oracle as O
     comm = pkg.engine.RcclComm()
-    out = {"rank": comm.rank, "nranks": comm.nranks}
+    out = {"rank": comm.rank, "nranks": comm.nranks, "nonblocking": comm.nonblocking}
     # all-reduce mean over one rank: sum / 1 leaves every value as it was
     x = torch.from_numpy(O.synth(5, 1_000_003)).cuda()
     y = x.clone()

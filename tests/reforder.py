@@ -17,3 +17,21 @@ def mpi4py_sum(rows, order):
                 v[r] = v[r] + v[r + m]
         m *= 2
     return v[0]
+
+
+def binary_counter_sum(rows):
+    """The binomial tree as mx_mean_rows computes it above 64 rows: a binary counter of partial
+    sums, folded right to left at the end (exchange.cpp, mean_rows_kernel TREE = 2)."""
+    stack, c = {}, 0
+    for r in rows:
+        p, lvl = r.copy(), 0
+        while (c >> lvl) & 1:
+            p = stack[lvl] + p
+            lvl += 1
+        stack[lvl] = p
+        c += 1
+    acc = None
+    for lvl in range(c.bit_length()):
+        if (c >> lvl) & 1:
+            acc = stack[lvl] if acc is None else stack[lvl] + acc
+    return acc

@@ -178,13 +178,14 @@ def test_cpu_inputs_staged_through_the_gpu(pkg, O):
         pkg.flatten_tensors([ts[0], ts[1].cuda()])
 
 
-@pytest.mark.parametrize("nrows", [1, 2, 3, 5, 7, 8, 9, 16, 33, 64])
+@pytest.mark.parametrize("nrows", [1, 2, 3, 5, 7, 8, 9, 16, 33, 64, 65, 100, 129, 300])
 @pytest.mark.parametrize("order", ["tree", "sequential"])
 def test_mean_rows_reference_order(pkg, O, nrows, order):
     """mx_mean_rows (the division step of centralizedCommunicator / sync_allreduce) sums in
-    mpi4py's binomial-tree order (default) or rank order, then divides: bit-exact vs numpy fp32."""
+    mpi4py's binomial-tree order (default) or rank order, then divides: bit-exact vs numpy fp32.
+    Above 64 rows the tree runs as a binary counter of partial sums (any world size)."""
     from reforder import mpi4py_sum as _mpi4py_sum
-    count, ld = 100_003, 100_032
+    count, ld = (100_003, 100_032) if nrows <= 64 else (20_011, 20_032)
     rows = [O.synth(31 * r + nrows, count) * np.float32(10.0 ** (r % 4 - 1)) for r in range(nrows)]
     dev = torch.zeros((nrows, ld), dtype=torch.float32, device="cuda")
     dev[:, :count] = torch.from_numpy(np.stack(rows))
@@ -196,4 +197,4 @@ def test_mean_rows_reference_order(pkg, O, nrows, order):
     # in place into row 0 (out aliases rows[0])
     pkg._lib.check(pkg.lib.mx_mean_rows(dev.data_ptr(), nrows, ld, count, code, dev.data_ptr(), None))
     assert np.array_equal(dev[0, :count].cpu().numpy().view(np.uint32), want.view(np.uint32))
-    assert pkg.lib.mx_mean_rows(dev.data_ptr(), 65, ld, count, code, out.data_ptr(), None) != 0
+    assert pkg.lib.mx_mean_rows(dev.data_ptr(), 0, ld, count, code, out.data_ptr(), None) != 0

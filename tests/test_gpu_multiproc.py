@@ -42,23 +42,58 @@ def test_multiprocess_rounds_match_oracle(nproc):
     assert res["world"] == nproc and all(v for k, v in res.items() if k != "world"), res
 
 
-def test_bench_multiprocess_path():
-    """bench.py's N > 1 branch (partition, exchange, barriers, max-over-ranks timing, xgmi object,
-    Choco figure) end to end with 2 ranks on one GPU."""
-    r = _torchrun(2, ["bench.py", "--gpus", "2", "--transport", "gloo", "--steps", "3", "--warmup", "1",
-                      "--params", "200000", "--choco-params", "300000", "--cpu-seconds", "0"])
+@pytest.mark.parametrize("nproc", [2, 4])
+def test_bench_multiprocess_path(nproc):
+    """bench.py's N > 1 branch (partition, exchange, barriers, max-over-ranks timing, xgmi object)
+    end to end on one GPU, with EVERY figure at reduced size: the headline, MATCHA 0.5, Choco (VGG
+    config 4), the WRN / ResNet configs 2-3 and the ER(64) budget sweep (config 5) -- each one's
+    oracle self-check must pass (configs 3-5 self-checking at N > 1)."""
+    r = _torchrun(nproc, ["bench.py", "--gpus", str(nproc), "--transport", "gloo", "--steps", "3", "--warmup", "1",
+                          "--params", "200000", "--choco-params", "300000", "--cpu-seconds", "0",
+                          "--wrn-params", "70000", "--resnet-params", "30000", "--er-params", "20000",
+                          "--er-rounds", "2", "--er-budgets", "0.3,1.0"], timeout=280)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     out = json.loads(line)
-    assert out["n_gpus"] == 2 and out["value"] > 0 and out["xgmi"]["max_link_bytes_per_round"] > 0
+    assert "error" not in out, out["error"]
+    assert out["n_gpus"] == nproc and out["value"] > 0 and out["xgmi"]["max_link_bytes_per_round"] > 0
     assert out["xgmi"]["exchange_only_ms"] > 0 and out["xgmi"]["p2p_probe"]["uni_GBps"] > 0
     ov = out["overlap"]
     assert ov["mode"] == "auto" and ov["chunks"] == 4 and ov["chosen"] in ("chunked", "unchunked")
     assert ov["calib_ms_unchunked"] > 0 and ov["calib_ms_chunked"] > 0
     assert out["choco"]["rounds_per_s"] > 0 and out["cpu_baseline"] is None
     assert out["allreduce_baseline"]["rounds_per_s"] > 0
-    assert out["parity_ok"] is True and out["choco"]["parity_ok"] is True     # self-checks vs 1-GPU recompute
-    assert len(out["xgmi"]["exchange_only_ms_per_rank"]) == 2
+    # every self-check is the oracle's (checker) on the same inputs
+    assert out["parity_ok"] is True and "oracle" in out["parity"]
+    assert out["choco"]["parity_ok"] is True
+    assert out["matcha_schedule"]["parity_ok"] is True
+    cf = out["configs"]
+    assert all(cf[k]["parity_ok"] is True and cf[k]["rounds_per_s"] > 0
+               for k in ("wrn28_10_matcha0.5", "wrn28_10_full", "resnet18_100_matcha0.5")), cf
+    er = out["er64_sweep"]
+    assert er["parity_ok"] is True and er["params_per_worker"] == 20000 and er["rows_per_gpu"] == 64 // nproc
+    assert len(er["sweep"]) == 2 and all(len(b["slots_per_rank"]) == nproc for b in er["sweep"])
+    full = er["sweep"][-1]
+    assert full["budget"] == 1.0 and full["max_link_bytes_per_round"] > 0 and full["rounds_per_s"] > 0
+    assert (full["exchange_only_ms"] or 0) > 0 or er["form"] != "rccl"
+    assert set(er["calib_ms"]) == {"rccl", "rccl_chunked", "pull"}
+    assert len(out["xgmi"]["exchange_only_ms_per_rank"]) == nproc
+
+
+def test_bench_watchdog_line_on_hang():
+    """A rank that skips a figure's collectives (--debug-skip allreduce:1) leaves its peer waiting:
+    the watchdog makes rank 0 print the line measured so far -- the headline intact -- with an
+    "error" naming the stuck figure, and every rank exits, instead of the run hanging."""
+    r = _torchrun(2, ["bench.py", "--gpus", "2", "--transport", "gloo", "--steps", "3", "--warmup", "1",
+                      "--params", "100000", "--cpu-seconds", "0", "--configs", "0", "--er", "0",
+                      "--figure-timeout", "15", "--debug-skip", "allreduce:1"], timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, lines
+    out = json.loads(lines[0])
+    assert out["value"] > 0 and out["parity_ok"] is True
+    errs = [out.get("error")] + [v.get("error") for v in out.values() if isinstance(v, dict)]
+    assert any(errs), out
 
 
 @pytest.mark.parametrize("nproc,overlap,pull", [(2, "on", "off"), (4, "off", "off"), (2, "off", "on"),
@@ -68,7 +103,7 @@ def test_bench_multiprocess_overlap_forms(nproc, overlap, pull):
     calibrated among all three; the timed form passes the self-check."""
     r = _torchrun(nproc, ["bench.py", "--gpus", str(nproc), "--transport", "gloo", "--steps", "3", "--warmup", "1",
                           "--params", "100000", "--choco", "0", "--cpu-seconds", "0", "--overlap", overlap,
-                          "--pull", pull])
+                          "--pull", pull, "--configs", "0", "--er", "0", "--allreduce", "0"])
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["value"] > 0 and out["parity_ok"] is True
@@ -100,26 +135,43 @@ def test_rccl_single_rank_linkage():
     r = _torchrun(1, [os.path.join(HERE, "rccl_single.py")], timeout=150)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
-    assert out == {"rank": 0, "nranks": 1, "allreduce_identity": True, "decen_bit_exact": True,
+    assert out == {"rank": 0, "nranks": 1, "nonblocking": True, "allreduce_identity": True, "decen_bit_exact": True,
                    "post_self_exchange": True, "post_validates": True, "post_validates_peer": True,
                    "allreduce_ordered_identity": True}, out
+
+
+def test_rccl_init_deadline():
+    """A 2-rank RCCL communicator whose second rank never joins: mx_rccl_init_timeout returns
+    MX_ERR_RCCL ("timed out") after its 4 s deadline instead of hanging, and the process exits."""
+    r = subprocess.run([sys.executable, os.path.join(HERE, "rccl_deadline.py")], cwd=ROOT, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["rc"] == -3 and out["handle_null"] and "never joined" in out["message"], out
+    assert 3.5 <= out["seconds"] < 60, out
 
 
 def test_bench_single_gpu_line():
     """bench.py at N = 1 (headline shape, few rounds): the line's contract fields, the self-check,
     the per-round event statistics, the config and host-model figures and the CPU baseline legs."""
     r = subprocess.run([sys.executable, "bench.py", "--steps", "4", "--warmup", "2",
-                        "--choco-params", "200000", "--cpu-seconds", "1"], cwd=ROOT, capture_output=True,
+                        "--choco-params", "200000", "--cpu-seconds", "1", "--er-params", "3e6",
+                        "--er-budgets", "0.2,1.0"], cwd=ROOT, capture_output=True,
                        text=True, timeout=280, env=dict(os.environ, OMP_NUM_THREADS="2"))
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["n_gpus"] == 1 and out["steps"] == 4 and out["warmup"] == 2 and out["value"] > 0
-    assert out["parity_ok"] is True
+    assert "error" not in out and out["parity_ok"] is True and "oracle" in out["parity"]
+    assert out["choco"]["parity_ok"] is True and out["matcha_schedule"]["parity_ok"] is True
+    assert out["er64_sweep"]["parity_ok"] is True and out["er64_sweep"]["params_per_worker"] == 3_000_000
+    assert all(out["configs"][k]["parity_ok"] for k in ("wrn28_10_matcha0.5", "wrn28_10_full",
+                                                         "resnet18_100_matcha0.5"))
     ru = out["round_us"]
     assert 0 < ru["events_min"] <= ru["events_median"]
     assert out["roofline"]["frac"] > 0 and out["roofline"]["min_launch_ms"] > 0
     assert out["cpu_resident_models"]["rounds_per_s"] > 0
-    assert set(out["configs"]) == {"wrn28_10_matcha0.5", "wrn28_10_full", "resnet18_100_matcha0.5"}
-    assert all(v["rounds_per_s"] > 0 and v["hbm_TBps"] > 0 for v in out["configs"].values())
+    cfg = {k: v for k, v in out["configs"].items() if k != "parity"}
+    assert set(cfg) == {"wrn28_10_matcha0.5", "wrn28_10_full", "resnet18_100_matcha0.5"}
+    assert all(v["rounds_per_s"] > 0 and v["hbm_TBps"] > 0 for v in cfg.values())
     cb = out["cpu_baseline"]
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["pickle"]["value"] > 0 and cb["pickle"]["cores"] >= 1

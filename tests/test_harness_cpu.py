@@ -83,3 +83,29 @@ def test_rendezvous_port_from_job_id(pkg):
     assert a != b and 20000 <= a < 50000 and a == rp({"PMIX_NAMESPACE": "prterun-node-1234@1"})
     assert rp({"SLURM_JOB_ID": "77"}) == rp({"SLURM_JOB_ID": "77"})
     assert rp({}) == 29533
+
+
+def test_pull_transport_refused_where_it_cannot_carry(pkg):
+    """The pull transport serves whole-row gossip only (VirtualWorkerGroup): the Choco and the
+    centralized communicators refuse it at construction with a clear TypeError, not
+    with a null-handle error at the first round.  No GPU: the refusal comes first."""
+    import pytest as _pytest
+    from conftest import Topo
+    t = pkg.PullTransport.__new__(pkg.PullTransport)
+    topo = Topo([[1, 0]], 0.5, [[1]])
+    with _pytest.raises(TypeError, match="PullTransport"):
+        pkg.centralizedCommunicator(0, 2, transport=t)
+    with _pytest.raises(TypeError, match="PullTransport"):
+        pkg.ChocoCommunicator(0, 2, topo, 0.9, 0.1, transport=t)
+
+
+def test_rccl_deadline_api_declared(pkg):
+    """The non-blocking RCCL communicator with a deadline is part of the C ABI (checked without a
+    GPU: argument validation only)."""
+    import ctypes
+    h = ctypes.c_void_p()
+    assert pkg.lib.mx_rccl_init_timeout(None, 2, 0, 1000, ctypes.byref(h), None) == -1
+    uid = (ctypes.c_char * 128)()
+    assert pkg.lib.mx_rccl_init_timeout(ctypes.cast(uid, ctypes.c_void_p), 2, 5, 1000, ctypes.byref(h), None) == -1
+    assert pkg.lib.mx_rccl_init_timeout(ctypes.cast(uid, ctypes.c_void_p), 2, 0, 0, ctypes.byref(h), None) == -1
+    assert pkg.lib.mx_rccl_abort(None) == 0 and pkg.lib.mx_rccl_destroy(None) == 0
