@@ -15,9 +15,10 @@
 //                      chunk-local index) into the chunk's own region in index order (wave scans
 //                      + one barrier), counts its top digit into the 12-bit candidate histogram
 //                      and adds the block's kept count to the row's candidate total;
-//                      compact_kernel(fallback) re-runs with b_lo = 0 (into a histogram of its
-//                      own) in the (sample-dependent, rare) case that fewer than k were kept --
-//                      the result is exact either way;
+//                      in the (sample-dependent, rare) case that fewer than k were kept, the
+//                      first candidate pass re-runs the compaction with b_lo = 0 (into a histogram
+//                      of its own) on its own blocks before histogramming (a row grid barrier in
+//                      that path only) -- the result is exact either way;
 //   C  cand_hist<10>, cand_hist<9>: the 10- and 9-bit digits of the candidates matching the
 //      prefix resolved so far; every block of a pass re-resolves the previous histograms itself
 //      (find_bin, read-only), so no one-block select launches sit between the passes;
@@ -30,8 +31,8 @@
 //      bounds that mx_choco_apply reads (the output offset of every chunk), and re-zeroes the
 //      histograms / counters for the next call.
 // Everything stays on the device; no host round trip.  All local workers' rows are processed by
-// the same launches (blockIdx.y = row): 6 launches per call for any number of rows (7 with the
-// fallback pass that sampling needs).
+// the same launches (blockIdx.y = row): 6 launches per call for any number of rows (the fallback
+// compaction that sampling may need rides in the first candidate pass: no launch of its own).
 //
 // Work invariant: the histograms and the candidate total are zero on entry (the
 // caller zero-fills the scratch once; every call leaves it that way), so no zeroing launch runs.
@@ -56,6 +57,7 @@ struct SelState {
     uint32_t T;           // exact threshold key (cand_mark)
     int64_t need;         // ties of T to take (cand_mark)
     unsigned long long cand_n;   // candidates kept by the first compact_kernel pass (zero on entry)
+    uint32_t bar;         // arrivals at the fallback's row barrier (zero on entry)
 };
 
 // Per-chunk counters and per-block totals are 64-byte records, each written whole by one store
@@ -363,9 +365,8 @@ __device__ Resolved resolve(const RowView& v, int64_t k, int stages) {
 // shuffle scans (several rows: 650 vs 655 us with ballots, whose 64-bit masks spill SGPRs)
 // LOOP: candidate stores in a loop over the lane's kept elements (mx_topk_set "compact_store" 1)
 template <bool BAL, bool LOOP>
-__global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double frac, int fallback) {
-    const RowView v = row_view(R);
-    if (fallback && v.st->cand_n >= (unsigned long long)R.k) return;
+__device__ void compact_run(const Rows& R, const RowView& v, int64_t S, double frac, int fallback, int64_t bx,
+                            int64_t gx) {
     __shared__ uint32_t wtot[2][kWaves];
     __shared__ uint32_t h[kTopBins];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -383,7 +384,7 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double
             ah[j] = h4 ? __builtin_nontemporal_load(h4 + q0 + j * 64) : f4{0.0f, 0.0f, 0.0f, 0.0f};
         }
     };
-    int64_t c = blockIdx.x;
+    int64_t c = bx;
     if (c < nc && whole(c)) issue(c);              // the first chunk flies while b_lo is resolved
 
     uint32_t b_lo = 0;
@@ -397,7 +398,7 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double
         int64_t rem, tot;
         find_bin<kTopBins>(v.hs, want, &b, &rem, &tot);
         b_lo = tot < want ? 0u : (uint32_t)b;               // too few sampled keys: keep everything
-        if (blockIdx.x == 0 && threadIdx.x == 0) v.st->b0 = b_lo;
+        if (bx == 0 && threadIdx.x == 0) v.st->b0 = b_lo;
     }
     // only digits >= b_lo are ever counted: zero and flush just those bins (b_lo is near the top)
     const int h0 = (int)(b_lo & ~(uint32_t)(kTPB - 1));
@@ -488,17 +489,17 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double
         if (threadIdx.x == 0) kept += all;
         par ^= 1;
     };
-    for (; c < nfull; c += gridDim.x) {
+    for (; c < nfull; c += gx) {
         float d[4][4];
         const int n[4] = {4, 4, 4, 4};
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
             for (int e = 0; e < 4; ++e) d[j][e] = h4 ? __fsub_rn(ax[j][e], ah[j][e]) : ax[j][e];
-        if (c + gridDim.x < nfull) issue(c + gridDim.x);
+        if (c + gx < nfull) issue(c + gx);
         step(c, d, n);
     }
-    for (; c < nc; c += gridDim.x) {
+    for (; c < nc; c += gx) {
         float d[4][4];
         int n[4];
         const int64_t q0 = c * (kChunk / 4) + wave * kSubQuads;
@@ -513,6 +514,29 @@ __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double
     if (!fallback && threadIdx.x == 0 && kept) atomicAdd(&v.st->cand_n, (unsigned long long)kept);
 }
 
+template <bool BAL, bool LOOP>
+__global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double frac) {
+    const RowView v = row_view(R);
+    compact_run<BAL, LOOP>(R, v, S, frac, 0, blockIdx.x, gridDim.x);
+}
+
+// Every block of this row's grid has arrived (rare path only: the fallback compaction inside the
+// first candidate pass).  Producers: every wave's stores drained and released at agent scope, then
+// one arrival per block on the row's counter; the poller's agent-scope acquire then covers the
+// workgroup behind the barrier.  The grid of that pass is a few hundred blocks per row, far below
+// what the chip holds at once, so every block of a row is resident while it waits.
+__device__ void row_grid_barrier(SelState* st, unsigned blocks) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(&st->bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (__hip_atomic_load(&st->bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < blocks)
+            __builtin_amdgcn_s_sleep(4);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+    __syncthreads();
+}
+
 // counts and first candidates of two chunk regions, loaded one step ahead by the candidate passes
 struct RegionPair {
     int64_t n1, n2;
@@ -521,9 +545,19 @@ struct RegionPair {
 
 // candidate histogram of the next digit (10 bits at 9, or 9 bits at 0) among candidates matching
 // the prefix resolved so far; one wave per chunk region; LDS histogram flushed once per block
-template <int BITS>
-__global__ __launch_bounds__(kTPB) void cand_hist(Rows R) {
+// The first candidate pass (BITS = 10) also stands in for the fallback compaction: with a
+// sampled floor (S > 1) a row whose compaction kept fewer than k keys is compacted again here, by
+// this pass's own blocks, keeping every key (into the fallback histogram), and the row's blocks
+// meet at a grid barrier before histogramming -- a rare path, so the common one pays no launch.
+template <int BITS, bool BAL, bool LOOP>
+__global__ __launch_bounds__(kTPB) void cand_hist(Rows R, int64_t S, double frac) {
     const RowView v = row_view(R);
+    if constexpr (BITS == kMidBits) {
+        if (S > 1 && v.st->cand_n < (unsigned long long)R.k) {     // block-uniform
+            compact_run<BAL, LOOP>(R, v, S, frac, 1, blockIdx.x, gridDim.x);
+            row_grid_barrier(v.st, gridDim.x);
+        }
+    }
     constexpr int NB = 1 << BITS;
     constexpr int stages = BITS == kMidBits ? 1 : 2;
     constexpr int shift = BITS == kMidBits ? kMidShift : 0;
@@ -655,7 +689,10 @@ __global__ __launch_bounds__(kTPB) void write_cand(Rows R, int64_t G) {
     // nothing reads the histograms or the candidate total any more: re-zero them for the next call
     for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < kHistWords; i += (int64_t)gridDim.x * kTPB)
         v.hs[i] = 0;
-    if (blockIdx.x == 0 && threadIdx.x == 0) v.st->cand_n = 0;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        v.st->cand_n = 0;
+        v.st->bar = 0;
+    }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t c_first = (int64_t)blockIdx.x * kWaves;
     const int64_t c = c_first + wave;
@@ -1132,10 +1169,12 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
     MX_L(sample_kernel, dim3(sgrid, nrows), kTPB, S);
     auto ck = nrows == 1 ? (g_compact_store ? compact_kernel<true, true> : compact_kernel<true, false>)
                          : (g_compact_store ? compact_kernel<false, true> : compact_kernel<false, false>);
-    MX_L(ck, dim3(bgrid, nrows), kTPB, S, frac, 0);
-    if (S > 1) MX_L(ck, dim3(bgrid, nrows), kTPB, S, frac, 1);
-    MX_L(cand_hist<kMidBits>, dim3(cgrid, nrows), kTPB);
-    MX_L(cand_hist<kLowBits>, dim3(cgrid, nrows), kTPB);
+    MX_L(ck, dim3(bgrid, nrows), kTPB, S, frac);
+    // the fallback compaction (S > 1, rare) runs inside the first candidate pass
+    auto h10 = nrows == 1 ? (g_compact_store ? cand_hist<kMidBits, true, true> : cand_hist<kMidBits, true, false>)
+                          : (g_compact_store ? cand_hist<kMidBits, false, true> : cand_hist<kMidBits, false, false>);
+    MX_L(h10, dim3(cgrid, nrows), kTPB, S, frac);
+    MX_L((cand_hist<kLowBits, false, false>), dim3(cgrid, nrows), kTPB, S, frac);
     const int64_t G = (nc + cgrid - 1) / cgrid;    // chunks per cand_mark block
     MX_L(cand_mark, dim3(cgrid, nrows), kTPB, G);
     MX_L(write_cand, dim3(wgrid, nrows), kTPB, G);

@@ -709,10 +709,13 @@ struct Cfg {
     int vec, ns;
 };
 
+int g_ns48 = 0;      // 33-48 slots: a 48-slot row-kernel class (48 KB tiles) instead of the 64-slot one
+
 Cfg pick(int n_slots) {
     if (n_slots <= 8) return {4, 8};
     if (n_slots <= 16) return {4, 16};
     if (n_slots <= 32) return {2, 32};
+    if (n_slots <= 48 && g_ns48) return {1, 48};
     if (n_slots <= 64) return {1, 64};
     if (n_slots <= kWideMaxSlots) return {1, 0};    // wide kernel only (256-column layout tiles)
     return {0, 0};
@@ -776,7 +779,7 @@ inline int64_t grid_for(int64_t total_tiles) {
 // auto picks the smallest split giving the persistent grid 1.5 work items per workgroup
 // (measured, 8 slots: 651 tiles run 11 % faster as 1302 sub-tiles, 977 tiles 5 % slower as 1954)
 int row_split(int ns, int64_t total_tiles) {
-    const int cap = ns == 64 ? 1 : (ns == 32 ? 2 : 4);
+    const int cap = ns >= 48 ? 1 : (ns == 32 ? 2 : 4);
     if (g_tune.split > 0) return g_tune.split < cap ? g_tune.split : cap;
     int s = 1;
     while (s < cap && 2 * total_tiles * s < 3 * grid_target()) s *= 2;
@@ -872,6 +875,9 @@ extern "C" int mx_mix_set(const char* key, int value) {
     } else if (!strcmp(key, "flat_small")) {
         MX_CHECK(value >= 0 && value <= 4096, "mx_mix_set: flat_small %d", value);
         slot = &g_tune.flat_small;
+    } else if (!strcmp(key, "ns48")) {
+        slot = &g_ns48;
+        value = value ? 1 : 0;
     }
     MX_CHECK(slot, "mx_mix_set: unknown key '%s'", key);
     *slot = value;
@@ -891,6 +897,7 @@ extern "C" int mx_mix_get(const char* key) {
     if (!strcmp(key, "rows")) return g_tune.rows;
     if (!strcmp(key, "split")) return g_tune.split;
     if (!strcmp(key, "flat_small")) return g_tune.flat_small;
+    if (!strcmp(key, "ns48")) return g_ns48;
     mx::set_error("mx_mix_get: unknown key '%s'", key);
     return MX_ERR_INVALID;
 }
@@ -1038,6 +1045,7 @@ int gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev, const int
         if (c.ns == 8) return sp == 4 ? MX_ROWS(8, 256, 4) : sp == 2 ? MX_ROWS(8, 512, 2) : MX_ROWS(8, 1024, 1);
         if (c.ns == 16) return sp == 4 ? MX_ROWS(16, 256, 4) : sp == 2 ? MX_ROWS(16, 512, 2) : MX_ROWS(16, 1024, 1);
         if (c.ns == 32) return sp == 2 ? MX_ROWS(32, 256, 2) : MX_ROWS(32, 512, 1);
+        if (c.ns == 48) return MX_ROWS(48, 256, 1);
         return MX_ROWS(64, 256, 1);
 #undef MX_ROWS
     }

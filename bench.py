@@ -93,6 +93,8 @@ def parse():
                     "the watchdog's")
     ap.add_argument("--debug-skip", default="", help="test hook FIGURE:RANK -- that rank skips that figure "
                     "(its peers then wait in the figure's collectives: exercises the watchdog)")
+    ap.add_argument("--debug-stall", default="", help="test hook FIGURE:RANK -- that rank stalls inside that "
+                    "figure (a hung peer: exercises the watchdog)")
     return ap.parse_args()
 
 
@@ -806,14 +808,45 @@ def timed_rounds(run, group, first, K):
 
 # ----------------------------------------------------------------------------------- main
 def main():
+    """The run happens on a worker thread; the main thread only waits, so it stays free to take
+    SIGTERM -- what the launcher (torchrun) sends every rank when one rank dies -- and rank 0
+    then prints the line measured so far with an "error" field before leaving."""
+    import signal
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
     line = Line(rank)
     wd = Watchdog(rank, line.emit)
+    failed = []
+
+    def on_term(signum, _frame):
+        line.emit(f"terminated by signal {signum} during {wd.name or 'the run'} (the launcher stops every rank "
+                  f"when one rank fails)")
+        os._exit(0)
+
+    signal.signal(signal.SIGTERM, on_term)
+
+    def body():
+        try:
+            run(args, world, rank, line, wd)
+        except BaseException as e:                   # noqa: BLE001 -- reported in the line, then re-raised
+            import traceback
+            traceback.print_exc()
+            failed.append(e)
+            line.emit(f"{wd.name or 'run'}: {type(e).__name__}: {e}")
+
+    t = threading.Thread(target=body, name="bench")
+    t.start()
+    while t.is_alive():
+        t.join(0.5)
+    if failed:
+        sys.exit(1)
+
+
+def run(args, world, rank, line, wd):
+    local = int(os.environ.get("LOCAL_RANK", "0"))
     wd.arm("startup (process group / RCCL communicator)", args.headline_timeout)
     import datetime
     import torch.distributed as dist
@@ -1053,10 +1086,13 @@ def main():
 
     # ------------------------------------------------------------------ secondary figures
     t_fig = time.monotonic()
-    skip = {}
+    skip, stall = {}, {}
     if args.debug_skip:
         nm, rk = args.debug_skip.split(":")
         skip = {nm: int(rk)}
+    if args.debug_stall:
+        nm, rk = args.debug_stall.split(":")
+        stall = {nm: int(rk)}
 
     def figure(name, fn, enabled=True):
         if not enabled:
@@ -1071,6 +1107,8 @@ def main():
         if skip.get(name) == rank:
             return {"skipped": "--debug-skip"}
         wd.arm(name, args.figure_timeout)
+        if stall.get(name) == rank:
+            time.sleep(10 * args.figure_timeout)
         res = guarded(name, fn)
         wd.disarm()
         return res

@@ -81,15 +81,16 @@ def test_bench_multiprocess_path(nproc):
 
 
 def test_bench_watchdog_line_on_hang():
-    """A rank that skips a figure's collectives (--debug-skip allreduce:1) leaves its peer waiting:
-    the watchdog makes rank 0 print the line measured so far -- the headline intact -- with an
-    "error" naming the stuck figure, and every rank exits, instead of the run hanging."""
+    """A rank that skips a figure's collectives (--debug-skip allreduce:1) desynchronises the job:
+    its peer waits in the figure (then the watchdog fires), or the mismatched collectives abort a
+    rank and the launcher SIGTERMs the others.  Either way rank 0 prints the line measured so far
+    -- the headline intact -- with an "error" field, and the job ends instead of hanging (the exit
+    status is the launcher's: non-zero when a rank aborted)."""
     r = _torchrun(2, ["bench.py", "--gpus", "2", "--transport", "gloo", "--steps", "3", "--warmup", "1",
                       "--params", "100000", "--cpu-seconds", "0", "--configs", "0", "--er", "0",
                       "--figure-timeout", "15", "--debug-skip", "allreduce:1"], timeout=240)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, lines
+    assert len(lines) == 1, r.stdout[-3000:] + r.stderr[-3000:]
     out = json.loads(lines[0])
     assert out["value"] > 0 and out["parity_ok"] is True
     errs = [out.get("error")] + [v.get("error") for v in out.values() if isinstance(v, dict)]
@@ -138,6 +139,22 @@ def test_rccl_single_rank_linkage():
     assert out == {"rank": 0, "nranks": 1, "nonblocking": True, "allreduce_identity": True, "decen_bit_exact": True,
                    "post_self_exchange": True, "post_validates": True, "post_validates_peer": True,
                    "allreduce_ordered_identity": True}, out
+
+
+def test_bench_watchdog_line_on_stall():
+    """A rank that hangs inside a figure (--debug-stall choco:1): its peer waits in the figure's
+    collectives until the watchdog's deadline, rank 0 prints the line measured so far with an error
+    naming the figure, and every rank exits 0 (the launcher then returns 0)."""
+    r = _torchrun(2, ["bench.py", "--gpus", "2", "--transport", "gloo", "--steps", "3", "--warmup", "1",
+                      "--params", "100000", "--choco-params", "100000", "--cpu-seconds", "0", "--configs", "0",
+                      "--er", "0", "--figure-timeout", "15", "--debug-stall", "choco:1"], timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:] + r.stderr[-3000:]
+    out = json.loads(lines[0])
+    assert out["value"] > 0 and out["parity_ok"] is True
+    assert "choco" in out["error"] and "no progress" in out["error"], out["error"]
+    assert out["allreduce_baseline"]["rounds_per_s"] > 0 and out.get("choco") is None
 
 
 def test_rccl_init_deadline():

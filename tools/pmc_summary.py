@@ -37,16 +37,17 @@ def counter_per_kernel(path, counter):
     return acc
 
 
-def main(src, dst):
-    stats = rows(os.path.join(src, "trace", "**", "*kernel_stats.csv"))
+def summarize(src, trace="trace", fetch_dir="fetch", write_dir="write"):
+    """kernel stats + per-launch HBM bytes of one profiled process tree under `src`"""
+    stats = rows(os.path.join(src, trace, "**", "*kernel_stats.csv"))
     kernels = {}
     for r in stats:
         name = pick(r, "Name", "KernelName")
         kernels[name] = {"calls": int(pick(r, "Calls")), "avg_us": float(pick(r, "AverageNs")) / 1e3,
                          "min_us": float(pick(r, "MinNs")) / 1e3, "max_us": float(pick(r, "MaxNs")) / 1e3,
                          "pct": float(pick(r, "Percentage"))}
-    fetch = counter_per_kernel(os.path.join(src, "fetch"), "FETCH_SIZE")
-    write = counter_per_kernel(os.path.join(src, "write"), "WRITE_SIZE")
+    fetch = counter_per_kernel(os.path.join(src, fetch_dir), "FETCH_SIZE")
+    write = counter_per_kernel(os.path.join(src, write_dir), "WRITE_SIZE")
     mix = {}
     for name in set(fetch) | set(write):
         if "mix_kernel" not in name:
@@ -73,16 +74,46 @@ def main(src, dst):
                       "hbm_read_bytes_corrected": 2 * 1024 * sum(f) / len(f),
                       "hbm_write_bytes": 1024 * sum(w) / len(w),
                       "hbm_bytes_per_launch": 2 * 1024 * sum(f) / len(f) + 1024 * sum(w) / len(w)}
-    out = {"source": src, "kernels": kernels, "mix_pmc": mix, "pmc_all": allk,
-           "note": "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB -> bytes x1024"}
+    return {"kernels": kernels, "mix_pmc": mix, "pmc_all": allk}
+
+
+def summarize_ranks(src):
+    """tools/profile_multi.sh layout: <pass>/rank<R>/... per rank (or, where this rocprofv3 did not
+    expand %env{RANK}%, one directory per process id).  Per rank: the summary above, the RCCL kernels'
+    share of the trace, and every fabric counter pass (fabric_<COUNTER>/) summed per mixing launch."""
+    out = {}
+    ranks = sorted({d.split("rank", 1)[1] for d in os.listdir(os.path.join(src, "trace")) if d.startswith("rank")})
+    for r in ranks:
+        rs = summarize(src, os.path.join("trace", "rank" + r), os.path.join("fetch_size", "rank" + r),
+                       os.path.join("write_size", "rank" + r))
+        rs["rccl_kernels"] = {k: v for k, v in rs["kernels"].items() if "nccl" in k.lower() or "rccl" in k.lower()}
+        fab = {}
+        for d in glob.glob(os.path.join(src, "fabric_*")):
+            c = os.path.basename(d)[len("fabric_"):]
+            per = counter_per_kernel(os.path.join(d, "rank" + r), c)
+            fab[c] = {k: sum(v) / len(v) for k, v in per.items() if "mix_kernel" in k and v}
+        rs["fabric_per_mix_launch"] = fab
+        out["rank" + r] = rs
+    return out
+
+
+def main(src, dst, ranks=False):
+    out = {"source": src}
+    if ranks:
+        out["ranks"] = summarize_ranks(src)
+    else:
+        out.update(summarize(src))
+    out["note"] = "FETCH_SIZE x2 (gfx950 wide-read undercount), KiB -> bytes x1024"
     os.makedirs(os.path.dirname(dst), exist_ok=True)
     with open(dst, "w") as f:
         json.dump(out, f, indent=1)
-    top = sorted(kernels.items(), key=lambda kv: -kv[1]["pct"])[:6]
-    for k, v in top:
-        print(f"{v['pct']:6.2f}%  {v['avg_us']:10.2f} us  x{v['calls']:4d}  {k[:100]}")
-    print(json.dumps(mix, indent=1))
+    for tag, rs in (out["ranks"].items() if ranks else [("", out)]):
+        top = sorted(rs["kernels"].items(), key=lambda kv: -kv[1]["pct"])[:6]
+        for k, v in top:
+            print(f"{tag} {v['pct']:6.2f}%  {v['avg_us']:10.2f} us  x{v['calls']:4d}  {k[:100]}")
+        print(tag, json.dumps(rs["mix_pmc"], indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    args = [a for a in sys.argv[1:] if a != "--ranks"]
+    main(args[0], args[1], ranks="--ranks" in sys.argv)
