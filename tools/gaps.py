@@ -22,21 +22,29 @@ import numpy as np
 
 
 def trace_gaps(path, K=20):
-    """All mixing launches of a kernel trace, and bench.py's timed region: the last K launches of
-    the headline kernel before the first launch of the self-check replay (the 64-column round
-    kernel, mix_kernel_rows<8, 256, ...>), which bench.py runs right after the timed rounds."""
+    """All mixing launches of a kernel trace, and bench.py's timed region: the first run of >= K
+    launches of the headline kernel with no event between them (gaps < 3 us) -- the warmup is
+    shorter than K and the settling blocks put an event pair around every launch, so the first
+    such run is the K timed rounds (the MATCHA figure's back-to-back rounds come later)."""
     allrows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
-    names = [r["Kernel_Name"] for r in allrows]
-    replay = [i for i, nm in enumerate(names) if "mix_kernel_rows<8, 256" in nm]
+    mixrows = [r for r in allrows if "mix_kernel" in r["Kernel_Name"]]
     timed = None
-    if replay:
-        before = [r for r in allrows[:replay[0]] if "mix_kernel" in r["Kernel_Name"]]
-        hk = before[-1]["Kernel_Name"] if before else None      # the timed rounds' kernel (whatever split)
-        head = [r for r in before if r["Kernel_Name"] == hk][-K:]
-        if len(head) == K:
-            st = np.array([int(r["Start_Timestamp"]) for r in head], np.int64)
-            en = np.array([int(r["End_Timestamp"]) for r in head], np.int64)
-            timed = {"launches": K, "kernel_us_mean": float(((en - st) / 1e3).mean()),
+    if mixrows:
+        hk = max({r["Kernel_Name"] for r in mixrows}, key=lambda nm: sum(r["Kernel_Name"] == nm for r in mixrows))
+        head = [r for r in mixrows if r["Kernel_Name"] == hk]
+        run = [head[0]]
+        for a, b in zip(head, head[1:]):
+            if (int(b["Start_Timestamp"]) - int(a["End_Timestamp"])) / 1e3 < 3.0:
+                run.append(b)
+                continue
+            if len(run) >= K:
+                break
+            run = [b]
+        if len(run) >= K:
+            run = run[:K]
+            st = np.array([int(r["Start_Timestamp"]) for r in run], np.int64)
+            en = np.array([int(r["End_Timestamp"]) for r in run], np.int64)
+            timed = {"launches": K, "kernel": hk[:80], "kernel_us_mean": float(((en - st) / 1e3).mean()),
                      "gaps_us": [round(float(g), 3) for g in (st[1:] - en[:-1]) / 1e3],
                      "span_us_per_round": float((en[-1] - st[0]) / 1e3 / K)}
     rows = [r for r in allrows if "mix_kernel" in r["Kernel_Name"]]
@@ -50,7 +58,7 @@ def trace_gaps(path, K=20):
                       "gap_us_p10_p90": [float(np.percentile(gap, 10)), float(np.percentile(gap, 90))] if len(gap) else None,
                       "gaps_counted": int(len(gap)), "timed_region": timed,
                       "note": "all mixing launches incl. per-round-event diagnostic blocks (events between "
-                              "launches) and the 64-column self-check replay; timed_region = bench.py's K "
+                              "launches) and the mixing-alone event timing; timed_region = bench.py's K "
                               "back-to-back rounds"}))
 
 

@@ -80,19 +80,21 @@ def summarize(src, trace="trace", fetch_dir="fetch", write_dir="write"):
 def summarize_ranks(src):
     """tools/profile_multi.sh layout: <pass>/rank<R>/... per rank (or, where this rocprofv3 did not
     expand %env{RANK}%, one directory per process id).  Per rank: the summary above, the RCCL kernels'
-    share of the trace, and every fabric counter pass (fabric_<COUNTER>/) summed per mixing launch."""
+    share of the trace, and the xGMI bytes per launch of every kernel (fabric_gmi/ pass)."""
     out = {}
     ranks = sorted({d.split("rank", 1)[1] for d in os.listdir(os.path.join(src, "trace")) if d.startswith("rank")})
     for r in ranks:
         rs = summarize(src, os.path.join("trace", "rank" + r), os.path.join("fetch_size", "rank" + r),
                        os.path.join("write_size", "rank" + r))
         rs["rccl_kernels"] = {k: v for k, v in rs["kernels"].items() if "nccl" in k.lower() or "rccl" in k.lower()}
+        # xGMI: 32-byte fabric requests to another GPU's memory, per launch of every kernel
         fab = {}
-        for d in glob.glob(os.path.join(src, "fabric_*")):
-            c = os.path.basename(d)[len("fabric_"):]
-            per = counter_per_kernel(os.path.join(d, "rank" + r), c)
-            fab[c] = {k: sum(v) / len(v) for k, v in per.items() if "mix_kernel" in k and v}
-        rs["fabric_per_mix_launch"] = fab
+        for c, what in (("TCC_EA0_RDREQ_GMI_32B_sum", "read"), ("TCC_EA0_WRREQ_WRITE_GMI_32B_sum", "write")):
+            per = counter_per_kernel(os.path.join(src, "fabric_gmi", "rank" + r), c)
+            for k, v in per.items():
+                if v:
+                    fab.setdefault(k, {"launches": len(v)})[f"xgmi_{what}_bytes_per_launch"] = 32 * sum(v) / len(v)
+        rs["xgmi_per_kernel"] = fab
         out["rank" + r] = rs
     return out
 
