@@ -364,7 +364,8 @@ __device__ Resolved resolve(const RowView& v, int64_t k, int stages) {
 // BAL: a wave's output offsets from ballots + mbcnt (one row: 117.5 -> 115.5 us per round) or from
 // shuffle scans (several rows: 650 vs 655 us with ballots, whose 64-bit masks spill SGPRs)
 // LOOP: candidate stores in a loop over the lane's kept elements (mx_topk_set "compact_store" 1)
-template <bool BAL, bool LOOP>
+// PF2: two whole chunks in flight per wave instead of one (a second register buffer, +32 VGPRs)
+template <bool BAL, bool LOOP, bool PF2 = false>
 __device__ void compact_run(const Rows& R, const RowView& v, int64_t S, double frac, int fallback, int64_t bx,
                             int64_t gx) {
     __shared__ uint32_t wtot[2][kWaves];
@@ -376,16 +377,21 @@ __device__ void compact_run(const Rows& R, const RowView& v, int64_t S, double f
     const f4* h4 = reinterpret_cast<const f4*>(v.xh);
     auto whole = [&](int64_t c) { return vec && (c + 1) * kChunk <= R.P; };
     f4 ax[4], ah[4];                               // raw loads of the next full chunk
-    auto issue = [&](int64_t c) {
+    f4 px[4], ph[4];                               // PF2: and of the one after
+    auto issue_to = [&](f4 (&X)[4], f4 (&H)[4], int64_t c) {
         const int64_t q0 = c * (kChunk / 4) + wave * kSubQuads + lane;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            ax[j] = __builtin_nontemporal_load(x4 + q0 + j * 64);
-            ah[j] = h4 ? __builtin_nontemporal_load(h4 + q0 + j * 64) : f4{0.0f, 0.0f, 0.0f, 0.0f};
+            X[j] = __builtin_nontemporal_load(x4 + q0 + j * 64);
+            H[j] = h4 ? __builtin_nontemporal_load(h4 + q0 + j * 64) : f4{0.0f, 0.0f, 0.0f, 0.0f};
         }
     };
+    auto issue = [&](int64_t c) { issue_to(ax, ah, c); };
     int64_t c = bx;
     if (c < nc && whole(c)) issue(c);              // the first chunk flies while b_lo is resolved
+    if constexpr (PF2) {
+        if (c + gx < nc && whole(c + gx)) issue_to(px, ph, c + gx);
+    }
 
     uint32_t b_lo = 0;
     if (!fallback) {
@@ -489,15 +495,43 @@ __device__ void compact_run(const Rows& R, const RowView& v, int64_t S, double f
         if (threadIdx.x == 0) kept += all;
         par ^= 1;
     };
-    for (; c < nfull; c += gx) {
-        float d[4][4];
+    if constexpr (PF2) {
         const int n[4] = {4, 4, 4, 4};
+        for (; c < nfull; c += 2 * gx) {
+            {
+                float d[4][4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+                for (int j = 0; j < 4; ++j)
 #pragma unroll
-            for (int e = 0; e < 4; ++e) d[j][e] = h4 ? __fsub_rn(ax[j][e], ah[j][e]) : ax[j][e];
-        if (c + gx < nfull) issue(c + gx);
-        step(c, d, n);
+                    for (int e = 0; e < 4; ++e) d[j][e] = h4 ? __fsub_rn(ax[j][e], ah[j][e]) : ax[j][e];
+                if (c + 2 * gx < nfull) issue_to(ax, ah, c + 2 * gx);
+                step(c, d, n);
+            }
+            if (c + gx >= nfull) {                 // the stride sequence's next chunk is past the whole ones
+                c += gx;
+                break;
+            }
+            {
+                float d[4][4];
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) d[j][e] = h4 ? __fsub_rn(px[j][e], ph[j][e]) : px[j][e];
+                if (c + 3 * gx < nfull) issue_to(px, ph, c + 3 * gx);
+                step(c + gx, d, n);
+            }
+        }
+    } else {
+        for (; c < nfull; c += gx) {
+            float d[4][4];
+            const int n[4] = {4, 4, 4, 4};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) d[j][e] = h4 ? __fsub_rn(ax[j][e], ah[j][e]) : ax[j][e];
+            if (c + gx < nfull) issue(c + gx);
+            step(c, d, n);
+        }
     }
     for (; c < nc; c += gx) {
         float d[4][4];
@@ -514,10 +548,10 @@ __device__ void compact_run(const Rows& R, const RowView& v, int64_t S, double f
     if (!fallback && threadIdx.x == 0 && kept) atomicAdd(&v.st->cand_n, (unsigned long long)kept);
 }
 
-template <bool BAL, bool LOOP>
+template <bool BAL, bool LOOP, bool PF2 = false>
 __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double frac) {
     const RowView v = row_view(R);
-    compact_run<BAL, LOOP>(R, v, S, frac, 0, blockIdx.x, gridDim.x);
+    compact_run<BAL, LOOP, PF2>(R, v, S, frac, 0, blockIdx.x, gridDim.x);
 }
 
 // Every block of this row's grid has arrived (rare path only: the fallback compaction inside the
@@ -1054,6 +1088,7 @@ int g_compact_blocks = 0;     // persistent compaction blocks over all rows; 0 =
 int g_sample_pieces = 1;      // sampled 1024-element pieces per wave (sample_kernel grid)
 int g_apply_pf = 1;           // apply pass: 1 message entries prefetched under the tile stream, 0 plain
 int g_apply_nt = -1;          // apply pass non-temporal accesses: -1 auto (only with several rows), 0, 1
+int g_compact_pf2 = 0;        // compaction: 1 = two whole chunks in flight per wave (PF2), 0 = one
 int g_compact_store = 1;      // compaction candidate stores: 1 (default) a loop over the lane's kept elements,
                               // 0 one masked store pair per (step, element) (same-box A/B: 8 rows 639 -> 632 us,
                               // one row 114.4 -> 113.2 us)
@@ -1110,6 +1145,11 @@ extern "C" int mx_topk_set(const char* key, int64_t value) {
         g_compact_store = (int)value;
         return MX_OK;
     }
+    if (!strcmp(key, "compact_pf2")) {
+        MX_CHECK(value == 0 || value == 1, "mx_topk_set: compact_pf2 %lld", (long long)value);
+        g_compact_pf2 = (int)value;
+        return MX_OK;
+    }
     if (!strcmp(key, "sample_pieces")) {
         MX_CHECK(value >= 1 && value <= 1024, "mx_topk_set: sample_pieces %lld", (long long)value);
         g_sample_pieces = (int)value;
@@ -1126,6 +1166,7 @@ extern "C" int64_t mx_topk_get(const char* key) {
     if (key && !strcmp(key, "apply_nt")) return g_apply_nt;
     if (key && !strcmp(key, "compact_store")) return g_compact_store;
     if (key && !strcmp(key, "apply_pf")) return g_apply_pf;
+    if (key && !strcmp(key, "compact_pf2")) return g_compact_pf2;
     mx::set_error("mx_topk_get: unknown key '%s'", key ? key : "(null)");
     return MX_ERR_INVALID;
 }
@@ -1167,8 +1208,10 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
     hipLaunchKernelGGL(kern, grid, dim3(tpb), 0, st, R, ##__VA_ARGS__);            \
     MX_LAUNCH_CHECK()
     MX_L(sample_kernel, dim3(sgrid, nrows), kTPB, S);
-    auto ck = nrows == 1 ? (g_compact_store ? compact_kernel<true, true> : compact_kernel<true, false>)
-                         : (g_compact_store ? compact_kernel<false, true> : compact_kernel<false, false>);
+    auto ck = nrows == 1 ? (g_compact_store ? (g_compact_pf2 ? compact_kernel<true, true, true> : compact_kernel<true, true>)
+                                            : compact_kernel<true, false>)
+                         : (g_compact_store ? (g_compact_pf2 ? compact_kernel<false, true, true> : compact_kernel<false, true>)
+                                            : compact_kernel<false, false>);
     MX_L(ck, dim3(bgrid, nrows), kTPB, S, frac);
     // the fallback compaction (S > 1, rare) runs inside the first candidate pass
     auto h10 = nrows == 1 ? (g_compact_store ? cand_hist<kMidBits, true, true> : cand_hist<kMidBits, true, false>)

@@ -83,11 +83,11 @@ def parse():
     ap.add_argument("--placement", choices=("auto", "contiguous"), default="auto",
                     help="N > 1: which workers share a GPU -- auto (placement.best_placement, fewest rows "
                          "over the busiest xGMI pair) or contiguous id blocks")
-    ap.add_argument("--figure-timeout", type=float, default=300.0, help="watchdog deadline per secondary "
+    ap.add_argument("--figure-timeout", type=float, default=240.0, help="watchdog deadline per secondary "
                     "figure (s): past it rank 0 prints the line so far with an error and every rank exits")
-    ap.add_argument("--figures-budget", type=float, default=900.0, help="total wall time for the secondary "
+    ap.add_argument("--figures-budget", type=float, default=600.0, help="total wall time for the secondary "
                     "figures (s); the ones left when it is spent are skipped")
-    ap.add_argument("--headline-timeout", type=float, default=900.0, help="watchdog deadline of the headline "
+    ap.add_argument("--headline-timeout", type=float, default=300.0, help="watchdog deadline of the headline "
                     "measurement (s)")
     ap.add_argument("--pg-timeout", type=float, default=1800.0, help="torch.distributed timeout (s), above "
                     "the watchdog's")
@@ -676,7 +676,9 @@ def er_figure(pkg, args, rank, world, comm, dev):
     P = int(-max_over_ranks(-float(P), world, dev))            # every rank runs the same P
     if P < 1024:
         raise RuntimeError(f"ER(64) leg: only {free / 2**30:.1f} GiB free on rank {rank}")
-    cand = [k for k in forms if fit[k] >= P]
+    # forms that fit at P on EVERY rank (free memory differs per GPU: agree, or the ranks would
+    # calibrate different forms and their collectives would not pair up)
+    cand = [k for k in forms if max_over_ranks(float(fit[k] < P), world, dev) == 0]
     cols = sample_columns(P)
     cols_dev = torch.from_numpy(cols).cuda()
     init = synth_columns(range(n), cols)

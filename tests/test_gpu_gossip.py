@@ -784,3 +784,36 @@ def test_choco_placement_loopback(pkg, O):
         for g in groups:
             got[g.workers] = g.rows.cpu().numpy()
         assert np.array_equal(got.view(np.uint32), X.view(np.uint32)), f"round {t}"
+
+
+@pytest.mark.parametrize("pattern", ["layers", "sampled_large", "ties", "gap", "coarse333"])
+@pytest.mark.parametrize("P", [2_000_001, 14_774_436])
+def test_topk_compaction_two_chunks_in_flight(pkg, O, P, pattern):
+    """The compaction with two whole chunks in flight per wave (mx_topk_set "compact_pf2" 1), one
+    row and (through ChocoWorkerGroup's batched rows) several: index sets and values equal the
+    oracle's, with the sampled-fallback pattern among them."""
+    ratio = 0.99
+    x = _topk_case(O, P, pattern)
+    k = O.topk_k(P, ratio)
+    ov, oi = O.topk_abs(x, k)
+    saved = int(pkg.lib.mx_topk_get(b"compact_pf2"))
+    pkg._lib.check(pkg.lib.mx_topk_set(b"compact_pf2", 1))
+    try:
+        v, i = pkg.get_top_k(torch.from_numpy(x).cuda(), ratio)
+        assert np.array_equal(i.cpu().numpy(), oi)
+        assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32))
+        if P < 3_000_000:                         # several rows in one launch
+            gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, 8, 4, True)
+            topo = Topo(gp.neighbors_info, 2 / 7, np.ones((2, 5), np.uint8))
+            grp = pkg.ChocoWorkerGroup(topo, numel=P, ratio=ratio, consensus_lr=0.1)
+            X = np.stack([x * np.float32(1 + r) for r in range(8)])
+            grp.rows.copy_(torch.from_numpy(X))
+            grp.compress(0)
+            torch.cuda.synchronize()
+            for r in range(8):
+                gv, gi = grp.message(r)
+                rv, ri = O.topk_abs(X[r], k)
+                assert np.array_equal(gi.cpu().numpy(), ri), r
+                assert np.array_equal(gv.cpu().numpy().view(np.uint32), rv.view(np.uint32)), r
+    finally:
+        pkg.lib.mx_topk_set(b"compact_pf2", saved)
