@@ -264,27 +264,37 @@ __global__ __launch_bounds__(kTPB) void sample_kernel(Rows R, int64_t S) {
         if (h[i]) atomicAdd(&v.hs[i], h[i]);
 }
 
-// Block-wide: the bin holding the need-th largest key of a finished histogram, scanning bins from
-// the top; *rem = rank of that key inside its bin.  bin 0 / rem = need - total when the histogram
-// holds fewer than `need` keys.  Read-only (every block of a kernel resolves the same answer),
-// so no separate one-block select launch sits between the passes.  Each thread loads its kPer
-// bins once (vector loads, kept in registers: the boundary search walks registers, not dependent
-// global loads), wave scans by shuffles, one barrier to combine the waves, one to publish.
+// A finished histogram's bins, kPer per thread, in registers (the boundary search walks registers,
+// not dependent global loads).
 template <int NBINS>
-__device__ void find_bin(const uint32_t* __restrict__ hist, int64_t need, int* bin, int64_t* rem,
-                         int64_t* total) {
-    constexpr int kPer = NBINS / kTPB;
+struct Bins {
+    static constexpr int kPer = NBINS / kTPB;
+    uint32_t c[kPer];                                    // bins NBINS-1-(t*kPer+j), top first
+};
+
+// this thread's kPer bins of a finished histogram (vector loads into registers)
+template <int NBINS>
+__device__ __forceinline__ void load_bins(const uint32_t* __restrict__ hist, Bins<NBINS>& b) {
+    const int t = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < Bins<NBINS>::kPer; ++j) b.c[j] = hist[NBINS - 1 - (t * Bins<NBINS>::kPer + j)];
+}
+
+// Block-wide, over bins already in registers: the bin holding the need-th largest key, scanning
+// bins from the top; *rem = rank of that key inside its bin.  bin 0 / rem = need - total when the
+// histogram holds fewer than `need` keys.  Read-only (every block of a kernel resolves the same
+// answer), so no separate one-block select launch sits between the passes.  Wave scans in DPP,
+// one barrier to combine the waves, one to publish.
+template <int NBINS>
+__device__ void scan_bins(const Bins<NBINS>& bs, int64_t need, int* bin, int64_t* rem, int64_t* total) {
+    constexpr int kPer = Bins<NBINS>::kPer;
     __shared__ int64_t wsum[kWaves];
     __shared__ int s_bin;
     __shared__ int64_t s_rem;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
-    uint32_t cnt[kPer];                                  // bins NBINS-1-(t*kPer+j), top first
     int64_t mine = 0;
 #pragma unroll
-    for (int j = 0; j < kPer; ++j) {
-        cnt[j] = hist[NBINS - 1 - (t * kPer + j)];
-        mine += cnt[j];
-    }
+    for (int j = 0; j < kPer; ++j) mine += bs.c[j];
     int64_t incl = wave_incl_scan64(mine);               // inclusive scan over the wave (DPP)
     if (lane == 63) wsum[wave] = incl;
     __syncthreads();
@@ -302,11 +312,11 @@ __device__ void find_bin(const uint32_t* __restrict__ hist, int64_t need, int* b
         int64_t r = 0;
 #pragma unroll
         for (int j = 0; j < kPer; ++j) {
-            if (b < 0 && acc + cnt[j] >= need) {
+            if (b < 0 && acc + bs.c[j] >= need) {
                 b = NBINS - 1 - (t * kPer + j);
                 r = need - acc;
             }
-            acc += cnt[j];
+            acc += bs.c[j];
         }
         s_bin = b;
         s_rem = r;
@@ -323,29 +333,52 @@ __device__ void find_bin(const uint32_t* __restrict__ hist, int64_t need, int* b
     __syncthreads();                                     // the shared answer may be reused
 }
 
+template <int NBINS>
+__device__ void find_bin(const uint32_t* __restrict__ hist, int64_t need, int* bin, int64_t* rem,
+                         int64_t* total) {
+    Bins<NBINS> bs;
+    load_bins<NBINS>(hist, bs);
+    scan_bins<NBINS>(bs, need, bin, rem, total);
+}
+
 // Threshold resolved so far from the finished candidate histograms: `stages` of 12 / 10 / 9 bits.
 struct Resolved {
     uint32_t prefix, mask;
     int64_t need;                                        // keys still to take at/below prefix
 };
 
+// Every histogram a stage will need is loaded up front -- the 12-bit one of both the first and the
+// fallback compaction (which one holds the candidates depends on the candidate count, itself a
+// load) -- so the stages cost one memory round trip, not one each; the scans follow in registers.
 __device__ Resolved resolve(const RowView& v, int64_t k, int stages) {
+    Bins<kTopBins> a12, f12;
+    Bins<1 << kMidBits> b10;
+    Bins<1 << kLowBits> b9;
+    const unsigned long long cand_n = v.st->cand_n;
+    load_bins<kTopBins>(v.h12, a12);
+    load_bins<kTopBins>(v.h12f, f12);
+    if (stages >= 2) load_bins<1 << kMidBits>(v.h10, b10);
+    if (stages >= 3) load_bins<1 << kLowBits>(v.h9, b9);
+    const bool fb = cand_n < (unsigned long long)k;      // the fallback pass ran for this row
+    if (fb) {
+#pragma unroll
+        for (int j = 0; j < Bins<kTopBins>::kPer; ++j) a12.c[j] = f12.c[j];
+    }
     Resolved z{0u, 0u, k};
     int b;
     int64_t rem, tot;
-    const bool fb = v.st->cand_n < (unsigned long long)k;   // the fallback pass ran for this row
-    find_bin<kTopBins>(fb ? v.h12f : v.h12, z.need, &b, &rem, &tot);
+    scan_bins<kTopBins>(a12, z.need, &b, &rem, &tot);
     z.prefix = (uint32_t)b << kTopShift;
     z.mask = 0xfffu << kTopShift;
     z.need = rem;
     if (stages >= 2) {
-        find_bin<1 << kMidBits>(v.h10, z.need, &b, &rem, &tot);
+        scan_bins<1 << kMidBits>(b10, z.need, &b, &rem, &tot);
         z.prefix |= (uint32_t)b << kMidShift;
         z.mask |= ((1u << kMidBits) - 1) << kMidShift;
         z.need = rem;
     }
     if (stages >= 3) {
-        find_bin<1 << kLowBits>(v.h9, z.need, &b, &rem, &tot);
+        scan_bins<1 << kLowBits>(b9, z.need, &b, &rem, &tot);
         z.prefix |= (uint32_t)b;
         z.mask = 0xffffffffu;
         z.need = rem;
@@ -552,6 +585,139 @@ template <bool BAL, bool LOOP, bool PF2 = false>
 __global__ __launch_bounds__(kTPB) void compact_kernel(Rows R, int64_t S, double frac) {
     const RowView v = row_view(R);
     compact_run<BAL, LOOP, PF2>(R, v, S, frac, 0, blockIdx.x, gridDim.x);
+}
+
+// The same pass with wave-owned chunks (mx_topk_set "compact_wave" 1): every wave streams whole
+// chunks of its own -- gw, gw + GW, ... (gw = the wave's index over the grid) -- in four
+// 1024-element sub-steps, each the 4 quads per lane of one wave step above, the next sub-step's
+// loads in flight while one is ranked.  A chunk's candidates are placed from the wave's own
+// running count, so the waves of a block never wait for each other (no barrier per chunk); they
+// share only the LDS histogram, flushed once at the end.  Output identical to compact_kernel's
+// (same regions, same index order, same counts and histograms).
+template <bool BAL>
+__global__ __launch_bounds__(kTPB) void compact_wave_kernel(Rows R, int64_t S, double frac) {
+    const RowView v = row_view(R);
+    __shared__ uint32_t h[kTopBins];
+    __shared__ uint32_t wk[kWaves];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int64_t nc = n_chunks(R.P);
+    const int64_t gw = (int64_t)blockIdx.x * kWaves + wave, GW = (int64_t)gridDim.x * kWaves;
+    const bool vec = (((uintptr_t)v.x | (uintptr_t)v.xh) & 15) == 0;
+    const f4* x4 = reinterpret_cast<const f4*>(v.x);
+    const f4* h4 = reinterpret_cast<const f4*>(v.xh);
+    const int64_t nfull = vec ? R.P / kChunk : 0;  // whole, aligned chunks: [0, nfull)
+    auto chunk_of = [&](int64_t s) { return gw + (s >> 2) * GW; };
+    f4 ax[4], ah[4];
+    auto issue = [&](int64_t s) {
+        const int64_t q0 = chunk_of(s) * (kChunk / 4) + (s & 3) * kSubQuads + lane;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            ax[j] = __builtin_nontemporal_load(x4 + q0 + j * 64);
+            ah[j] = h4 ? __builtin_nontemporal_load(h4 + q0 + j * 64) : f4{0.0f, 0.0f, 0.0f, 0.0f};
+        }
+    };
+    int64_t s = 0;
+    if (chunk_of(0) < nfull) issue(0);             // in flight while b_lo is resolved
+    uint32_t b_lo = 0;
+    {
+        int64_t want = R.k;
+        if (S > 1) {
+            const double e = (double)R.k * frac;
+            want = (int64_t)ceil(1.25 * e + 4.0 * sqrt(e) + 16.0);
+        }
+        int b;
+        int64_t rem, tot;
+        find_bin<kTopBins>(v.hs, want, &b, &rem, &tot);
+        b_lo = tot < want ? 0u : (uint32_t)b;
+        if (blockIdx.x == 0 && threadIdx.x == 0) v.st->b0 = b_lo;
+    }
+    const int h0 = (int)(b_lo & ~(uint32_t)(kTPB - 1));
+    for (int i = h0 + threadIdx.x; i < kTopBins; i += kTPB) h[i] = 0;
+    __syncthreads();
+    uint32_t run = 0, kept = 0;                    // the current chunk's candidates so far / the wave's
+    auto sub = [&](int64_t s, float (&d)[4][4], const int (&n)[4]) {
+        const int64_t c = chunk_of(s);
+        const int u = (int)(s & 3);
+        uint32_t keep = 0, ex[4], wt[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            ex[j] = 0;
+            wt[j] = 0;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const uint32_t dg = key_of(d[j][e]) >> kTopShift;
+                const bool f = e < n[j] && dg >= b_lo;
+                keep |= (f ? 1u : 0u) << (4 * j + e);
+                if constexpr (BAL) {
+                    const uint64_t b = __ballot(f);
+                    ex[j] += lanes_below(b);
+                    wt[j] += (uint32_t)__popcll(b);
+                } else {
+                    ex[j] += f;
+                }
+                if (f) atomicAdd(&h[dg], 1u);
+            }
+            if constexpr (!BAL) {
+                const uint32_t incl = wave_incl_scan(ex[j]);
+                wt[j] = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                ex[j] = incl - ex[j];
+            }
+        }
+        float* cv = v.cval + c * kCvLd;
+        uint16_t* cl = v.cloc + c * kClLd;
+        uint32_t base[4], pos = run;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            base[j] = pos + ex[j];
+            pos += wt[j];
+        }
+        for (uint32_t rem = keep; rem; rem &= rem - 1) {
+            const int b = __builtin_ctz(rem);
+            const int j = b >> 2;
+            float val = d[0][0];
+            uint32_t bj = base[0];
+#pragma unroll
+            for (int t = 1; t < 16; ++t) val = b == t ? d[t >> 2][t & 3] : val;
+#pragma unroll
+            for (int t = 1; t < 4; ++t) bj = j == t ? base[t] : bj;
+            const uint32_t p = bj + __popc(keep & ((1u << b) - 1) & (0xfu << (4 * j)));
+            cv[p] = val;
+            cl[p] = (uint16_t)(kSub * u + 4 * (64 * j + lane) + (b & 3));
+        }
+        run = pos;
+        if (u == 3) {                              // the chunk is complete: its whole record
+            if (lane < kRec) v.cnt[kRec * c + lane] = lane == 3 ? run : 0;
+            kept += run;
+            run = 0;
+        }
+    };
+    for (; chunk_of(s) < nfull; ++s) {
+        float d[4][4];
+        const int n[4] = {4, 4, 4, 4};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) d[j][e] = h4 ? __fsub_rn(ax[j][e], ah[j][e]) : ax[j][e];
+        if (chunk_of(s + 1) < nfull) issue(s + 1);
+        sub(s, d, n);
+    }
+    for (; chunk_of(s) < nc; ++s) {                // partial / unaligned chunks
+        float d[4][4];
+        int n[4];
+        const int64_t q0 = chunk_of(s) * (kChunk / 4) + (s & 3) * kSubQuads;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) n[j] = load_quad(v.x, v.xh, q0 + j * 64 + lane, R.P, vec, d[j]);
+        sub(s, d, n);
+    }
+    if (lane == 0) wk[wave] = kept;
+    __syncthreads();
+    for (int i = h0 + threadIdx.x; i < kTopBins; i += kTPB)
+        if (h[i]) atomicAdd(&v.h12[i], h[i]);
+    if (threadIdx.x == 0) {
+        uint32_t all = 0;
+        for (int w = 0; w < kWaves; ++w) all += wk[w];
+        if (all) atomicAdd(&v.st->cand_n, (unsigned long long)all);
+    }
 }
 
 // Every block of this row's grid has arrived (rare path only: the fallback compaction inside the
@@ -1088,6 +1254,8 @@ int g_compact_blocks = 0;     // persistent compaction blocks over all rows; 0 =
 int g_sample_pieces = 1;      // sampled 1024-element pieces per wave (sample_kernel grid)
 int g_apply_pf = 1;           // apply pass: 1 message entries prefetched under the tile stream, 0 plain
 int g_apply_nt = -1;          // apply pass non-temporal accesses: -1 auto (only with several rows), 0, 1
+int g_compact_wave = 0;       // compaction with wave-owned chunks: 0 = off (block-owned chunks), c > 0 = about
+                              // c chunks per wave
 int g_compact_pf2 = 0;        // compaction: 1 = two whole chunks in flight per wave (PF2), 0 = one
 int g_compact_store = 1;      // compaction candidate stores: 1 (default) a loop over the lane's kept elements,
                               // 0 one masked store pair per (step, element) (same-box A/B: 8 rows 639 -> 632 us,
@@ -1145,6 +1313,11 @@ extern "C" int mx_topk_set(const char* key, int64_t value) {
         g_compact_store = (int)value;
         return MX_OK;
     }
+    if (!strcmp(key, "compact_wave")) {
+        MX_CHECK(value >= 0 && value <= 1024, "mx_topk_set: compact_wave %lld", (long long)value);
+        g_compact_wave = (int)value;
+        return MX_OK;
+    }
     if (!strcmp(key, "compact_pf2")) {
         MX_CHECK(value == 0 || value == 1, "mx_topk_set: compact_pf2 %lld", (long long)value);
         g_compact_pf2 = (int)value;
@@ -1167,6 +1340,7 @@ extern "C" int64_t mx_topk_get(const char* key) {
     if (key && !strcmp(key, "compact_store")) return g_compact_store;
     if (key && !strcmp(key, "apply_pf")) return g_apply_pf;
     if (key && !strcmp(key, "compact_pf2")) return g_compact_pf2;
+    if (key && !strcmp(key, "compact_wave")) return g_compact_wave;
     mx::set_error("mx_topk_get: unknown key '%s'", key ? key : "(null)");
     return MX_ERR_INVALID;
 }
@@ -1212,7 +1386,15 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
                                             : compact_kernel<true, false>)
                          : (g_compact_store ? (g_compact_pf2 ? compact_kernel<false, true, true> : compact_kernel<false, true>)
                                             : compact_kernel<false, false>);
-    MX_L(ck, dim3(bgrid, nrows), kTPB, S, frac);
+    if (g_compact_wave) {
+        // wave-owned chunks: about g_compact_wave chunks per wave (1 = one chunk each)
+        const int64_t waves = (nc + g_compact_wave - 1) / g_compact_wave;
+        const unsigned wg = clamp_grid(waves, kWaves, 65535);
+        auto cw = nrows == 1 ? compact_wave_kernel<true> : compact_wave_kernel<false>;
+        MX_L(cw, dim3(wg, nrows), kTPB, S, frac);
+    } else {
+        MX_L(ck, dim3(bgrid, nrows), kTPB, S, frac);
+    }
     // the fallback compaction (S > 1, rare) runs inside the first candidate pass
     auto h10 = nrows == 1 ? (g_compact_store ? cand_hist<kMidBits, true, true> : cand_hist<kMidBits, true, false>)
                           : (g_compact_store ? cand_hist<kMidBits, false, true> : cand_hist<kMidBits, false, false>);

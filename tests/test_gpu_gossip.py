@@ -786,18 +786,21 @@ def test_choco_placement_loopback(pkg, O):
         assert np.array_equal(got.view(np.uint32), X.view(np.uint32)), f"round {t}"
 
 
+@pytest.mark.parametrize("knob", [("compact_pf2", 1), ("compact_wave", 1), ("compact_wave", 3)])
 @pytest.mark.parametrize("pattern", ["layers", "sampled_large", "ties", "gap", "coarse333"])
 @pytest.mark.parametrize("P", [2_000_001, 14_774_436])
-def test_topk_compaction_two_chunks_in_flight(pkg, O, P, pattern):
-    """The compaction with two whole chunks in flight per wave (mx_topk_set "compact_pf2" 1), one
-    row and (through ChocoWorkerGroup's batched rows) several: index sets and values equal the
-    oracle's, with the sampled-fallback pattern among them."""
+def test_topk_compaction_variants(pkg, O, P, pattern, knob):
+    """The compaction variants -- two whole chunks in flight per wave ("compact_pf2" 1), wave-owned
+    chunks ("compact_wave" c: about c chunks per wave) -- one row and (through ChocoWorkerGroup's
+    batched rows) several: index sets and values equal the oracle's, the sampled-fallback pattern
+    among them."""
     ratio = 0.99
     x = _topk_case(O, P, pattern)
     k = O.topk_k(P, ratio)
     ov, oi = O.topk_abs(x, k)
-    saved = int(pkg.lib.mx_topk_get(b"compact_pf2"))
-    pkg._lib.check(pkg.lib.mx_topk_set(b"compact_pf2", 1))
+    key, val = knob[0].encode(), knob[1]
+    saved = int(pkg.lib.mx_topk_get(key))
+    pkg._lib.check(pkg.lib.mx_topk_set(key, val))
     try:
         v, i = pkg.get_top_k(torch.from_numpy(x).cuda(), ratio)
         assert np.array_equal(i.cpu().numpy(), oi)
@@ -816,4 +819,4 @@ def test_topk_compaction_two_chunks_in_flight(pkg, O, P, pattern):
                 assert np.array_equal(gi.cpu().numpy(), ri), r
                 assert np.array_equal(gv.cpu().numpy().view(np.uint32), rv.view(np.uint32)), r
     finally:
-        pkg.lib.mx_topk_set(b"compact_pf2", saved)
+        pkg.lib.mx_topk_set(key, saved)
