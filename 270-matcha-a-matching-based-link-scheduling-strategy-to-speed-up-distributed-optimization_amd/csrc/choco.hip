@@ -54,10 +54,11 @@ constexpr int kHistWords = 3 * kTopBins + (1 << kMidBits) + (1 << kLowBits);   /
 
 struct SelState {
     uint32_t b0;          // lowest top digit kept as a candidate (b_lo)
-    uint32_t T;           // exact threshold key (cand_mark)
-    int64_t need;         // ties of T to take (cand_mark)
+    uint32_t T;           // exact threshold key (cand_mark / select_kernel)
+    int64_t need;         // ties of T to take (cand_mark / select_kernel)
     unsigned long long cand_n;   // candidates kept by the first compact_kernel pass (zero on entry)
-    uint32_t bar;         // arrivals at the fallback's row barrier (zero on entry)
+    uint32_t bar;         // arrivals at the row's grid barriers (zeroed by the compaction pass)
+    uint32_t err;         // sticky: a row barrier's bounded wait expired (select_kernel)
 };
 
 // Per-chunk counters and per-block totals are 64-byte records, each written whole by one store
@@ -71,8 +72,13 @@ constexpr int kCvLd = kChunk + 64;           // floats per value region
 constexpr int kClLd = kChunk + 128;          // uint16 per index region
 
 struct WorkLayout {
-    size_t hist, state, cnt, bt, cval, cloc, total;
+    size_t hist, state, cnt, bt, cval, cloc, pub, total;
 };
+
+// select_kernel's per-block published histograms (one row: kSelMaxB blocks at most)
+constexpr int kSelMaxB = 32;
+constexpr int kPub10 = 1 << kMidBits;            // words per block: its 10-bit histogram
+constexpr int kPub9 = (1 << kLowBits) + 16;      // its 9-bit histogram, then its count above the 22-bit prefix
 
 __host__ __device__ inline int64_t n_chunks(int64_t P) { return (P + kChunk - 1) / kChunk; }
 __host__ __device__ inline int64_t n_subs(int64_t P) { return (P + kSub - 1) / kSub; }
@@ -86,7 +92,8 @@ __host__ __device__ inline WorkLayout layout(int64_t P) {
     w.bt = w.cnt + sizeof(int64_t) * kRec * (size_t)nc;           // cand_mark block totals (<= nc blocks)
     w.cval = (w.bt + sizeof(int64_t) * kRec * (size_t)nc + 255) / 256 * 256;
     w.cloc = w.cval + sizeof(float) * (size_t)nc * kCvLd;
-    w.total = (w.cloc + sizeof(uint16_t) * (size_t)nc * kClLd + 255) / 256 * 256;
+    w.pub = (w.cloc + sizeof(uint16_t) * (size_t)nc * kClLd + 255) / 256 * 256;
+    w.total = w.pub + sizeof(uint32_t) * (size_t)kSelMaxB * (kPub10 + kPub9);
     return w;
 }
 
@@ -121,8 +128,7 @@ struct RowView {
     int64_t* idx;
 };
 
-__device__ __forceinline__ RowView row_view(const Rows& R) {
-    const int r = blockIdx.y;
+__device__ __forceinline__ RowView row_view(const Rows& R, int r) {
     const WorkLayout w = layout(R.P);
     char* wb = R.work + (int64_t)r * R.work_ld;
     RowView v;
@@ -142,6 +148,8 @@ __device__ __forceinline__ RowView row_view(const Rows& R) {
     v.idx = reinterpret_cast<int64_t*>(R.out + (int64_t)r * R.out_ld + R.idx_off);
     return v;
 }
+
+__device__ __forceinline__ RowView row_view(const Rows& R) { return row_view(R, blockIdx.y); }
 
 __device__ __forceinline__ uint32_t key_of(float d) { return __float_as_uint(d) & 0x7fffffffu; }
 
@@ -238,16 +246,15 @@ __device__ __forceinline__ int64_t lane63(int64_t v) {
     return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
-// ---- S: top-digit histogram over every S-th 1024-element piece, one wave per sampled piece
-__global__ __launch_bounds__(kTPB) void sample_kernel(Rows R, int64_t S) {
-    const RowView v = row_view(R);
-    __shared__ uint32_t h[kTopBins];
+// ---- S: top-digit histogram over every S-th 1024-element piece, one wave per sampled piece;
+// this block takes pieces (bx + i gx) * kWaves + wave into its LDS histogram h (zeroed here)
+__device__ __forceinline__ void sample_into(const Rows& R, const RowView& v, int64_t S, int64_t bx, int64_t gx, uint32_t* h) {
     for (int i = threadIdx.x; i < kTopBins; i += kTPB) h[i] = 0;
     __syncthreads();
     const bool vec = (((uintptr_t)v.x | (uintptr_t)v.xh) & 15) == 0;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int64_t nsamp = (n_subs(R.P) + S - 1) / S;
-    for (int64_t u = (int64_t)blockIdx.x * kWaves + wave; u < nsamp; u += (int64_t)gridDim.x * kWaves) {
+    for (int64_t u = bx * kWaves + wave; u < nsamp; u += gx * kWaves) {
         const int64_t q0 = u * S * kSubQuads;
         float d[4][4];
         int n[4];
@@ -260,24 +267,64 @@ __global__ __launch_bounds__(kTPB) void sample_kernel(Rows R, int64_t S) {
                 if (c < n[j]) atomicAdd(&h[key_of(d[j][c]) >> kTopShift], 1u);
     }
     __syncthreads();
+}
+
+__global__ __launch_bounds__(kTPB) void sample_kernel(Rows R, int64_t S) {
+    const RowView v = row_view(R);
+    __shared__ uint32_t h[kTopBins];
+    sample_into(R, v, S, blockIdx.x, gridDim.x, h);
     for (int i = threadIdx.x; i < kTopBins; i += kTPB)
         if (h[i]) atomicAdd(&v.hs[i], h[i]);
 }
 
+typedef __attribute__((address_space(1))) uint32_t g_u32;
+
+__device__ __forceinline__ void st_sc1(uint32_t* p, uint32_t v) {
+    __hip_atomic_store((g_u32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
+    return __hip_atomic_load((g_u32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr uint64_t kSpinTicks = 1ull << 28;    // ~2.7 s of the 100 MHz constant clock
+
+// block-uniform values the compiler cannot prove uniform (they come through LDS): into SGPRs
+__device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ int64_t uni(int64_t x) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)((uint64_t)x >> 32));
+    return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+// one thread: poll a counter (`sc1` loads) until `target`; false when the bounded wait expired
+__device__ __forceinline__ bool wait_count(const uint32_t* ctr, uint32_t target) {
+    const uint64_t t0 = wall_clock64();
+    while (ld_sc1(ctr) < target) {
+        __builtin_amdgcn_s_sleep(2);
+        if ((uint64_t)wall_clock64() - t0 > kSpinTicks) return false;
+    }
+    return true;
+}
+
 // A finished histogram's bins, kPer per thread, in registers (the boundary search walks registers,
-// not dependent global loads).
-template <int NBINS>
+// not dependent global loads).  With fewer bins than threads, thread t holds bin NBINS-1-t (threads
+// past NBINS hold empty bins).
+template <int NBINS, int TPB = kTPB>
 struct Bins {
-    static constexpr int kPer = NBINS / kTPB;
+    static constexpr int kPer = NBINS >= TPB ? NBINS / TPB : 1;
     uint32_t c[kPer];                                    // bins NBINS-1-(t*kPer+j), top first
 };
 
 // this thread's kPer bins of a finished histogram (vector loads into registers)
-template <int NBINS>
-__device__ __forceinline__ void load_bins(const uint32_t* __restrict__ hist, Bins<NBINS>& b) {
+template <int NBINS, int TPB = kTPB>
+__device__ __forceinline__ void load_bins(const uint32_t* __restrict__ hist, Bins<NBINS, TPB>& b) {
     const int t = threadIdx.x;
+    constexpr int kPer = Bins<NBINS, TPB>::kPer;
 #pragma unroll
-    for (int j = 0; j < Bins<NBINS>::kPer; ++j) b.c[j] = hist[NBINS - 1 - (t * Bins<NBINS>::kPer + j)];
+    for (int j = 0; j < kPer; ++j) {
+        if constexpr (NBINS >= TPB) b.c[j] = hist[NBINS - 1 - (t * kPer + j)];   // unpredicated: vector loads
+        else b.c[j] = t < NBINS ? hist[NBINS - 1 - t] : 0u;
+    }
 }
 
 // Block-wide, over bins already in registers: the bin holding the need-th largest key, scanning
@@ -285,10 +332,11 @@ __device__ __forceinline__ void load_bins(const uint32_t* __restrict__ hist, Bin
 // histogram holds fewer than `need` keys.  Read-only (every block of a kernel resolves the same
 // answer), so no separate one-block select launch sits between the passes.  Wave scans in DPP,
 // one barrier to combine the waves, one to publish.
-template <int NBINS>
-__device__ void scan_bins(const Bins<NBINS>& bs, int64_t need, int* bin, int64_t* rem, int64_t* total) {
-    constexpr int kPer = Bins<NBINS>::kPer;
-    __shared__ int64_t wsum[kWaves];
+template <int NBINS, int TPB = kTPB>
+__device__ void scan_bins(const Bins<NBINS, TPB>& bs, int64_t need, int* bin, int64_t* rem, int64_t* total) {
+    constexpr int kPer = Bins<NBINS, TPB>::kPer;
+    constexpr int kW = TPB / 64;
+    __shared__ int64_t wsum[kW];
     __shared__ int s_bin;
     __shared__ int64_t s_rem;
     const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
@@ -300,7 +348,7 @@ __device__ void scan_bins(const Bins<NBINS>& bs, int64_t need, int* bin, int64_t
     __syncthreads();
     int64_t base = 0, tot = 0;
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w) {
+    for (int w = 0; w < kW; ++w) {
         base += w < wave ? wsum[w] : 0;
         tot += wsum[w];
     }
@@ -437,7 +485,10 @@ __device__ void compact_run(const Rows& R, const RowView& v, int64_t S, double f
         int64_t rem, tot;
         find_bin<kTopBins>(v.hs, want, &b, &rem, &tot);
         b_lo = tot < want ? 0u : (uint32_t)b;               // too few sampled keys: keep everything
-        if (bx == 0 && threadIdx.x == 0) v.st->b0 = b_lo;
+        if (bx == 0 && threadIdx.x == 0) {
+            v.st->b0 = b_lo;
+            v.st->bar = 0;                                  // the selection's row barriers start here
+        }
     }
     // only digits >= b_lo are ever counted: zero and flush just those bins (b_lo is near the top)
     const int h0 = (int)(b_lo & ~(uint32_t)(kTPB - 1));
@@ -629,7 +680,10 @@ __global__ __launch_bounds__(kTPB) void compact_wave_kernel(Rows R, int64_t S, d
         int64_t rem, tot;
         find_bin<kTopBins>(v.hs, want, &b, &rem, &tot);
         b_lo = tot < want ? 0u : (uint32_t)b;
-        if (blockIdx.x == 0 && threadIdx.x == 0) v.st->b0 = b_lo;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            v.st->b0 = b_lo;
+            v.st->bar = 0;
+        }
     }
     const int h0 = (int)(b_lo & ~(uint32_t)(kTPB - 1));
     for (int i = h0 + threadIdx.x; i < kTopBins; i += kTPB) h[i] = 0;
@@ -957,6 +1011,450 @@ __global__ __launch_bounds__(kTPB) void write_cand(Rows R, int64_t G) {
     }
 }
 
+// ---- D: the whole selection after the compaction in ONE launch (mx_topk_set "select" 1): the work
+// of cand_hist<10>, cand_hist<9>, cand_mark and write_cand by B blocks of 1024 threads per row (one
+// per CU) that meet at two row barriers instead of three kernel boundaries, with every candidate
+// read from memory once.
+//   load   the block's contiguous chunk regions [cb, ce) -- wave w owns chunks cb + w + 16 i -- the
+//          first 128 candidates of each of up to kSelRC regions per wave cached in LDS; the 12-bit
+//          candidate histogram resolved (bin b12, rank need1) while they fly
+//   pass 1 10-bit digits (bits 9..18) of the candidates in bin b12 -> the block's histogram,
+//          published to its slot (`sc1` stores); barrier 1; every block sums the B slots (`sc1`
+//          loads) and resolves bin b10, rank need2
+//   pass 2 9-bit digits of the candidates matching the 22-bit prefix -> the block's histogram, and
+//          its count of keys above the prefix; barrier 2; every block sums the slots -> the exact
+//          threshold key T and the ties to take, and from the slots of the blocks before it, its
+//          own output base (keys > T and ties before its first chunk)
+//   write  the counts > T / == T of every chunk, one block-wide scan in chunk order, then every
+//          region's selected candidates in index order and its tile bound (write_cand's loop)
+// Measured (tools/select_trace.py stage clocks, one row of the VGG-16 share, 29 blocks): load +
+// 12-bit resolve 5.2 us, pass 1 1.6, barrier 1.8, 10-bit sums 2.6, pass 2 2.2, barrier 2.4, bases
+// 3.3, write 7.6: 26.7 us, about the four passes' own kernel time (27.6 us), and the rounds are
+// slower (one row 100.6 -> 103.9 us, 8 rows 608 -> 638 us, same box): the row's work sits on 29
+// CUs instead of the whole chip, and each barrier costs what a kernel boundary does.  Not the
+// default (mx_topk_set "select" 1 selects it); kept tested as the measured answer to "one launch".
+// Hand-off protocol (MI355X_MICROARCH.md, "Valid forms", table row 1): the published words are
+// `sc1` stores, every storing wave waits `vmcnt(0)`, a workgroup barrier, then one lane's agent-scope
+// add to the row's counter; the consumer polls it with an `sc1` load, a workgroup barrier, then
+// `sc1` loads of the slots; one workgroup per CU (the launch's LDS holds the CU).  The rare
+// sampled-floor fallback (fewer than k candidates kept) re-compacts every key here, by these blocks,
+// behind a fenced row barrier.  Every wait is bounded (the row's `err` word is set on expiry: the
+// output is then undefined, never a hang); the row's blocks are co-resident (the host launches at
+// most half the chip's CUs' worth of blocks at once).
+constexpr int kSelTPB = 1024;
+constexpr int kSelWaves = kSelTPB / 64;
+constexpr int kSelRC = 8;                      // chunk regions per wave cached in LDS (128 candidates each)
+// thread 0: poll the row's arrival counter until `target` (bounded: the row's error word is set)
+__device__ __forceinline__ void spin_until(SelState* st, uint32_t target) {
+    if (!wait_count(&st->bar, target)) st_sc1(&st->err, 1u);
+}
+
+// after this block's `sc1` publishing stores: arrive, wait for the row's other blocks
+__device__ __forceinline__ void sel_barrier(SelState* st, uint32_t target) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add((g_u32*)&st->bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        spin_until(st, target);
+    }
+    __syncthreads();
+}
+
+// after plain stores (the fallback compaction): release, arrive, wait, acquire
+__device__ __forceinline__ void sel_barrier_fenced(SelState* st, uint32_t target) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_fetch_add((g_u32*)&st->bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        spin_until(st, target);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+}
+
+// block-wide sum of one value per thread (all threads receive it)
+__device__ __forceinline__ int64_t sel_block_sum(int64_t x) {
+    __shared__ int64_t part[kSelWaves];
+    x = wave_sum64(x);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = x;
+    __syncthreads();
+    int64_t s = 0;
+#pragma unroll
+    for (int w = 0; w < kSelWaves; ++w) s += part[w];
+    __syncthreads();
+    return s;
+}
+
+__global__ __launch_bounds__(kSelTPB) void select_kernel(Rows R, int row0, int B, int64_t S, int trace) {
+    // the launch's LDS caches the first 128 candidates of each of the wave's first kSelRC regions
+    // (each wave reads back only its own regions: no barrier between a fill and its reads); its
+    // size also holds the CU for this one workgroup
+    extern __shared__ uint32_t sel_lds[];
+    float* lv = reinterpret_cast<float*>(sel_lds);                           // [kSelRC][16][128]
+    uint16_t* ll = reinterpret_cast<uint16_t*>(lv + kSelRC * kSelWaves * 128);   // the same, locations
+    __shared__ int cnl[kSelRC][kSelWaves];
+    const int r = row0 + (int)blockIdx.y;
+    const RowView v = row_view(R, r);
+    uint32_t* pub10 = reinterpret_cast<uint32_t*>(R.work + (int64_t)r * R.work_ld + layout(R.P).pub);
+    uint32_t* pub9 = pub10 + kSelMaxB * kPub10;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // mx_topk_set("select_trace", 1): thread 0 of every block stores the constant clock at the stage
+    // boundaries into the spare words of its 9-bit slot (a diagnostic; off by default)
+    auto stamp = [&](int i) {
+        if (trace && threadIdx.x == 0) pub9[blockIdx.x * kPub9 + (1 << kLowBits) + 1 + i] = (uint32_t)wall_clock64();
+    };
+    stamp(0);   // wave-uniform: region addresses in SGPRs
+    const int b = blockIdx.x;
+    const int64_t nc = n_chunks(R.P);
+    const int64_t G = (nc + B - 1) / B;
+    const int64_t cb = b * G < nc ? b * G : nc, ce = cb + G < nc ? cb + G : nc;
+    const int iters = (int)((ce - cb + kSelWaves - 1) / kSelWaves);
+    const int ncache = iters < kSelRC ? iters : kSelRC;
+    __shared__ uint32_t h[kTopBins];
+
+    // the wave's cached regions (speculative loads, all in flight together: a region is allocated
+    // whatever its count, dead regions alias the block's first)
+    auto load_cache = [&]() {
+        float a0[kSelRC], a1[kSelRC];
+        uint32_t l0[kSelRC], l1[kSelRC];
+        int n[kSelRC];
+#pragma unroll
+        for (int i = 0; i < kSelRC; ++i) {
+            const int64_t c = cb + (int64_t)i * kSelWaves + wave;
+            const bool live = i < ncache && c < ce;
+            const int64_t cc = live ? c : (cb < nc ? cb : 0);
+            n[i] = live ? (int)v.cnt[kRec * cc + 3] : 0;
+            a0[i] = v.cval[cc * kCvLd + lane];
+            a1[i] = v.cval[cc * kCvLd + 64 + lane];
+            l0[i] = v.cloc[cc * kClLd + lane];
+            l1[i] = v.cloc[cc * kClLd + 64 + lane];
+        }
+#pragma unroll
+        for (int i = 0; i < kSelRC; ++i) {
+            const int o = (i * kSelWaves + wave) * 128;
+            lv[o + lane] = a0[i];
+            lv[o + 64 + lane] = a1[i];
+            ll[o + lane] = (uint16_t)l0[i];
+            ll[o + 64 + lane] = (uint16_t)l1[i];
+            if (lane == 0) cnl[i][wave] = n[i];
+        }
+    };
+    load_cache();
+    const unsigned long long cand_n = v.st->cand_n;
+    Bins<kTopBins, kSelTPB> a12, f12;
+    load_bins<kTopBins, kSelTPB>(v.h12, a12);
+    load_bins<kTopBins, kSelTPB>(v.h12f, f12);
+    const bool fb = S > 1 && cand_n < (unsigned long long)R.k;   // row-uniform
+    uint32_t bar0 = 0;
+    if (fb) {
+        // keep every key of this block's chunks, in index order, digits into the fallback histogram
+        for (int i = tid; i < kTopBins; i += kSelTPB) h[i] = 0;
+        __syncthreads();
+        const bool vec = (((uintptr_t)v.x | (uintptr_t)v.xh) & 15) == 0;
+        for (int64_t c = cb; c < ce; ++c) {
+            for (int u = tid; u < kChunk / 4; u += kSelTPB) {
+                float d[4];
+                const int n = load_quad(v.x, v.xh, c * (kChunk / 4) + u, R.P, vec, d);
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    if (e < n) {
+                        v.cval[c * kCvLd + 4 * u + e] = d[e];
+                        v.cloc[c * kClLd + 4 * u + e] = (uint16_t)(4 * u + e);
+                        atomicAdd(&h[key_of(d[e]) >> kTopShift], 1u);
+                    }
+                }
+            }
+            const int64_t len = R.P - c * kChunk < kChunk ? R.P - c * kChunk : kChunk;
+            if (wave == 0 && lane < kRec) v.cnt[kRec * c + lane] = lane == 3 ? len : 0;
+        }
+        __syncthreads();
+        for (int i = tid; i < kTopBins; i += kSelTPB)
+            if (h[i]) atomicAdd(&v.h12f[i], h[i]);
+        bar0 = (uint32_t)B;
+        sel_barrier_fenced(v.st, bar0);
+        load_cache();
+        load_bins<kTopBins, kSelTPB>(v.h12f, f12);
+    }
+    // 12-bit stage (the compaction's histogram, or the fallback's)
+    int b12, b10, b9;
+    int64_t need, tot;
+    if (fb) {
+#pragma unroll
+        for (int j = 0; j < Bins<kTopBins, kSelTPB>::kPer; ++j) a12.c[j] = f12.c[j];
+    }
+    scan_bins<kTopBins, kSelTPB>(a12, R.k, &b12, &need, &tot);
+    b12 = uni(b12);
+    need = uni(need);
+    stamp(1);
+
+    // every candidate of the wave's i-th region, in 64-wide steps (cached ones from LDS)
+    auto region_of = [&](int i) { return cb + (int64_t)i * kSelWaves + wave; };
+    auto count_of = [&](int i) {
+        if (i < ncache) return cnl[i][wave];
+        const int64_t c = region_of(i);
+        return c < ce ? (int)v.cnt[kRec * c + 3] : 0;
+    };
+    auto val_of = [&](int i, int j) {
+        return i < ncache && j < 128 ? lv[(i * kSelWaves + wave) * 128 + j] : v.cval[region_of(i) * kCvLd + j];
+    };
+    auto loc_of = [&](int i, int j) {
+        return i < ncache && j < 128 ? (uint32_t)ll[(i * kSelWaves + wave) * 128 + j]
+                                     : (uint32_t)v.cloc[region_of(i) * kClLd + j];
+    };
+    // the cached regions' counts and both 64-wide slots, all read from LDS at once (one latency,
+    // not a chain per region; regions past ncache were cached with count 0); tails past 128 and
+    // uncached regions from memory
+    int rn[kSelRC];
+    float ra0[kSelRC], ra1[kSelRC];
+    auto read_cache = [&]() {
+#pragma unroll
+        for (int i = 0; i < kSelRC; ++i) {
+            const int o = (i * kSelWaves + wave) * 128;
+            rn[i] = cnl[i][wave];
+            ra0[i] = lv[o + lane];
+            ra1[i] = lv[o + 64 + lane];
+        }
+    };
+    auto for_regions = [&](auto&& f) {
+        read_cache();
+#pragma unroll
+        for (int i = 0; i < kSelRC; ++i) {
+            if (lane < rn[i]) f(ra0[i]);
+            if (64 + lane < rn[i]) f(ra1[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < kSelRC; ++i)
+            for (int j = 128 + lane; j < rn[i]; j += 64) f(v.cval[region_of(i) * kCvLd + j]);
+        for (int i = ncache; i < iters; ++i) {
+            const int64_t c = region_of(i);
+            const int n = c < ce ? (int)v.cnt[kRec * c + 3] : 0;
+            for (int j = lane; j < n; j += 64) f(v.cval[c * kCvLd + j]);
+        }
+    };
+
+    // pass 1: 10-bit digits of bin b12; keys above bin b12 counted
+    for (int i = tid; i < (1 << kMidBits); i += kSelTPB) h[i] = 0;
+    __syncthreads();
+    uint32_t gt = 0;
+    for_regions([&](float d) {
+        const uint32_t key = key_of(d);
+        const uint32_t dg = key >> kTopShift;
+        gt += dg > (uint32_t)b12;
+        if (dg == (uint32_t)b12) atomicAdd(&h[(key >> kMidShift) & ((1u << kMidBits) - 1)], 1u);
+    });
+    __syncthreads();
+    stamp(2);
+    for (int i = tid; i < kPub10; i += kSelTPB) st_sc1(&pub10[b * kPub10 + i], h[i]);
+    sel_barrier(v.st, bar0 + B);
+    stamp(3);
+    if (b == 0) {                                // nothing reads the 12-bit histograms or the
+        for (int i = tid; i < 3 * kTopBins; i += kSelTPB) v.hs[i] = 0;   // candidate total any more
+        if (tid == 0) v.st->cand_n = 0;
+    }
+    {
+        Bins<1 << kMidBits, kSelTPB> s10;        // thread t: bins 1023 - (2t + j), summed over the row's blocks
+        constexpr int kPer = Bins<1 << kMidBits, kSelTPB>::kPer;
+        uint32_t xs[kPer][kSelMaxB];             // every slot's load in flight at once (a summing loop
+#pragma unroll                                   // waits one round trip per slot)
+        for (int j = 0; j < kPer; ++j)
+#pragma unroll
+            for (int q = 0; q < kSelMaxB; ++q)
+                xs[j][q] = ld_sc1(&pub10[(q < B ? q : 0) * kPub10 + (1 << kMidBits) - 1 - (tid * kPer + j)]);
+#pragma unroll
+        for (int j = 0; j < kPer; ++j) {
+            uint32_t acc = 0;
+#pragma unroll
+            for (int q = 0; q < kSelMaxB; ++q) acc += q < B ? xs[j][q] : 0u;
+            s10.c[j] = acc;
+        }
+        scan_bins<1 << kMidBits, kSelTPB>(s10, need, &b10, &need, &tot);
+        b10 = uni(b10);
+        need = uni(need);
+    }
+    stamp(4);
+    const uint32_t pre22 = ((uint32_t)b12 << kMidBits) | (uint32_t)b10;   // key >> 9 of the prefix
+
+    // pass 2: 9-bit digits of the keys matching the 22-bit prefix; keys above it counted
+    for (int i = tid; i < (1 << kLowBits); i += kSelTPB) h[i] = 0;
+    __syncthreads();
+    for_regions([&](float d) {
+        const uint32_t key = key_of(d);
+        if ((key >> kTopShift) == (uint32_t)b12) {
+            const uint32_t hi = key >> kMidShift;
+            gt += hi > pre22;
+            if (hi == pre22) atomicAdd(&h[key & ((1u << kLowBits) - 1)], 1u);
+        }
+    });
+    const int64_t gt_blk = sel_block_sum(gt);  // its barriers also order the LDS histogram
+    stamp(5);
+    if (tid < (1 << kLowBits)) st_sc1(&pub9[b * kPub9 + tid], h[tid]);
+    if (tid == 0) st_sc1(&pub9[b * kPub9 + (1 << kLowBits)], (uint32_t)gt_blk);
+    sel_barrier(v.st, bar0 + 2 * B);
+    stamp(6);
+    int64_t base_gt, base_eq;
+    {
+        Bins<1 << kLowBits, kSelTPB> s9;         // thread t < 512: bin 511 - t
+        uint32_t all = 0, before = 0;
+        if (tid < (1 << kLowBits)) {
+            uint32_t xs[kSelMaxB];
+#pragma unroll
+            for (int q = 0; q < kSelMaxB; ++q) xs[q] = ld_sc1(&pub9[(q < B ? q : 0) * kPub9 + (1 << kLowBits) - 1 - tid]);
+#pragma unroll
+            for (int q = 0; q < kSelMaxB; ++q) {
+                all += q < B ? xs[q] : 0u;
+                before += q < b ? xs[q] : 0u;
+            }
+        }
+        s9.c[0] = all;
+        scan_bins<1 << kLowBits, kSelTPB>(s9, need, &b9, &need, &tot);
+        b9 = uni(b9);
+        need = uni(need);
+        const int bin = (1 << kLowBits) - 1 - tid;
+        int64_t g = tid < (1 << kLowBits) && bin > b9 ? before : 0;
+        if (tid < b) g += ld_sc1(&pub9[tid * kPub9 + (1 << kLowBits)]);
+        base_gt = uni(sel_block_sum(g));
+        base_eq = uni(sel_block_sum(tid < (1 << kLowBits) && bin == b9 ? before : 0));
+    }
+    stamp(7);
+    const uint32_t T = (pre22 << kMidShift) | (uint32_t)b9;
+    const int64_t need_eq = need;
+    if (b == 0 && tid == 0) {
+        v.st->T = T;
+        v.st->need = need_eq;
+    }
+
+    int32_t* bnd = R.bnd_off >= 0 ? reinterpret_cast<int32_t*>(R.out + (int64_t)r * R.out_ld + R.bnd_off) : nullptr;
+    // one 64-wide step of a chunk's candidates in index order: ties ranked, the selected placed
+    auto put = [&](int64_t c, float d, uint32_t loc, bool in, int64_t& run_out, int64_t& run_e) {
+        const uint32_t key = key_of(d);
+        const bool eq = in && key == T;
+        const uint64_t be = __ballot(eq);
+        const bool sel = in && (key > T || (eq && run_e + (int64_t)lanes_below(be) < need_eq));
+        const uint64_t bs = __ballot(sel);
+        const int64_t pos = run_out + lanes_below(bs);
+        if (sel && pos < R.k) {
+            v.vals[pos] = d;
+            v.idx[pos] = c * kChunk + loc;
+        }
+        run_out += __popcll(bs);
+        run_e += __popcll(be);
+    };
+    auto chunk_start = [&](int64_t c, int64_t gt_before, int64_t eq_before) {
+        const int64_t run_out = gt_before + (eq_before < need_eq ? eq_before : need_eq);
+        if (bnd && lane == 0) {
+            bnd[c] = (int32_t)(run_out < R.k ? run_out : R.k);
+            if (c == nc - 1) bnd[nc] = (int32_t)R.k;
+        }
+        return run_out;
+    };
+    if (iters <= kSelRC) {
+        // every chunk cached: counts > T / == T of all of them at once, ONE block-wide exclusive
+        // scan in chunk order (chunk cb + 16 i + w is entry 16 i + w), then every region placed
+        // independently of the others
+        __shared__ uint32_t sg[kSelRC * kSelWaves], se[kSelRC * kSelWaves];
+        read_cache();
+#pragma unroll
+        for (int i = 0; i < kSelRC; ++i) {
+            uint32_t g = (uint32_t)__popcll(__ballot(lane < rn[i] && key_of(ra0[i]) > T)) +
+                         (uint32_t)__popcll(__ballot(64 + lane < rn[i] && key_of(ra1[i]) > T));
+            uint32_t e = (uint32_t)__popcll(__ballot(lane < rn[i] && key_of(ra0[i]) == T)) +
+                         (uint32_t)__popcll(__ballot(64 + lane < rn[i] && key_of(ra1[i]) == T));
+            if (rn[i] > 128) {                       // a long region's tail (wave-uniform, rare)
+                uint32_t tg = 0, te = 0;
+                for (int j = 128 + lane; j < rn[i]; j += 64) {
+                    const uint32_t key = key_of(v.cval[region_of(i) * kCvLd + j]);
+                    tg += key > T;
+                    te += key == T;
+                }
+                g += (uint32_t)wave_sum64(tg);
+                e += (uint32_t)wave_sum64(te);
+            }
+            if (lane == 0) {
+                sg[i * kSelWaves + wave] = g;
+                se[i * kSelWaves + wave] = e;
+            }
+        }
+        __syncthreads();
+        static_assert(kSelRC * kSelWaves == 128, "one wave scans the block's chunk counts, two per lane");
+        if (wave == 0) {
+            const uint32_t g0 = sg[2 * lane], g1 = sg[2 * lane + 1], e0 = se[2 * lane], e1 = se[2 * lane + 1];
+            const uint32_t gx = wave_incl_scan(g0 + g1) - (g0 + g1), ex = wave_incl_scan(e0 + e1) - (e0 + e1);
+            sg[2 * lane] = gx;
+            sg[2 * lane + 1] = gx + g0;
+            se[2 * lane] = ex;
+            se[2 * lane + 1] = ex + e0;
+        }
+        __syncthreads();
+        // placement: everything it reads is in LDS (re-read per region rather than held across the
+        // scan); a long region's tail (rare) reads memory after its region's stores.  Nothing loaded
+        // from memory may still be in flight when the loop starts: the waitcnt pass would otherwise
+        // wait for every output store at the loop head (vmcnt counts stores too)
+        __builtin_amdgcn_s_waitcnt(0x0f70);      // vmcnt(0) (expcnt / lgkmcnt left alone)
+        for (int i = 0; i < ncache; ++i) {
+            const int64_t c = region_of(i);
+            if (c >= ce) continue;
+            const int o = (i * kSelWaves + wave) * 128;
+            const int n = cnl[i][wave];
+            int64_t run_e = base_eq + se[i * kSelWaves + wave];
+            int64_t run_out = chunk_start(c, base_gt + sg[i * kSelWaves + wave], run_e);
+            put(c, lv[o + lane], ll[o + lane], lane < n, run_out, run_e);
+            if (n > 64) put(c, lv[o + 64 + lane], ll[o + 64 + lane], 64 + lane < n, run_out, run_e);
+            for (int i0 = 128; i0 < n; i0 += 64) {
+                const bool in = i0 + lane < n;
+                put(c, in ? v.cval[c * kCvLd + i0 + lane] : 0.0f, in ? v.cloc[c * kClLd + i0 + lane] : 0u, in,
+                    run_out, run_e);
+            }
+        }
+    } else {
+        // more regions than cached: per 16 chunks (one per wave), counts scanned across the waves
+        __shared__ uint32_t xg[2][kSelWaves], xe[2][kSelWaves];
+        int64_t run_gt = base_gt, run_eq = base_eq;
+        int par = 0;
+        for (int it = 0; it < iters; ++it) {
+            const int64_t c = region_of(it);
+            const int n = count_of(it);
+            uint32_t g = 0, e = 0;
+            for (int j = lane; j < n; j += 64) {
+                const uint32_t key = key_of(val_of(it, j));
+                g += key > T;
+                e += key == T;
+            }
+            g = (uint32_t)wave_sum64(g);
+            e = (uint32_t)wave_sum64(e);
+            if (lane == 0) {
+                xg[par][wave] = g;
+                xe[par][wave] = e;
+            }
+            __syncthreads();
+            int64_t pg = 0, pe = 0, ag = 0, ae = 0;
+#pragma unroll
+            for (int w = 0; w < kSelWaves; ++w) {
+                pg += w < wave ? xg[par][w] : 0u;
+                pe += w < wave ? xe[par][w] : 0u;
+                ag += xg[par][w];
+                ae += xe[par][w];
+            }
+            if (c < ce) {
+                int64_t run_e = run_eq + pe;
+                int64_t run_out = chunk_start(c, run_gt + pg, run_e);
+                for (int i0 = 0; i0 < n; i0 += 64) {
+                    const int i = i0 + lane;
+                    const bool in = i < n;
+                    put(c, in ? val_of(it, i) : 0.0f, in ? loc_of(it, i) : 0u, in, run_out, run_e);
+                }
+            }
+            run_gt += ag;
+            run_eq += ae;
+            par ^= 1;
+        }
+    }
+    __syncthreads();
+    stamp(8);
+}
+
 // ------------------------------------------------------------------------------- apply
 // ChocoCommunicator.averaging (communicator.py:200-230) fused into one pass per state tile.
 // Row r's tile [t0, t0 + kTile) of s and x_hat is staged in LDS; every message that touches the
@@ -1265,6 +1763,29 @@ int g_cand_chunks = 0;        // chunk regions per wave of cand_hist / cand_mark
                               // flush of cand_hist<10>'s 1024 bins measured +3.7 us on one row; same-box
                               // sweep 2 -> 4 / 8: one row 121.7 -> 119.6 us, 8 rows 655 -> 640 us)
 
+int g_select = 0;             // selection after the compaction: 0 = the four passes (cand_hist<10>,
+                              // cand_hist<9>, cand_mark, write_cand), 1 = one launch (select_kernel; same-box
+                              // A/B: one row 100.6 -> 103.9 us, 8 rows 608 -> 638 us per round, not the default)
+int g_select_blocks = 0;      // select_kernel blocks per row; 0 = auto (every region cached, <= 32)
+int g_select_trace = 0;       // select_kernel stage clocks into the scratch (diagnostic)
+constexpr size_t kSelHoldBytes = (size_t)kSelRC * kSelWaves * 128 * 6;   // select_kernel's region cache (96 KB)
+
+// select_kernel blocks one launch may hold: half the chip's CUs (one block per CU; the rest of the
+// chip stays free for whatever else runs, so a row's blocks are always co-resident)
+int select_capacity() {
+    static int cached[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 64;
+    if (!cached[dev]) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 2) cus = 128;
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(select_kernel),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)kSelHoldBytes);
+        cached[dev] = cus / 2;
+    }
+    return cached[dev];
+}
+
 int64_t sample_stride(int64_t P) {
     const int64_t nc = n_chunks(P);
     int64_t S = g_sample_stride > 0 ? g_sample_stride : (nc * kChunk) / kSampleTarget;
@@ -1323,6 +1844,20 @@ extern "C" int mx_topk_set(const char* key, int64_t value) {
         g_compact_pf2 = (int)value;
         return MX_OK;
     }
+    if (!strcmp(key, "select")) {
+        MX_CHECK(value == 0 || value == 1, "mx_topk_set: select %lld", (long long)value);
+        g_select = (int)value;
+        return MX_OK;
+    }
+    if (!strcmp(key, "select_trace")) {
+        g_select_trace = value != 0;
+        return MX_OK;
+    }
+    if (!strcmp(key, "select_blocks")) {
+        MX_CHECK(value >= 0 && value <= kSelMaxB, "mx_topk_set: select_blocks %lld", (long long)value);
+        g_select_blocks = (int)value;
+        return MX_OK;
+    }
     if (!strcmp(key, "sample_pieces")) {
         MX_CHECK(value >= 1 && value <= 1024, "mx_topk_set: sample_pieces %lld", (long long)value);
         g_sample_pieces = (int)value;
@@ -1341,6 +1876,9 @@ extern "C" int64_t mx_topk_get(const char* key) {
     if (key && !strcmp(key, "apply_pf")) return g_apply_pf;
     if (key && !strcmp(key, "compact_pf2")) return g_compact_pf2;
     if (key && !strcmp(key, "compact_wave")) return g_compact_wave;
+    if (key && !strcmp(key, "select")) return g_select;
+    if (key && !strcmp(key, "select_blocks")) return g_select_blocks;
+    if (key && !strcmp(key, "select_trace")) return g_select_trace;
     mx::set_error("mx_topk_get: unknown key '%s'", key ? key : "(null)");
     return MX_ERR_INVALID;
 }
@@ -1371,7 +1909,7 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
         sampled += (P - c0 < kSub) ? P - c0 : kSub;
     }
     const double frac = (double)sampled / (double)P;
-    MX_CHECK(nc <= 0x7fffffff, "mx_topk_abs_diff_rows: P too large");
+    MX_CHECK(nc <= 0x7fffffff && P < ((int64_t)1 << 32), "mx_topk_abs_diff_rows: P too large (uint32 histograms)");
     const int cblocks = g_compact_blocks > 0 ? g_compact_blocks : (nrows == 1 ? 640 : 2560);
     const unsigned bgrid = clamp_grid(nc, 1, (cblocks + nrows - 1) / nrows);   // persistent
     const unsigned wgrid = (unsigned)((nc + kWaves - 1) / kWaves);          // one wave per chunk
@@ -1394,6 +1932,23 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
         MX_L(cw, dim3(wg, nrows), kTPB, S, frac);
     } else {
         MX_L(ck, dim3(bgrid, nrows), kTPB, S, frac);
+    }
+    if (g_select) {
+        // the fallback compaction (S > 1, rare) runs inside select_kernel; rows in batches of at
+        // most select_capacity() blocks per launch
+        // auto: the fewest blocks whose waves hold every region in the LDS cache (one row of the
+        // VGG-16 share: 29), at most kSelMaxB
+        int64_t Bw = g_select_blocks > 0 ? g_select_blocks : (nc + kSelRC * kSelWaves - 1) / (kSelRC * kSelWaves);
+        const int B = (int)(Bw > kSelMaxB ? kSelMaxB : Bw < 1 ? 1 : Bw);
+        const int cap = select_capacity();
+        const int rpl = cap / B > 0 ? cap / B : 1;
+        for (int r0 = 0; r0 < nrows; r0 += rpl) {
+            const int nr = nrows - r0 < rpl ? nrows - r0 : rpl;
+            hipLaunchKernelGGL(select_kernel, dim3((unsigned)B, (unsigned)nr), dim3(kSelTPB), kSelHoldBytes, st, R, r0,
+                               B, S, g_select_trace);
+            MX_LAUNCH_CHECK();
+        }
+        return MX_OK;
     }
     // the fallback compaction (S > 1, rare) runs inside the first candidate pass
     auto h10 = nrows == 1 ? (g_compact_store ? cand_hist<kMidBits, true, true> : cand_hist<kMidBits, true, false>)

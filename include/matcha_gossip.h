@@ -193,7 +193,13 @@ size_t mx_topk_work_bytes(int64_t P);
  * "apply_nt" = mx_choco_apply's access hints: -1 (default) non-temporal with several rows only,
  * 0 / 1 forced;
  * "apply_pf" = 1 (default): mx_choco_apply prefetches every message's tile bounds and first entries
- * under the tile stream, 0: the plain kernel (bounds and entries loaded per message).
+ * under the tile stream, 0: the plain kernel (bounds and entries loaded per message);
+ * "select" = 0 (default): the selection after the compaction as four passes (candidate histograms
+ * of the 10 and 9 low digits, threshold mark, placement), 1: as ONE launch (select_kernel: B
+ * workgroups of 1024 threads per row meeting at two row barriers; measured slower);
+ * "select_blocks" = select_kernel workgroups per row (0 = auto: the fewest whose LDS caches every
+ * candidate region, at most 32); "select_trace" = 1: select_kernel stores stage clocks in the
+ * scratch (diagnostic, tools/select_trace.py).
  * Knobs tune speed only, never results. */
 int mx_topk_set(const char* key, int64_t value);
 int64_t mx_topk_get(const char* key);

@@ -296,20 +296,25 @@ def test_topk_unaligned_input(pkg, O, pattern):
     assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32))
 
 
-def test_topk_work_reuse_and_tile_bounds(pkg, O):
+@pytest.mark.parametrize("select", [1, 0])
+def test_topk_work_reuse_and_tile_bounds(pkg, O, select):
     """One zero-filled scratch serves a sequence of calls of different P / k / patterns (incl. the
     fallback pass): each call leaves its histograms and counters zero (no zeroing launch runs),
     results stay exact, and the tile bounds the message carries are the index-range starts of
-    every 4096-element tile (what mx_choco_apply reads)."""
+    every 4096-element tile (what mx_choco_apply reads) -- with the one-launch selection and with
+    the four selection passes."""
     L = pkg.lib
     big = max(int(L.mx_topk_work_bytes(P)) for P in (2_000_001, 4097, 300_000))
     work = torch.zeros(big, dtype=torch.uint8, device="cuda")
     hist_bytes = 4 * (3 * 4096 + 1024 + 512)
+    saved = int(L.mx_topk_get(b"select"))
+    pkg._lib.check(L.mx_topk_set(b"select", select))
     pkg._lib.check(L.mx_topk_set(b"sample_stride", 16))      # sampled_large then needs the fallback pass
     try:
         _reuse_calls(pkg, O, work, hist_bytes)
     finally:
         L.mx_topk_set(b"sample_stride", 0)
+        L.mx_topk_set(b"select", saved)
 
 
 def _reuse_calls(pkg, O, work, hist_bytes):
@@ -339,6 +344,7 @@ def _reuse_calls(pkg, O, work, hist_bytes):
         assert not w[:hist_bytes].any(), "histograms not re-zeroed"
         state = w[hist_bytes:hist_bytes + 24].view(np.uint64)     # b0|T, need, cand_n
         assert state[2] == 0, "candidate total not reset"
+        assert w[hist_bytes + 28:hist_bytes + 32].view(np.uint32)[0] == 0, "a row barrier's wait expired"
 
 
 # ------------------------------------------------------------------------------------ helpers
@@ -480,12 +486,14 @@ def test_choco_vs_oracle_larger(pkg, O, P, ratio, apply_nt):
 
 
 @pytest.mark.parametrize("knobs", [{"compact_store": 0}, {"compact_store": 1}, {"compact_store": 0, "apply_nt": 0},
-                                   {"apply_pf": 0}, {"apply_pf": 0, "apply_nt": 1}])
+                                   {"apply_pf": 0}, {"apply_pf": 0, "apply_nt": 1}, {"select": 0},
+                                   {"select": 1, "select_blocks": 3}, {"select": 0, "compact_store": 0}])
 def test_choco_knob_variants(pkg, O, knobs):
     """Every Choco kernel variant selected by mx_topk_set (compaction stores looped over the kept
     elements or one masked store pair per element; apply access hints; apply with or without the
-    message entries prefetched under the tile stream) is bit-exact: the 8-row round (x / x_hat / s,
-    3 rounds) and the one-row top-k on the tie / far-threshold / sampled-fallback patterns."""
+    message entries prefetched under the tile stream; the selection as four passes or one launch)
+    is bit-exact: the 8-row round (x / x_hat / s, 3 rounds) and the one-row top-k on the tie /
+    far-threshold / sampled-fallback patterns."""
     saved = {k: int(pkg.lib.mx_topk_get(k.encode())) for k in knobs}
     for k, v in knobs.items():
         pkg._lib.check(pkg.lib.mx_topk_set(k.encode(), v))
@@ -820,3 +828,59 @@ def test_topk_compaction_variants(pkg, O, P, pattern, knob):
                 assert np.array_equal(gv.cpu().numpy().view(np.uint32), rv.view(np.uint32)), r
     finally:
         pkg.lib.mx_topk_set(key, saved)
+
+
+@pytest.mark.parametrize("blocks", [0, 1, 5, 32])
+@pytest.mark.parametrize("pattern,stride", [("layers", 0), ("sampled_large", 16), ("ties", 0), ("gap", 0),
+                                            ("coarse333", 1), ("constant", 0), ("spread", 0)])
+@pytest.mark.parametrize("P", [2_000_001, 14_774_436])
+def test_topk_select_kernel(pkg, O, P, pattern, stride, blocks):
+    """The one-launch selection (select_kernel: 10- and 9-bit passes, exact threshold, output placed
+    from the per-block slots, behind two row barriers) for any number of blocks per row -- one
+    (no other block to wait for), an odd count, the maximum -- on one row and on 8 rows of one
+    launch batch (ChocoWorkerGroup): index sets, values and tile bounds equal the oracle's, the
+    sampled fallback (stride 16: fewer than k candidates kept, every key re-compacted inside the
+    launch) among them; the rows' barrier error word stays clear."""
+    ratio = 0.99
+    x = _topk_case(O, P, pattern)
+    k = O.topk_k(P, ratio)
+    ov, oi = O.topk_abs(x, k)
+    L = pkg.lib
+    saved = {key: int(L.mx_topk_get(key)) for key in (b"select", b"select_blocks")}
+    pkg._lib.check(L.mx_topk_set(b"select", 1))
+    pkg._lib.check(L.mx_topk_set(b"select_blocks", blocks))
+    pkg._lib.check(L.mx_topk_set(b"sample_stride", stride))
+    try:
+        v, i = pkg.get_top_k(torch.from_numpy(x).cuda(), ratio)
+        assert np.array_equal(i.cpu().numpy(), oi)
+        assert np.array_equal(v.cpu().numpy().view(np.uint32), ov.view(np.uint32))
+        if P < 3_000_000:
+            kpad = (k + 1) // 2 * 2
+            nb = int(L.mx_choco_msg_bytes(P, k))
+            nt = (P + 4095) // 4096
+            wb = int(L.mx_topk_work_bytes(P))
+            wld = (wb + 255) // 256 * 256
+            X = np.stack([x * np.float32(1 + r) for r in range(8)])
+            xd = torch.from_numpy(X).cuda()
+            out = torch.zeros(8 * nb + 8 * 8, dtype=torch.uint8, device="cuda")
+            old = (nb + 7) // 8 * 8
+            work = torch.zeros(8 * wld, dtype=torch.uint8, device="cuda")
+            pkg._lib.check(L.mx_topk_abs_diff_rows(xd.data_ptr(), None, P, 8, P, k, out.data_ptr(), old, 4 * kpad,
+                                                   4 * kpad + 8 * k, work.data_ptr(), wld, None), "topk rows")
+            torch.cuda.synchronize()
+            o = out.cpu().numpy()
+            w = work.cpu().numpy()
+            for r in range(8):
+                rv, ri = O.topk_abs(X[r], k)
+                m = o[r * old:r * old + nb]
+                assert np.array_equal(m[:4 * k].view(np.uint32), rv.view(np.uint32)), r
+                assert np.array_equal(m[4 * kpad:4 * kpad + 8 * k].view(np.int64), ri), r
+                bnd = m[4 * kpad + 8 * k:nb].view(np.int32)
+                assert np.array_equal(bnd, np.searchsorted(ri, np.arange(nt + 1) * 4096).astype(np.int32)), r
+                hb = r * wld + 4 * (3 * 4096 + 1024 + 512)
+                assert not w[r * wld:hb].any(), "histograms not re-zeroed"
+                assert w[hb + 28:hb + 32].view(np.uint32)[0] == 0, "a row barrier's wait expired"
+    finally:
+        L.mx_topk_set(b"sample_stride", 0)
+        for key, val in saved.items():
+            L.mx_topk_set(key, val)

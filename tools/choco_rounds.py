@@ -27,6 +27,9 @@ else:
     torch.cuda.synchronize()
     for s in range(c.n_local, c.engine.n_slots):
         c.msgs[s * c.msg_ld:(s + 1) * c.msg_ld].copy_(c.msgs[:c.msg_ld])
+for kv in filter(None, os.environ.get("TOPK_SET", "").split(":")):     # e.g. TOPK_SET=select=1:select_blocks=32
+    k_, v_ = kv.split("=")
+    pkg._lib.check(pkg.lib.mx_topk_set(k_.encode(), int(v_)))
 for it in range(K):
     c.step(it)
 torch.cuda.synchronize()
