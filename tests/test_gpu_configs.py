@@ -83,10 +83,21 @@ def test_wrn_config_full_size(pkg, O):
     torch.cuda.empty_cache()
 
 
-def test_vgg_choco_config_full_size(pkg, O):
+@pytest.mark.parametrize("select", [0, 1])
+def test_vgg_choco_config_full_size(pkg, O, select):
     """Config 4's gossip on one GPU: 8 workers x 14,774,436 params, ratio 0.99 (k = 147,744),
     consensus_lr 0.1, a full round then two partial ones, parameter drift between rounds (the
-    optimizer step of train_mpi.py:134); x, x_hat and s uint32-exact after every round."""
+    optimizer step of train_mpi.py:134); x, x_hat and s uint32-exact after every round -- with the
+    selection as four passes (default) and as one launch (select_kernel, two launches of 4 rows)."""
+    saved = int(pkg.lib.mx_topk_get(b"select"))
+    pkg._lib.check(pkg.lib.mx_topk_set(b"select", select))
+    try:
+        _vgg_choco_rounds(pkg, O)
+    finally:
+        pkg.lib.mx_topk_set(b"select", saved)
+
+
+def _vgg_choco_rounds(pkg, O):
     n, P, ratio, gamma = 8, VGG_P, 0.99, 0.1
     gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, n, 4, True)
     flags = np.array([[1, 1, 1, 1, 1], [1, 0, 1, 1, 0], [0, 1, 1, 0, 1]], np.uint8)
