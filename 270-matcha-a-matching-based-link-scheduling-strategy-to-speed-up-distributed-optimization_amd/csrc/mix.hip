@@ -428,7 +428,11 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_reg(float* const* __restrict_
 // SPLIT > 1 (small rows, fewer layout tiles than the persistent grid): each layout tile of
 // TW * SPLIT columns is worked as SPLIT sub-tiles of TW columns, so a 181k-parameter round
 // spreads over every CU instead of a few dozen (layouts and tile_off stay in layout-tile units).
-template <int NS, int TW, bool NT, int SPLIT = 1>
+//
+// PF2: two tiles' loads in flight instead of one (two register sets, the loop unrolled by two) --
+// a persistent workgroup whose tile stages few of its NS slots (a GPU's share of a big topology:
+// few local rows, many received ones) otherwise keeps too little in flight per CU.
+template <int NS, int TW, bool NT, int SPLIT = 1, bool PF2 = false>
 __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict__ seg_ptrs,
                                                         const int64_t* __restrict__ seg_len,
                                                         const int64_t* __restrict__ tile_off,
@@ -478,7 +482,7 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict
         return gq;
     };
     F R[E4];
-    auto stage = [&](const Geo& gq) {
+    auto stage_to = [&](F (&RR)[E4], const Geo& gq) {
 #pragma unroll
         for (int j = 0; j < E4; ++j) {
             const int k = (wave * 64 + kTPB * j) / C4;            // wave-uniform slot
@@ -486,14 +490,15 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict
                 const int64_t c = gq.col0 + (int64_t)((wave * 64 + kTPB * j) % C4 + lane) * 4;
                 const float* row = gq.ptrs[k];
                 if (gq.vec_ok && c + 4 <= gq.lim) {
-                    R[j] = ld<NT, F>(row + c);
+                    RR[j] = ld<NT, F>(row + c);
                 } else {
 #pragma unroll
-                    for (int t = 0; t < 4; ++t) R[j][t] = (c + t < gq.lim) ? ld1(row + c + t) : 0.0f;
+                    for (int t = 0; t < 4; ++t) RR[j][t] = (c + t < gq.lim) ? ld1(row + c + t) : 0.0f;
                 }
             }
         }
     };
+    auto stage = [&](const Geo& gq) { stage_to(R, gq); };
 
     // deal the items (row r, pass q) = r * NQ + q to the waves: wave 0 ranks them by weight
     if (wave == 0) {
@@ -508,26 +513,23 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict
         if (lane < NI) wl[(round & 1) ? 3 - within : within][round] = w > 0 ? lane : -1;
     }
     Geo cur = geo(blockIdx.x);
+    F R2[PF2 ? E4 : 1];
+    Geo cur2 = cur;
     stage(cur);
+    if constexpr (PF2) {
+        if (niter > 1) {
+            cur2 = geo(blockIdx.x + gridDim.x);
+            stage_to(R2, cur2);
+        }
+    }
     __syncthreads();
     // ranks grow along a wave's list, so its unused (-1) entries form a suffix
     int nmy = 0;
     while (nmy < NI / 4 && wl[wave][nmy] >= 0) ++nmy;
     nmy = __builtin_amdgcn_readfirstlane(nmy);
 
-    for (int64_t i = 0; i < niter; ++i) {
-        if (i) __syncthreads();                  // every wave is done reading the previous tile
-#pragma unroll
-        for (int j = 0; j < E4; ++j) {
-            const int k = (wave * 64 + kTPB * j) / C4;
-            if ((need >> k) & 1ull) lds[k * C4 + (wave * 64 + kTPB * j) % C4 + lane] = R[j];
-        }
-        __syncthreads();
-        Geo nxt = cur;
-        if (i + 1 < niter) {                     // next tile's loads fly while this one is mixed
-            nxt = geo(blockIdx.x + (i + 1) * gridDim.x);
-            stage(nxt);
-        }
+    // mix the tile staged in LDS (columns of `cur`) and store the local rows
+    auto mix_tile = [&](const Geo& cur) {
         auto finish = [&](int it, F acc) {
             const int r = it / NQ;
             const int col = (it % NQ) * 64 + lane;
@@ -583,7 +585,45 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict
             }
             finish(ia, a);
         }
-        cur = nxt;
+    };
+    if constexpr (!PF2) {
+        for (int64_t i = 0; i < niter; ++i) {
+            if (i) __syncthreads();              // every wave is done reading the previous tile
+#pragma unroll
+            for (int j = 0; j < E4; ++j) {
+                const int k = (wave * 64 + kTPB * j) / C4;
+                if ((need >> k) & 1ull) lds[k * C4 + (wave * 64 + kTPB * j) % C4 + lane] = R[j];
+            }
+            __syncthreads();
+            Geo nxt = cur;
+            if (i + 1 < niter) {                 // next tile's loads fly while this one is mixed
+                nxt = geo(blockIdx.x + (i + 1) * gridDim.x);
+                stage(nxt);
+            }
+            mix_tile(cur);
+            cur = nxt;
+        }
+    } else {
+        // tile i in register set (i % 2); after it is parked in LDS, the set takes tile i + 2
+        auto step = [&](int64_t i, F (&RR)[E4], Geo& gi) {
+            if (i) __syncthreads();
+#pragma unroll
+            for (int j = 0; j < E4; ++j) {
+                const int k = (wave * 64 + kTPB * j) / C4;
+                if ((need >> k) & 1ull) lds[k * C4 + (wave * 64 + kTPB * j) % C4 + lane] = RR[j];
+            }
+            __syncthreads();
+            const Geo here = gi;
+            if (i + 2 < niter) {
+                gi = geo(blockIdx.x + (i + 2) * gridDim.x);
+                stage_to(RR, gi);
+            }
+            mix_tile(here);
+        };
+        for (int64_t i = 0; i < niter; i += 2) {
+            step(i, R, cur);
+            if (i + 1 < niter) step(i + 1, R2, cur2);
+        }
     }
 }
 
@@ -741,6 +781,10 @@ struct Tune {
                          // 1 = 9-64 slots only (<= 8: register-indexed / LDS-column), 0 = never
     int split = 0;       // row kernel sub-tiles per layout tile: 0 = auto (enough work items for
                          // the persistent grid), 1 / 2 / 4 = forced (capped by the geometry)
+    int rows_pf2 = 2;    // row kernel, persistent grids of 32-64 slots: two tiles' loads in flight -- 1 on,
+                         // 0 off, 2 auto: when at most 5/8 of the class's slots are staged (ER(64)'s N = 8
+                         // share, 35 of 64 slots: 0.874 -> 0.927 of the headline kernel's HBM rate; all 64
+                         // slots staged: 1.058 -> 0.971, tools/er_share.py, profiles/r03c_er_share_pf2.log)
     int flat_small = 256;  // row kernel: rounds of at most flat_small x the persistent grid's work items
                          // launch one workgroup per item instead (a second pass over the persistent
                          // grid is a second memory round trip on latency-bound short rows); 0 = never
@@ -804,7 +848,7 @@ int launch(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_o
     return MX_OK;
 }
 
-template <int NS, int TW, bool NT, int SPLIT = 1>
+template <int NS, int TW, bool NT, int SPLIT = 1, bool PF2 = false>
 int launch_rows(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_off,
                 const uint8_t* seg_vec, int nseg, int n_slots, const int32_t* plan, int64_t iter, const int64_t* iter_dev,
                 int n_local, int M, float alpha, int64_t total_tiles, hipStream_t st) {
@@ -813,7 +857,7 @@ int launch_rows(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* t
     // walks) the persistent grid stays faster (ER(32): 286 vs 350 us, ER(64): 324 vs 426 us)
     const int64_t grid = (NS <= 16 && g_tune.flat_small > 0 && g_tune.grid == 0 &&
                           work <= (int64_t)g_tune.flat_small * grid_target()) ? work : grid_for(work);
-    hipLaunchKernelGGL((mix_kernel_rows<NS, TW, NT, SPLIT>), dim3((unsigned)grid), dim3(kTPB),
+    hipLaunchKernelGGL((mix_kernel_rows<NS, TW, NT, SPLIT, PF2>), dim3((unsigned)grid), dim3(kTPB),
                        0, st, seg_ptrs, seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan,
                        iter, iter_dev, n_local, M, alpha);
     MX_LAUNCH_CHECK();
@@ -872,6 +916,9 @@ extern "C" int mx_mix_set(const char* key, int value) {
     } else if (!strcmp(key, "split")) {
         MX_CHECK(value == 0 || value == 1 || value == 2 || value == 4, "mx_mix_set: split %d", value);
         slot = &g_tune.split;
+    } else if (!strcmp(key, "rows_pf2")) {
+        MX_CHECK(value >= 0 && value <= 2, "mx_mix_set: rows_pf2 %d", value);
+        slot = &g_tune.rows_pf2;
     } else if (!strcmp(key, "flat_small")) {
         MX_CHECK(value >= 0 && value <= 4096, "mx_mix_set: flat_small %d", value);
         slot = &g_tune.flat_small;
@@ -897,6 +944,7 @@ extern "C" int mx_mix_get(const char* key) {
     if (!strcmp(key, "rows")) return g_tune.rows;
     if (!strcmp(key, "split")) return g_tune.split;
     if (!strcmp(key, "flat_small")) return g_tune.flat_small;
+    if (!strcmp(key, "rows_pf2")) return g_tune.rows_pf2;
     if (!strcmp(key, "ns48")) return g_ns48;
     mx::set_error("mx_mix_get: unknown key '%s'", key);
     return MX_ERR_INVALID;
@@ -1044,9 +1092,14 @@ int gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev, const int
 #define MX_ROWS(N, TW, S) (nt ? launch_rows<N, TW, true, S>(MX_ARGS) : launch_rows<N, TW, false, S>(MX_ARGS))
         if (c.ns == 8) return sp == 4 ? MX_ROWS(8, 256, 4) : sp == 2 ? MX_ROWS(8, 512, 2) : MX_ROWS(8, 1024, 1);
         if (c.ns == 16) return sp == 4 ? MX_ROWS(16, 256, 4) : sp == 2 ? MX_ROWS(16, 512, 2) : MX_ROWS(16, 1024, 1);
-        if (c.ns == 32) return sp == 2 ? MX_ROWS(32, 256, 2) : MX_ROWS(32, 512, 1);
-        if (c.ns == 48) return MX_ROWS(48, 256, 1);
-        return MX_ROWS(64, 256, 1);
+#define MX_ROWSP(N, TW, S)                                                                                  \
+    ((g_tune.rows_pf2 == 1 || (g_tune.rows_pf2 == 2 && 8 * n_slots <= 5 * (N)))                                  \
+         ? (nt ? launch_rows<N, TW, true, S, true>(MX_ARGS) : launch_rows<N, TW, false, S, true>(MX_ARGS))     \
+         : MX_ROWS(N, TW, S))
+        if (c.ns == 32) return sp == 2 ? MX_ROWSP(32, 256, 2) : MX_ROWSP(32, 512, 1);
+        if (c.ns == 48) return MX_ROWSP(48, 256, 1);
+        return MX_ROWSP(64, 256, 1);
+#undef MX_ROWSP
 #undef MX_ROWS
     }
     if (g_tune.regidx && c.ns == 8) {

@@ -127,6 +127,10 @@ int mx_mix_tile(int n_slots);
  *   flat_small     row kernel, 8-16 slots: rounds of at most flat_small x (CUs x blocks_per_cu) work items
  *                  launch one workgroup per item instead of the persistent grid (default 256;
  *                  0 = always persistent; ignored when grid > 0)
+ *   ns48           33-48 slots: 1 = a 48-slot row-kernel class instead of the 64-slot one (default 0)
+ *   rows_pf2       row kernel, persistent grids of 32-64 slots: two tiles' loads in flight instead of
+ *                  one -- 1 on, 0 off, 2 auto (default): when at most 5/8 of the class's slots are
+ *                  staged (a GPU's share of a big topology: few local rows, many received ones)
  * "unroll" changes the tile size: rebuild layouts (mx_mix_layout) after setting it.
  * mx_mix_get returns the current value (negative on an unknown key).
  * mx_mix_kernel_name: the kernel mx_gossip_mix launches for n_slots under the current knobs

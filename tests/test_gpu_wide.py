@@ -91,3 +91,51 @@ def test_slot_limit_message(pkg):
     topo = Topo(partner, 0.01, np.ones((2, partner.shape[0]), np.uint8))
     with pytest.raises(pkg.MXError, match="156"):
         pkg.VirtualWorkerGroup(topo, numel=100)
+
+
+@pytest.mark.parametrize("ns48,pf2", [(0, 0), (1, 0), (0, 1), (1, 1), (0, 2)])
+@pytest.mark.parametrize("nranks,P", [(8, 70_001), (4, 512 * 9 + 3), (2, 33_333), (1, 20_011)])
+def test_er64_shares_slot_classes(pkg, O, nranks, P, ns48, pf2):
+    """Config 5's topology, ER(64, 0.1, 1234), split over 8 / 4 / 2 loopback ranks (placement
+    "auto", as the bench): the per-rank shares of 35-53 slots run the 64-slot row class or the
+    48-slot one (ns48), with one or two tiles' loads in flight (rows_pf2 0 / 1, 2 = by the staged
+    share of the class); and all 64 workers on
+    one rank.  3 MATCHA-like rounds, ragged P, bit-exact vs the oracle."""
+    n = 64
+    random.seed(0)
+    base = pkg.erdos_renyi(n, 0.1, 1234)
+    gp0 = pkg.GraphProcessor(base, 1.0, 0, n, 4, False)
+    partner0 = np.asarray(gp0.neighbors_info, np.int32)
+    M = partner0.shape[0]
+    rng = np.random.RandomState(5)
+    flags = (rng.uniform(size=(3, M)) < 0.6).astype(np.uint8)
+    flags[0] = 1
+    saved = pkg.engine.mix_tuning()
+    pkg.engine.set_mix_tuning(ns48=ns48, rows_pf2=pf2)
+    try:
+        topo = Topo(partner0, 0.4 / M, flags)
+        if nranks == 1:
+            groups = [pkg.VirtualWorkerGroup(topo, numel=P)]
+            hub = None
+        else:
+            hub = LoopbackHub(nranks)
+            groups = [pkg.VirtualWorkerGroup(topo, numel=P, rank=r, nranks=nranks, comm=hub.comm(r), placement="auto")
+                      for r in range(nranks)]
+        if nranks == 8:
+            assert any(33 <= g.engine.n_slots <= 48 for g in groups)
+        X = np.stack([O.synth(700 + i, P) for i in range(n)])
+        for g in groups:
+            w = np.asarray(g.workers)
+            g.rows.copy_(torch.from_numpy(X[w]))
+            if hub is not None:
+                hub.register(g.row_base, g._row_ptrs)
+        for it, f in enumerate(flags):
+            for g in groups:
+                g.step(it)
+            torch.cuda.synchronize()
+            X = O.decen_round(X, partner0, f, topo.neighbor_weight)
+        for g in groups:
+            w = np.asarray(g.workers)
+            assert np.array_equal(g.rows.cpu().numpy().view(np.uint32), X[w].view(np.uint32))
+    finally:
+        pkg.engine.set_mix_tuning(**saved)
