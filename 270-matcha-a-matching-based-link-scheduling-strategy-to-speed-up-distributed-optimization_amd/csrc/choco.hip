@@ -1744,8 +1744,8 @@ unsigned clamp_grid(int64_t n, int64_t per, int64_t cap) {
 }  // namespace
 
 int g_sample_stride = 0;   // 0 = auto (about kSampleTarget sampled elements per row)
-int g_compact_blocks = 0;     // persistent compaction blocks over all rows; 0 = auto: 512 for one
-                              // row, 2048 for several (same-box sweeps: one row 256 / 384 / 512 / 640 /
+int g_compact_blocks = 0;     // persistent compaction blocks over all rows; 0 = auto: ~720 for one
+                              // row (an even chunk count each), 2560 for several (same-box sweeps: one row 256 / 384 / 512 / 640 /
                               // 1024 / 2048 blocks 131 / 121 / 116.4 / 116.2 / 119 / 134 us per round,
                               // the per-block prologue and flush outweigh the parallelism; 8 rows
                               // 0.667 -> 0.656 ms at 2048, flat from 768 to 3072)
@@ -1911,7 +1911,13 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
     const double frac = (double)sampled / (double)P;
     MX_CHECK(nc <= 0x7fffffff && P < ((int64_t)1 << 32), "mx_topk_abs_diff_rows: P too large (uint32 histograms)");
     const int cblocks = g_compact_blocks > 0 ? g_compact_blocks : (nrows == 1 ? 640 : 2560);
-    const unsigned bgrid = clamp_grid(nc, 1, (cblocks + nrows - 1) / nrows);   // persistent
+    unsigned bgrid = clamp_grid(nc, 1, (cblocks + nrows - 1) / nrows);   // persistent
+    if (nrows == 1 && g_compact_blocks == 0) {
+        // one row: about 720 workgroups dealt whole chunk counts, so no last pass runs on a few
+        // (VGG-16 share, 3607 chunks: 722 x 5; same box 101.3 -> 100.1 us per round vs 640)
+        const int64_t q = (nc + 360) / 720 > 1 ? (nc + 360) / 720 : 1;
+        bgrid = (unsigned)((nc + q - 1) / q);
+    }
     const unsigned wgrid = (unsigned)((nc + kWaves - 1) / kWaves);          // one wave per chunk
     const unsigned sgrid = clamp_grid(nsamp, (int64_t)g_sample_pieces * kWaves, (1024 + nrows - 1) / nrows);
     const int cchunks = g_cand_chunks > 0 ? g_cand_chunks : (nrows == 1 ? 4 : 8);
