@@ -630,17 +630,29 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict
 // Wide kernel: any matching count and up to kWideMaxSlots slots (more workers per GPU, or more
 // remote partners, than the NS <= 64 kernels and their 32-matching plan records in LDS take).
 // A layout tile (256 columns) is worked in pieces of 64 * VEC columns, VEC = 4 / 2 / 1 chosen so
-// that a piece of every slot fits in <= 40 KB of dynamic LDS (4 workgroups per CU): the whole
-// workgroup stages a piece of every needed slot (16 / 8 / 4-byte loads, slot wave-uniform), the
-// next piece's loads are issued into registers right after the barrier and fly while this piece
-// is mixed; each wave then takes rows wave, wave + 4, ... and walks the row's partner list, read
-// with wave-uniform loads from the plan record in global memory, in matching order with the self
-// term last -- the same FMA chain as every other kernel.
+// that a piece of every slot fits the LDS budget (default 158 KB: VEC = 4 up to 156 slots, one
+// 1024-thread workgroup per CU, two when the piece is <= 79 KB): the whole workgroup stages a piece
+// of every needed slot (16 / 8 / 4-byte loads, slot wave-uniform), the next piece's loads are
+// issued into registers right after the barrier and fly while this piece is mixed; each wave then
+// takes rows wave, wave + WV, ... in pairs and walks their partner lists (from the plan record,
+// copied to LDS when that costs no occupancy) two partners a step, in matching order with the self
+// term last -- the same FMA chain as every other kernel.  The partner walk is latency-bound per
+// wave, so the waves sharing one staged piece set the rate: 4 -> 16 waves per piece took 96-150
+// slots from 2.2-2.3 to 4.4 TB/s (tools/sessions/r3_s39.sh).
 constexpr int kWideMaxSlots = 156;
-constexpr int kWideRegs = (kWideMaxSlots * 64 + kTPB - 1) / kTPB;   // staged vectors per lane
 
-template <int VEC, bool NT>
-__global__ __launch_bounds__(kTPB) void mix_kernel_wide(float* const* __restrict__ seg_ptrs,
+// BIG: staging registers for up to kWideMaxSlots slots at VEC = 4 / 2 (wider pieces for big slot
+// counts, with the LDS that takes -- mx_mix_set "wide_lds_kb").
+// PLDS: the round's plan record is copied into LDS behind the pieces (when it fits), so the partner
+// walk reads slots with ds_read instead of a global load per step.
+// TPB: workgroup size (mx_mix_set "wide_tpb"): more waves share one staged piece, so more rows'
+// partner walks run at once per byte of LDS.
+template <int VEC, bool BIG, int TPB>
+constexpr int wide_regs() {
+    return ((BIG ? kWideMaxSlots : VEC == 4 ? 40 : VEC == 2 ? 80 : kWideMaxSlots) + TPB / 64 - 1) / (TPB / 64);
+}
+template <int VEC, bool NT, bool BIG, bool PLDS, int TPB>
+__global__ __launch_bounds__(TPB) void mix_kernel_wide(float* const* __restrict__ seg_ptrs,
                                                         const int64_t* __restrict__ seg_len,
                                                         const int64_t* __restrict__ tile_off,
                                                         const uint8_t* __restrict__ seg_vec, int nseg,
@@ -650,13 +662,21 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_wide(float* const* __restrict
                                                         float alpha) {
     using F = typename VT<VEC>::type;
     constexpr int PW = 64 * VEC;              // columns per piece
-    constexpr int NR = VEC == 4 ? 10 : VEC == 2 ? 20 : kWideRegs;   // 40 / 80 / 156 slots
+    constexpr int NR = wide_regs<VEC, BIG, TPB>();   // staged vectors per lane
+    constexpr int WV = TPB / 64;
     extern __shared__ __attribute__((aligned(16))) float wlds_raw[];
     F* wlds = reinterpret_cast<F*>(wlds_raw);  // [n_slots][64] vectors
     iter = round_of(iter, iter_dev);
     if (iter < 0) return;
     const int32_t* rec = plan + iter * mx::plan_words(n_local, M);
     if (rec[0] == 0) return;                  // all flags zero
+    if constexpr (PLDS) {
+        const int64_t W = mx::plan_words(n_local, M);
+        int32_t* pl = reinterpret_cast<int32_t*>(wlds_raw + (int64_t)n_slots * 64 * VEC);
+        for (int64_t i = threadIdx.x; i < W; i += TPB) pl[i] = rec[i];
+        __syncthreads();
+        rec = pl;
+    }
     const int n_remote = rec[1];
     const bool idle = rec[2] != 0;
     const int32_t* deg = rec + mx::kPlanHeader;
@@ -666,7 +686,7 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_wide(float* const* __restrict
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int pieces = tile_cols / PW;
     const int64_t work = total_tiles * pieces;
-    const int nj = (n_slots * 64 + kTPB - 1) / kTPB;   // staged vectors per lane (slot = wave + 4 j)
+    const int nj = (n_slots + WV - 1) / WV;      // staged vectors per lane (slot = wave + WV j)
     struct Geo {
         float* const* ptrs;
         int64_t col0, lim;
@@ -693,7 +713,7 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_wide(float* const* __restrict
     auto stage = [&](const Geo& g) {
 #pragma unroll
         for (int j = 0; j < NR; ++j) {
-            const int k = wave + 4 * j;                    // wave-uniform slot
+            const int k = wave + WV * j;                    // wave-uniform slot
             if (j < nj && k < n_slots && needed(k)) {
                 const int64_t c = g.col0 + (int64_t)lane * VEC;
                 if (g.vec_ok && c + VEC <= g.lim) {
@@ -712,7 +732,7 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_wide(float* const* __restrict
     for (; wi < work; wi += gridDim.x) {
 #pragma unroll
         for (int j = 0; j < NR; ++j) {
-            const int k = wave + 4 * j;
+            const int k = wave + WV * j;
             if (j < nj && k < n_slots && needed(k)) wlds[k * 64 + lane] = R[j];
         }
         __syncthreads();
@@ -721,24 +741,71 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_wide(float* const* __restrict
             nxt = geo(wi + gridDim.x);
             stage(nxt);
         }
-        for (int r = wave; r < n_local; r += kTPB / 64) {
-            const int d = __builtin_amdgcn_readfirstlane(deg[r]);
-            if (d == 0 && !idle) continue;
-            F a;
-#pragma unroll
-            for (int t = 0; t < VEC; ++t) a[t] = 0.0f;
-            for (int e = 0; e < d; ++e) {
-                const int sl = __builtin_amdgcn_readfirstlane(src[(int64_t)r * M + e]);
-                const F x = wlds[sl * 64 + lane];
-#pragma unroll
-                for (int t = 0; t < VEC; ++t) a[t] = __builtin_fmaf(alpha, x[t], a[t]);
-            }
+        // this wave's rows in pairs (r, r + WV): the two partner walks interleaved, two partners per
+        // step, so four slot reads and four piece reads are in flight at once (no branch between
+        // them); each row's FMA order is unchanged (partners in matching order, then the self term)
+        const int64_t c = cur.col0 + (int64_t)lane * VEC;
+        const bool vok = cur.vec_ok && c + VEC <= cur.lim;
+        auto finish = [&](int r, F acc) {
             const F xs = wlds[r * 64 + lane];
             const float s = sw[r];
 #pragma unroll
-            for (int t = 0; t < VEC; ++t) a[t] = __builtin_fmaf(s, xs[t], a[t]);
-            const int64_t c = cur.col0 + (int64_t)lane * VEC;
-            if (c < cur.lim) store_one<VEC, NT>(cur.ptrs[r], c, cur.lim, cur.vec_ok && c + VEC <= cur.lim, a);
+            for (int t = 0; t < VEC; ++t) acc[t] = __builtin_fmaf(s, xs[t], acc[t]);
+            if (c < cur.lim) store_one<VEC, NT>(cur.ptrs[r], c, cur.lim, vok, acc);
+        };
+        auto tail = [&](const int32_t* sr, int e, int d, F& acc) {
+            for (; e + 2 <= d; e += 2) {
+                const int s0 = __builtin_amdgcn_readfirstlane(sr[e]);
+                const int s1 = __builtin_amdgcn_readfirstlane(sr[e + 1]);
+                const F x0 = wlds[s0 * 64 + lane];
+                const F x1 = wlds[s1 * 64 + lane];
+#pragma unroll
+                for (int t = 0; t < VEC; ++t) acc[t] = __builtin_fmaf(alpha, x0[t], acc[t]);
+#pragma unroll
+                for (int t = 0; t < VEC; ++t) acc[t] = __builtin_fmaf(alpha, x1[t], acc[t]);
+            }
+            if (e < d) {
+                const F x0 = wlds[__builtin_amdgcn_readfirstlane(sr[e]) * 64 + lane];
+#pragma unroll
+                for (int t = 0; t < VEC; ++t) acc[t] = __builtin_fmaf(alpha, x0[t], acc[t]);
+            }
+        };
+        for (int ra = wave; ra < n_local; ra += 2 * WV) {
+            const int rb = ra + WV;
+            const bool hb = rb < n_local;
+            const int da = __builtin_amdgcn_readfirstlane(deg[ra]);
+            const int db = hb ? __builtin_amdgcn_readfirstlane(deg[rb]) : 0;
+            const int32_t* sa = src + (int64_t)ra * M;
+            const int32_t* sb = src + (int64_t)rb * M;
+            F a, b;
+#pragma unroll
+            for (int t = 0; t < VEC; ++t) a[t] = b[t] = 0.0f;
+            const int dm = da < db ? da : db;
+            int e = 0;
+            for (; e + 2 <= dm; e += 2) {
+                const int a0 = __builtin_amdgcn_readfirstlane(sa[e]);
+                const int a1 = __builtin_amdgcn_readfirstlane(sa[e + 1]);
+                const int b0 = __builtin_amdgcn_readfirstlane(sb[e]);
+                const int b1 = __builtin_amdgcn_readfirstlane(sb[e + 1]);
+                const F xa0 = wlds[a0 * 64 + lane];
+                const F xa1 = wlds[a1 * 64 + lane];
+                const F xb0 = wlds[b0 * 64 + lane];
+                const F xb1 = wlds[b1 * 64 + lane];
+#pragma unroll
+                for (int t = 0; t < VEC; ++t) {
+                    a[t] = __builtin_fmaf(alpha, xa0[t], a[t]);
+                    b[t] = __builtin_fmaf(alpha, xb0[t], b[t]);
+                }
+#pragma unroll
+                for (int t = 0; t < VEC; ++t) {
+                    a[t] = __builtin_fmaf(alpha, xa1[t], a[t]);
+                    b[t] = __builtin_fmaf(alpha, xb1[t], b[t]);
+                }
+            }
+            tail(sa, e, da, a);
+            tail(sb, e, db, b);
+            if (da > 0 || idle) finish(ra, a);
+            if (hb && (db > 0 || idle)) finish(rb, b);
         }
         __syncthreads();                      // the piece is read by every wave before restaging
         cur = nxt;
@@ -781,6 +848,10 @@ struct Tune {
                          // 1 = 9-64 slots only (<= 8: register-indexed / LDS-column), 0 = never
     int split = 0;       // row kernel sub-tiles per layout tile: 0 = auto (enough work items for
                          // the persistent grid), 1 / 2 / 4 = forced (capped by the geometry)
+    int wide_lds_kb = 158;  // wide kernel (65-156 slots): LDS per piece (KB); more -> wider pieces, fewer WGs per CU
+    int wide_tpb = 1024;    // wide kernel: workgroup size (256 / 512 / 1024)
+    int wide_per_cu = 0;    // wide kernel: workgroups per CU cap (0 = 4; fewer when the LDS does not fit)
+    int wide_plan_lds = 1;  // wide kernel: the plan record in LDS (when <= 32 KB) instead of global loads
     int rows_pf2 = 2;    // row kernel, persistent grids of 32-64 slots: two tiles' loads in flight -- 1 on,
                          // 0 off, 2 auto: when at most 5/8 of the class's slots are staged (ER(64)'s N = 8
                          // share, 35 of 64 slots: 0.874 -> 0.927 of the headline kernel's HBM rate; all 64
@@ -916,6 +987,18 @@ extern "C" int mx_mix_set(const char* key, int value) {
     } else if (!strcmp(key, "split")) {
         MX_CHECK(value == 0 || value == 1 || value == 2 || value == 4, "mx_mix_set: split %d", value);
         slot = &g_tune.split;
+    } else if (!strcmp(key, "wide_lds_kb")) {
+        MX_CHECK(value >= 8 && value <= 158, "mx_mix_set: wide_lds_kb %d", value);
+        slot = &g_tune.wide_lds_kb;
+    } else if (!strcmp(key, "wide_tpb")) {
+        MX_CHECK(value == 256 || value == 512 || value == 1024, "mx_mix_set: wide_tpb %d", value);
+        slot = &g_tune.wide_tpb;
+    } else if (!strcmp(key, "wide_per_cu")) {
+        MX_CHECK(value >= 0 && value <= 8, "mx_mix_set: wide_per_cu %d", value);
+        slot = &g_tune.wide_per_cu;
+    } else if (!strcmp(key, "wide_plan_lds")) {
+        MX_CHECK(value == 0 || value == 1, "mx_mix_set: wide_plan_lds %d", value);
+        slot = &g_tune.wide_plan_lds;
     } else if (!strcmp(key, "rows_pf2")) {
         MX_CHECK(value >= 0 && value <= 2, "mx_mix_set: rows_pf2 %d", value);
         slot = &g_tune.rows_pf2;
@@ -945,6 +1028,10 @@ extern "C" int mx_mix_get(const char* key) {
     if (!strcmp(key, "split")) return g_tune.split;
     if (!strcmp(key, "flat_small")) return g_tune.flat_small;
     if (!strcmp(key, "rows_pf2")) return g_tune.rows_pf2;
+    if (!strcmp(key, "wide_lds_kb")) return g_tune.wide_lds_kb;
+    if (!strcmp(key, "wide_plan_lds")) return g_tune.wide_plan_lds;
+    if (!strcmp(key, "wide_per_cu")) return g_tune.wide_per_cu;
+    if (!strcmp(key, "wide_tpb")) return g_tune.wide_tpb;
     if (!strcmp(key, "ns48")) return g_ns48;
     mx::set_error("mx_mix_get: unknown key '%s'", key);
     return MX_ERR_INVALID;
@@ -1043,20 +1130,57 @@ int gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev, const int
     if (total_tiles <= 0) return MX_OK;
     if (c.ns == 0 || M > kMaxM) {             // wide kernel: > 64 slots or > 32 matchings
         const int tile_cols = mx_mix_tile(n_slots);
-        const int vec = n_slots <= 40 ? 4 : n_slots <= 80 ? 2 : 1;   // <= 40 KB of LDS per piece
-        const size_t lds = (size_t)n_slots * 64 * vec * sizeof(float);
-        int64_t grid = (int64_t)cu_count() * 4;
+        // the widest piece (64 x VEC columns of every slot) within the LDS budget (default 40 KB:
+        // 4 workgroups per CU); the persistent grid as many per CU as that LDS allows (<= 4)
+        const size_t budget = (size_t)g_tune.wide_lds_kb * 1024;
+        int vec = 1;
+        if ((size_t)n_slots * 64 * 4 * sizeof(float) <= budget) vec = 4;
+        else if ((size_t)n_slots * 64 * 2 * sizeof(float) <= budget) vec = 2;
+        const size_t plan_bytes = (size_t)mx::plan_words(n_local, M) * sizeof(int32_t);
+        const size_t piece_bytes = (size_t)n_slots * 64 * vec * sizeof(float);
+        auto fit = [](size_t b) { return std::min<int64_t>(4, (int64_t)((159 * 1024) / b)); };
+        // the plan goes to LDS only when it costs no workgroup per CU (occupancy beats ds_read here)
+        const bool plds = g_tune.wide_plan_lds && plan_bytes <= 32 * 1024 &&
+                          piece_bytes + plan_bytes <= 158 * 1024 && fit(piece_bytes + plan_bytes) == fit(piece_bytes);
+        const size_t lds = (size_t)n_slots * 64 * vec * sizeof(float) + (plds ? plan_bytes : 0);
+        const int tpb = g_tune.wide_tpb;
+        int64_t per_cu = (int64_t)((159 * 1024) / lds);
+        int64_t cap = g_tune.wide_per_cu > 0 ? g_tune.wide_per_cu : 4;
+        if (cap > 2048 / tpb) cap = 2048 / tpb;  // 32 waves per CU
+        per_cu = per_cu > cap ? cap : per_cu < 1 ? 1 : per_cu;
+        int64_t grid = (int64_t)cu_count() * per_cu;
         const int64_t work = total_tiles * (tile_cols / (64 * vec));
         if (grid > work) grid = work;
         const bool nt = g_tune.nontemporal != 0;
-#define MX_WIDE(V, N)                                                                                      \
-    hipLaunchKernelGGL((mix_kernel_wide<V, N>), dim3((unsigned)(grid < 1 ? 1 : grid)), dim3(kTPB), lds, st, \
-                       seg_ptrs_dev, seg_len_dev, tile_off_dev, seg_vec_dev, nseg, total_tiles, tile_cols,   \
-                       n_slots, plan_dev, iter, iter_dev, n_local, M, alpha)
-        if (vec == 4) { if (nt) MX_WIDE(4, true); else MX_WIDE(4, false); }
-        else if (vec == 2) { if (nt) MX_WIDE(2, true); else MX_WIDE(2, false); }
-        else { if (nt) MX_WIDE(1, true); else MX_WIDE(1, false); }
+        const bool big = (vec == 4 && n_slots > 40) || (vec == 2 && n_slots > 80);
+        MX_CHECK(n_slots <= (big || vec == 1 ? kWideMaxSlots : vec == 4 ? 40 : 80), "mx_gossip_mix: wide staging");
+#define MX_WIDE1(V, N, B, PL, T)                                                                               \
+    do {                                                                                                      \
+        if (lds > 64 * 1024)                                                                                  \
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(mix_kernel_wide<V, N, B, PL, T>),         \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                 \
+        hipLaunchKernelGGL((mix_kernel_wide<V, N, B, PL, T>), dim3((unsigned)(grid < 1 ? 1 : grid)), dim3(T),  \
+                           lds, st, seg_ptrs_dev, seg_len_dev, tile_off_dev, seg_vec_dev, nseg, total_tiles,  \
+                           tile_cols, n_slots, plan_dev, iter, iter_dev, n_local, M, alpha);                  \
+    } while (0)
+#define MX_WIDE2(V, N, B, PL)                                                                                 \
+    do {                                                                                                      \
+        if (tpb == 1024) MX_WIDE1(V, N, B, PL, 1024);                                                        \
+        else if (tpb == 512) MX_WIDE1(V, N, B, PL, 512);                                                     \
+        else MX_WIDE1(V, N, B, PL, 256);                                                                     \
+    } while (0)
+#define MX_WIDE(V, N, B)                                                                                      \
+    do {                                                                                                      \
+        if (plds) MX_WIDE2(V, N, B, true); else MX_WIDE2(V, N, B, false);                                     \
+    } while (0)
+        if (vec == 4 && big) { if (nt) MX_WIDE(4, true, true); else MX_WIDE(4, false, true); }
+        else if (vec == 4) { if (nt) MX_WIDE(4, true, false); else MX_WIDE(4, false, false); }
+        else if (vec == 2 && big) { if (nt) MX_WIDE(2, true, true); else MX_WIDE(2, false, true); }
+        else if (vec == 2) { if (nt) MX_WIDE(2, true, false); else MX_WIDE(2, false, false); }
+        else { if (nt) MX_WIDE(1, true, false); else MX_WIDE(1, false, false); }
 #undef MX_WIDE
+#undef MX_WIDE2
+#undef MX_WIDE1
         MX_LAUNCH_CHECK();
         return MX_OK;
     }

@@ -131,6 +131,13 @@ int mx_mix_tile(int n_slots);
  *   rows_pf2       row kernel, persistent grids of 32-64 slots: two tiles' loads in flight instead of
  *                  one -- 1 on, 0 off, 2 auto (default): when at most 5/8 of the class's slots are
  *                  staged (a GPU's share of a big topology: few local rows, many received ones)
+ *   wide_tpb       wide kernel: workgroup size 256 / 512 / 1024 (default 1024: 16 waves walk the rows of
+ *                  one staged piece)
+ *   wide_lds_kb    wide kernel: LDS budget per staged piece, 8-158 KB (default 158: 64 x 4 columns of
+ *                  every slot up to 156 slots); smaller -> narrower pieces, more workgroups per CU
+ *   wide_per_cu    wide kernel: workgroups per CU cap, 0 = auto (LDS- and wave-limited, <= 4)
+ *   wide_plan_lds  wide kernel: copy the round's plan record to LDS when that costs no occupancy
+ *                  (default 1)
  * "unroll" changes the tile size: rebuild layouts (mx_mix_layout) after setting it.
  * mx_mix_get returns the current value (negative on an unknown key).
  * mx_mix_kernel_name: the kernel mx_gossip_mix launches for n_slots under the current knobs
