@@ -432,8 +432,8 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_reg(float* const* __restrict_
 // PF2: two tiles' loads in flight instead of one (two register sets, the loop unrolled by two) --
 // a persistent workgroup whose tile stages few of its NS slots (a GPU's share of a big topology:
 // few local rows, many received ones) otherwise keeps too little in flight per CU.
-template <int NS, int TW, bool NT, int SPLIT = 1, bool PF2 = false>
-__global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict__ seg_ptrs,
+template <int NS, int TW, bool NT, int SPLIT = 1, bool PF2 = false, int TPB = kTPB>
+__global__ __launch_bounds__(TPB) void mix_kernel_rows(float* const* __restrict__ seg_ptrs,
                                                         const int64_t* __restrict__ seg_len,
                                                         const int64_t* __restrict__ tile_off,
                                                         const uint8_t* __restrict__ seg_vec, int nseg,
@@ -444,11 +444,12 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict
     constexpr int C4 = TW / 4;            // float4 per slot per tile
     constexpr int NQ = TW / 256;          // 256-column passes per row
     constexpr int NI = NS * NQ;           // items per tile (<= 64: one per lane of wave 0)
-    constexpr int E4 = NS * C4 / kTPB;    // float4 staged per lane per tile
-    static_assert(NI <= 64 && NI % 4 == 0 && E4 >= 1 && C4 % 64 == 0, "row kernel geometry");
+    constexpr int WV = TPB / 64;          // waves sharing the staged tile
+    constexpr int E4 = NS * C4 / TPB;     // float4 staged per lane per tile
+    static_assert(NI <= 64 && NI % WV == 0 && E4 >= 1 && E4 * TPB == NS * C4 && C4 % 64 == 0, "row kernel geometry");
     __shared__ F lds[NS * C4];
     __shared__ PlanLds<NS> sp;
-    __shared__ int32_t wl[4][NI / 4];
+    __shared__ int32_t wl[WV][NI / WV];
     const uint64_t need = load_plan<NS>(sp, plan, round_of(iter, iter_dev), n_local, M);
     if (need == 0) return;
     const int32_t* deg = sp.w + mx::kPlanHeader;
@@ -485,9 +486,9 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict
     auto stage_to = [&](F (&RR)[E4], const Geo& gq) {
 #pragma unroll
         for (int j = 0; j < E4; ++j) {
-            const int k = (wave * 64 + kTPB * j) / C4;            // wave-uniform slot
+            const int k = (wave * 64 + TPB * j) / C4;            // wave-uniform slot
             if ((need >> k) & 1ull) {
-                const int64_t c = gq.col0 + (int64_t)((wave * 64 + kTPB * j) % C4 + lane) * 4;
+                const int64_t c = gq.col0 + (int64_t)((wave * 64 + TPB * j) % C4 + lane) * 4;
                 const float* row = gq.ptrs[k];
                 if (gq.vec_ok && c + 4 <= gq.lim) {
                     RR[j] = ld<NT, F>(row + c);
@@ -509,8 +510,8 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict
             const int wj = __builtin_amdgcn_readlane(w, j);
             rank += (wj > w) || (wj == w && j < lane);
         }
-        const int round = rank >> 2, within = rank & 3;
-        if (lane < NI) wl[(round & 1) ? 3 - within : within][round] = w > 0 ? lane : -1;
+        const int round = rank / WV, within = rank % WV;
+        if (lane < NI) wl[(round & 1) ? WV - 1 - within : within][round] = w > 0 ? lane : -1;
     }
     Geo cur = geo(blockIdx.x);
     F R2[PF2 ? E4 : 1];
@@ -525,7 +526,7 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict
     __syncthreads();
     // ranks grow along a wave's list, so its unused (-1) entries form a suffix
     int nmy = 0;
-    while (nmy < NI / 4 && wl[wave][nmy] >= 0) ++nmy;
+    while (nmy < NI / WV && wl[wave][nmy] >= 0) ++nmy;
     nmy = __builtin_amdgcn_readfirstlane(nmy);
 
     // mix the tile staged in LDS (columns of `cur`) and store the local rows
@@ -591,8 +592,8 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict
             if (i) __syncthreads();              // every wave is done reading the previous tile
 #pragma unroll
             for (int j = 0; j < E4; ++j) {
-                const int k = (wave * 64 + kTPB * j) / C4;
-                if ((need >> k) & 1ull) lds[k * C4 + (wave * 64 + kTPB * j) % C4 + lane] = R[j];
+                const int k = (wave * 64 + TPB * j) / C4;
+                if ((need >> k) & 1ull) lds[k * C4 + (wave * 64 + TPB * j) % C4 + lane] = R[j];
             }
             __syncthreads();
             Geo nxt = cur;
@@ -609,8 +610,8 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_rows(float* const* __restrict
             if (i) __syncthreads();
 #pragma unroll
             for (int j = 0; j < E4; ++j) {
-                const int k = (wave * 64 + kTPB * j) / C4;
-                if ((need >> k) & 1ull) lds[k * C4 + (wave * 64 + kTPB * j) % C4 + lane] = RR[j];
+                const int k = (wave * 64 + TPB * j) / C4;
+                if ((need >> k) & 1ull) lds[k * C4 + (wave * 64 + TPB * j) % C4 + lane] = RR[j];
             }
             __syncthreads();
             const Geo here = gi;
@@ -849,6 +850,7 @@ struct Tune {
     int split = 0;       // row kernel sub-tiles per layout tile: 0 = auto (enough work items for
                          // the persistent grid), 1 / 2 / 4 = forced (capped by the geometry)
     int wide_lds_kb = 158;  // wide kernel (65-156 slots): LDS per piece (KB); more -> wider pieces, fewer WGs per CU
+    int rows_tpb = 256;     // row kernel, 32-64 slots (unsplit tiles): workgroup size 256 / 512 / 1024
     int wide_tpb = 1024;    // wide kernel: workgroup size (256 / 512 / 1024)
     int wide_per_cu = 0;    // wide kernel: workgroups per CU cap (0 = 4; fewer when the LDS does not fit)
     int wide_plan_lds = 1;  // wide kernel: the plan record in LDS (when <= 32 KB) instead of global loads
@@ -919,7 +921,7 @@ int launch(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_o
     return MX_OK;
 }
 
-template <int NS, int TW, bool NT, int SPLIT = 1, bool PF2 = false>
+template <int NS, int TW, bool NT, int SPLIT = 1, bool PF2 = false, int TPB = kTPB>
 int launch_rows(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_off,
                 const uint8_t* seg_vec, int nseg, int n_slots, const int32_t* plan, int64_t iter, const int64_t* iter_dev,
                 int n_local, int M, float alpha, int64_t total_tiles, hipStream_t st) {
@@ -928,7 +930,7 @@ int launch_rows(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* t
     // walks) the persistent grid stays faster (ER(32): 286 vs 350 us, ER(64): 324 vs 426 us)
     const int64_t grid = (NS <= 16 && g_tune.flat_small > 0 && g_tune.grid == 0 &&
                           work <= (int64_t)g_tune.flat_small * grid_target()) ? work : grid_for(work);
-    hipLaunchKernelGGL((mix_kernel_rows<NS, TW, NT, SPLIT, PF2>), dim3((unsigned)grid), dim3(kTPB),
+    hipLaunchKernelGGL((mix_kernel_rows<NS, TW, NT, SPLIT, PF2, TPB>), dim3((unsigned)grid), dim3(TPB),
                        0, st, seg_ptrs, seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan,
                        iter, iter_dev, n_local, M, alpha);
     MX_LAUNCH_CHECK();
@@ -990,6 +992,9 @@ extern "C" int mx_mix_set(const char* key, int value) {
     } else if (!strcmp(key, "wide_lds_kb")) {
         MX_CHECK(value >= 8 && value <= 158, "mx_mix_set: wide_lds_kb %d", value);
         slot = &g_tune.wide_lds_kb;
+    } else if (!strcmp(key, "rows_tpb")) {
+        MX_CHECK(value == 256 || value == 512 || value == 1024, "mx_mix_set: rows_tpb %d", value);
+        slot = &g_tune.rows_tpb;
     } else if (!strcmp(key, "wide_tpb")) {
         MX_CHECK(value == 256 || value == 512 || value == 1024, "mx_mix_set: wide_tpb %d", value);
         slot = &g_tune.wide_tpb;
@@ -1032,6 +1037,7 @@ extern "C" int mx_mix_get(const char* key) {
     if (!strcmp(key, "wide_plan_lds")) return g_tune.wide_plan_lds;
     if (!strcmp(key, "wide_per_cu")) return g_tune.wide_per_cu;
     if (!strcmp(key, "wide_tpb")) return g_tune.wide_tpb;
+    if (!strcmp(key, "rows_tpb")) return g_tune.rows_tpb;
     if (!strcmp(key, "ns48")) return g_ns48;
     mx::set_error("mx_mix_get: unknown key '%s'", key);
     return MX_ERR_INVALID;
@@ -1220,9 +1226,17 @@ int gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev, const int
     ((g_tune.rows_pf2 == 1 || (g_tune.rows_pf2 == 2 && 8 * n_slots <= 5 * (N)))                                  \
          ? (nt ? launch_rows<N, TW, true, S, true>(MX_ARGS) : launch_rows<N, TW, false, S, true>(MX_ARGS))     \
          : MX_ROWS(N, TW, S))
-        if (c.ns == 32) return sp == 2 ? MX_ROWSP(32, 256, 2) : MX_ROWSP(32, 512, 1);
-        if (c.ns == 48) return MX_ROWSP(48, 256, 1);
-        return MX_ROWSP(64, 256, 1);
+#define MX_ROWST(N, TW, T)                                                                                  \
+    ((g_tune.rows_pf2 == 1 || (g_tune.rows_pf2 == 2 && 8 * n_slots <= 5 * (N)))                                  \
+         ? (nt ? launch_rows<N, TW, true, 1, true, T>(MX_ARGS) : launch_rows<N, TW, false, 1, true, T>(MX_ARGS)) \
+         : (nt ? launch_rows<N, TW, true, 1, false, T>(MX_ARGS) : launch_rows<N, TW, false, 1, false, T>(MX_ARGS)))
+#define MX_ROWSW(N, TW)                                                                                     \
+    (g_tune.rows_tpb == 1024 ? MX_ROWST(N, TW, 1024) : g_tune.rows_tpb == 512 ? MX_ROWST(N, TW, 512) : MX_ROWSP(N, TW, 1))
+        if (c.ns == 32) return sp == 2 ? MX_ROWSP(32, 256, 2) : MX_ROWSW(32, 512);
+        if (c.ns == 48) return MX_ROWSW(48, 256);
+        return MX_ROWSW(64, 256);
+#undef MX_ROWSW
+#undef MX_ROWST
 #undef MX_ROWSP
 #undef MX_ROWS
     }

@@ -131,6 +131,8 @@ int mx_mix_tile(int n_slots);
  *   rows_pf2       row kernel, persistent grids of 32-64 slots: two tiles' loads in flight instead of
  *                  one -- 1 on, 0 off, 2 auto (default): when at most 5/8 of the class's slots are
  *                  staged (a GPU's share of a big topology: few local rows, many received ones)
+ *   rows_tpb       row kernel, 32-64-slot classes on unsplit tiles: workgroup size 256 (default) / 512 /
+ *                  1024 -- the tile's items dealt to 4 / 8 / 16 waves (measured neutral, r3)
  *   wide_tpb       wide kernel: workgroup size 256 / 512 / 1024 (default 1024: 16 waves walk the rows of
  *                  one staged piece)
  *   wide_lds_kb    wide kernel: LDS budget per staged piece, 8-158 KB (default 158: 64 x 4 columns of

@@ -93,13 +93,14 @@ def test_slot_limit_message(pkg):
         pkg.VirtualWorkerGroup(topo, numel=100)
 
 
-@pytest.mark.parametrize("ns48,pf2", [(0, 0), (1, 0), (0, 1), (1, 1), (0, 2)])
+@pytest.mark.parametrize("ns48,pf2,tpb", [(0, 0, 256), (1, 0, 256), (0, 1, 256), (1, 1, 256), (0, 2, 256),
+                                          (0, 2, 1024), (1, 2, 1024), (0, 1, 1024), (0, 0, 512), (1, 1, 512)])
 @pytest.mark.parametrize("nranks,P", [(8, 70_001), (4, 512 * 9 + 3), (2, 33_333), (1, 20_011)])
-def test_er64_shares_slot_classes(pkg, O, nranks, P, ns48, pf2):
+def test_er64_shares_slot_classes(pkg, O, nranks, P, ns48, pf2, tpb):
     """Config 5's topology, ER(64, 0.1, 1234), split over 8 / 4 / 2 loopback ranks (placement
     "auto", as the bench): the per-rank shares of 35-53 slots run the 64-slot row class or the
     48-slot one (ns48), with one or two tiles' loads in flight (rows_pf2 0 / 1, 2 = by the staged
-    share of the class); and all 64 workers on
+    share of the class), in 256 / 512 / 1024-thread workgroups (rows_tpb); and all 64 workers on
     one rank.  3 MATCHA-like rounds, ragged P, bit-exact vs the oracle."""
     n = 64
     random.seed(0)
@@ -111,7 +112,7 @@ def test_er64_shares_slot_classes(pkg, O, nranks, P, ns48, pf2):
     flags = (rng.uniform(size=(3, M)) < 0.6).astype(np.uint8)
     flags[0] = 1
     saved = pkg.engine.mix_tuning()
-    pkg.engine.set_mix_tuning(ns48=ns48, rows_pf2=pf2)
+    pkg.engine.set_mix_tuning(ns48=ns48, rows_pf2=pf2, rows_tpb=tpb)
     try:
         topo = Topo(partner0, 0.4 / M, flags)
         if nranks == 1:
@@ -161,6 +162,35 @@ def test_wide_lds_budget(pkg, O, n, p, seed, P, lds_kb, plan_lds, tpb):
     try:
         grp = pkg.VirtualWorkerGroup(topo, numel=P)
         X = np.stack([O.synth(23 * seed + i, P) for i in range(n)])
+        grp.rows.copy_(torch.from_numpy(X))
+        for f in flags:
+            grp.communicate()
+            X = O.decen_round(X, partner, f, topo.neighbor_weight)
+        got = grp.rows.cpu().numpy()
+    finally:
+        pkg.engine.set_mix_tuning(**saved)
+    assert np.array_equal(got.view(np.uint32), X.view(np.uint32))
+
+
+@pytest.mark.parametrize("tpb,pf2", [(512, 0), (1024, 0), (1024, 1)])
+@pytest.mark.parametrize("n,p,seed", [(32, 0.15, 2), (48, 0.1, 4), (64, 0.1, 1234)])
+def test_rows_tpb_full_tiles(pkg, O, n, p, seed, tpb, pf2):
+    """The 32 / 48 / 64-slot row classes on unsplit tiles (more layout tiles than the persistent
+    grid) in 512 / 1024-thread workgroups (rows_tpb: the items of a tile dealt to 8 / 16 waves),
+    one or two tiles in flight; 4 MATCHA-like rounds with skipped matchings, ragged P, bit-exact."""
+    partner = _er(pkg, n, p, seed)
+    M = partner.shape[0]
+    rng = np.random.RandomState(seed)
+    flags = (rng.uniform(size=(4, M)) < 0.5).astype(np.uint8)
+    flags[0] = 1
+    topo = Topo(partner, 0.5 / M, flags)
+    P = 700 * 512 + 77
+    saved = pkg.engine.mix_tuning()
+    pkg.engine.set_mix_tuning(rows_tpb=tpb, rows_pf2=pf2, ns48=1 if n == 48 else 0)
+    try:
+        grp = pkg.VirtualWorkerGroup(topo, numel=P)
+        assert pkg.engine.mix_kernel_name(grp.engine.n_slots) == "mix_kernel_rows"
+        X = np.stack([O.synth(31 * seed + i, P) for i in range(n)])
         grp.rows.copy_(torch.from_numpy(X))
         for f in flags:
             grp.communicate()
