@@ -1,0 +1,7 @@
+#!/bin/bash
+# Round 3, session 42: the whole GPU suite on the current tree, then the smoke entry point.
+set -u
+OUT=gpurun_out/r3s42; mkdir -p $OUT; export TMPDIR=/tmp
+step() { local name=$1 lim=$2; shift 2; echo "== $name $(date +%T)"; timeout -k 10 $lim "$@" > $OUT/$name.log 2>&1; local rc=$?; echo "rc=$rc"; tail -${TAILN:-16} $OUT/$name.log | cut -c1-300; if [ $rc -ne 0 ]; then exit $rc; fi; return 0; }
+TAILN=8 step suite 1050 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests
+TAILN=4 step smoke 120 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')"
