@@ -1149,6 +1149,7 @@ int gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev, const int
         const bool plds = g_tune.wide_plan_lds && plan_bytes <= 32 * 1024 &&
                           piece_bytes + plan_bytes <= 158 * 1024 && fit(piece_bytes + plan_bytes) == fit(piece_bytes);
         const size_t lds = (size_t)n_slots * 64 * vec * sizeof(float) + (plds ? plan_bytes : 0);
+        MX_CHECK(lds <= 158 * 1024, "mx_gossip_mix: wide kernel LDS %zu", lds);
         const int tpb = g_tune.wide_tpb;
         int64_t per_cu = (int64_t)((159 * 1024) / lds);
         int64_t cap = g_tune.wide_per_cu > 0 ? g_tune.wide_per_cu : 4;
@@ -1162,9 +1163,12 @@ int gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev, const int
         MX_CHECK(n_slots <= (big || vec == 1 ? kWideMaxSlots : vec == 4 ? 40 : 80), "mx_gossip_mix: wide staging");
 #define MX_WIDE1(V, N, B, PL, T)                                                                               \
     do {                                                                                                      \
-        if (lds > 64 * 1024)                                                                                  \
+        static bool big_lds = false;          /* once per instantiation: the most the kernel may ask */   \
+        if (lds > 64 * 1024 && !big_lds) {                                                                    \
             (void)hipFuncSetAttribute(reinterpret_cast<const void*>(mix_kernel_wide<V, N, B, PL, T>),         \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                 \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, 158 * 1024);               \
+            big_lds = true;                                                                                   \
+        }                                                                                                     \
         hipLaunchKernelGGL((mix_kernel_wide<V, N, B, PL, T>), dim3((unsigned)(grid < 1 ? 1 : grid)), dim3(T),  \
                            lds, st, seg_ptrs_dev, seg_len_dev, tile_off_dev, seg_vec_dev, nseg, total_tiles,  \
                            tile_cols, n_slots, plan_dev, iter, iter_dev, n_local, M, alpha);                  \
