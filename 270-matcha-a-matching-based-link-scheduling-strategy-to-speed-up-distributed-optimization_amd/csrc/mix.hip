@@ -861,6 +861,8 @@ struct Tune {
     int flat_small = 256;  // row kernel: rounds of at most flat_small x the persistent grid's work items
                          // launch one workgroup per item instead (a second pass over the persistent
                          // grid is a second memory round trip on latency-bound short rows); 0 = never
+    int mid_bpc = 4;       // row kernel, 8 slots, rows of at most mid_tiles x CUs layout tiles: a persistent
+    int mid_tiles = 8;     // grid of mid_bpc workgroups per CU instead of the flat one (0 = off)
 };
 Tune g_tune;
 
@@ -892,6 +894,14 @@ inline int64_t grid_for(int64_t total_tiles) {
     return grid < 1 ? 1 : grid;
 }
 
+// 8 slots, mid-sized rows (0.4-2M params: a few work items per CU): a persistent grid of mid_bpc
+// workgroups per CU, each with its next item's loads in flight, beats one workgroup per item by 7-13 %
+// (graph-replayed rounds, tools/small_cfg.py; equal at 181k, the flat grid 1-3 % ahead from 4M on)
+inline bool rows_mid(int ns, int64_t total_tiles) {
+    return ns == 8 && g_tune.mid_bpc > 0 && g_tune.flat_small > 0 && g_tune.grid == 0 &&
+           total_tiles <= (int64_t)g_tune.mid_tiles * cu_count();
+}
+
 // row kernel sub-tiles per layout tile: a sub-tile keeps >= 256 columns (one wave pass), and
 // auto picks the smallest split giving the persistent grid 1.5 work items per workgroup
 // (measured, 8 slots: 651 tiles run 11 % faster as 1302 sub-tiles, 977 tiles 5 % slower as 1954)
@@ -899,6 +909,10 @@ int row_split(int ns, int64_t total_tiles) {
     const int cap = ns >= 48 ? 1 : (ns == 32 ? 2 : 4);
     if (g_tune.split > 0) return g_tune.split < cap ? g_tune.split : cap;
     int s = 1;
+    if (rows_mid(ns, total_tiles)) {
+        while (s < cap && 2 * total_tiles * s < 3 * (int64_t)cu_count() * g_tune.mid_bpc) s *= 2;
+        return s;
+    }
     while (s < cap && 2 * total_tiles * s < 3 * grid_target()) s *= 2;
     // with one workgroup per work item (flat_small), 512-column sub-tiles beat whole 1024-column
     // tiles at every size measured for 8 slots (2M-36.5M params: -1 to -6 %; headline 283.8 ->
@@ -928,8 +942,10 @@ int launch_rows(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* t
     const int64_t work = total_tiles * SPLIT;
     // one workgroup per item only for 8-16 slots: with 32 / 64 slots (narrower tiles, longer partner
     // walks) the persistent grid stays faster (ER(32): 286 vs 350 us, ER(64): 324 vs 426 us)
-    const int64_t grid = (NS <= 16 && g_tune.flat_small > 0 && g_tune.grid == 0 &&
-                          work <= (int64_t)g_tune.flat_small * grid_target()) ? work : grid_for(work);
+    const int64_t mid = rows_mid(NS, total_tiles) ? (int64_t)cu_count() * g_tune.mid_bpc : 0;
+    const int64_t grid = mid ? (work < mid ? work : mid)
+                         : (NS <= 16 && g_tune.flat_small > 0 && g_tune.grid == 0 &&
+                            work <= (int64_t)g_tune.flat_small * grid_target()) ? work : grid_for(work);
     hipLaunchKernelGGL((mix_kernel_rows<NS, TW, NT, SPLIT, PF2, TPB>), dim3((unsigned)grid), dim3(TPB),
                        0, st, seg_ptrs, seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan,
                        iter, iter_dev, n_local, M, alpha);
@@ -1007,6 +1023,12 @@ extern "C" int mx_mix_set(const char* key, int value) {
     } else if (!strcmp(key, "rows_pf2")) {
         MX_CHECK(value >= 0 && value <= 2, "mx_mix_set: rows_pf2 %d", value);
         slot = &g_tune.rows_pf2;
+    } else if (!strcmp(key, "mid_bpc")) {
+        MX_CHECK(value >= 0 && value <= 16, "mx_mix_set: mid_bpc %d", value);
+        slot = &g_tune.mid_bpc;
+    } else if (!strcmp(key, "mid_tiles")) {
+        MX_CHECK(value >= 0 && value <= 1024, "mx_mix_set: mid_tiles %d", value);
+        slot = &g_tune.mid_tiles;
     } else if (!strcmp(key, "flat_small")) {
         MX_CHECK(value >= 0 && value <= 4096, "mx_mix_set: flat_small %d", value);
         slot = &g_tune.flat_small;
@@ -1032,6 +1054,8 @@ extern "C" int mx_mix_get(const char* key) {
     if (!strcmp(key, "rows")) return g_tune.rows;
     if (!strcmp(key, "split")) return g_tune.split;
     if (!strcmp(key, "flat_small")) return g_tune.flat_small;
+    if (!strcmp(key, "mid_bpc")) return g_tune.mid_bpc;
+    if (!strcmp(key, "mid_tiles")) return g_tune.mid_tiles;
     if (!strcmp(key, "rows_pf2")) return g_tune.rows_pf2;
     if (!strcmp(key, "wide_lds_kb")) return g_tune.wide_lds_kb;
     if (!strcmp(key, "wide_plan_lds")) return g_tune.wide_plan_lds;

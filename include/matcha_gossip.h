@@ -127,6 +127,9 @@ int mx_mix_tile(int n_slots);
  *   flat_small     row kernel, 8-16 slots: rounds of at most flat_small x (CUs x blocks_per_cu) work items
  *                  launch one workgroup per item instead of the persistent grid (default 256;
  *                  0 = always persistent; ignored when grid > 0)
+ *   mid_bpc        row kernel, 8 slots, rows of at most mid_tiles x CUs layout tiles (0.4-2M params): a
+ *   mid_tiles      persistent grid of mid_bpc workgroups per CU instead of the flat one (defaults 4 / 8;
+ *                  mid_bpc 0 = off)
  *   ns48           33-48 slots: 1 = a 48-slot row-kernel class instead of the 64-slot one (default 0)
  *   rows_pf2       row kernel, persistent grids of 32-64 slots: two tiles' loads in flight instead of
  *                  one -- 1 on, 0 off, 2 auto (default): when at most 5/8 of the class's slots are

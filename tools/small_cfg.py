@@ -22,8 +22,11 @@ for tune in os.environ.get("SMALL_TUNE", "").split(";"):
     pkg.engine.set_mix_tuning(**DEFAULT)
     if tune:
         pkg.engine.set_mix_tuning(**{k: int(v) for k, v in (kv.split("=") for kv in tune.split(","))})
-    for name, P, budget in (("resnet18_100_matcha0.5", 181_668, 0.5), ("mlp_matcha0.5", 666_547, 0.5),
-                            ("resnet18_100_full", 181_668, 1.0)):
+    cases = (("resnet18_100_matcha0.5", 181_668, 0.5), ("mlp_matcha0.5", 666_547, 0.5),
+             ("resnet18_100_full", 181_668, 1.0))
+    if os.environ.get("SMALL_P"):                # e.g. SMALL_P=1000000,2000000 (MATCHA 0.5 rows of that size)
+        cases = tuple((f"P{p}_matcha0.5", int(float(p)), 0.5) for p in os.environ["SMALL_P"].split(","))
+    for name, P, budget in cases:
         np.random.seed(1234)
         gp = pkg.MatchaProcessor(pkg.select_graph(0), budget, 0, 8, 2 * (W + K) + 2, True)
         g = pkg.VirtualWorkerGroup(gp, numel=P)
