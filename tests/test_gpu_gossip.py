@@ -394,13 +394,14 @@ def test_mix_row_kernel_for_eight_slots(pkg, O, bpc, nt, u, sp):
         pkg.engine.set_mix_tuning(**saved)
 
 
-@pytest.mark.parametrize("flat,bpc", [(0, 2), (0, 1), (128, 2)])
-def test_mix_persistent_and_flat_grids(pkg, O, flat, bpc):
+@pytest.mark.parametrize("flat,bpc,mid", [(0, 2, 4), (0, 1, 4), (128, 2, 0), (128, 2, 4), (256, 2, 2), (256, 2, 8)])
+def test_mix_persistent_and_flat_grids(pkg, O, flat, bpc, mid):
     """The row kernel's grid: persistent workgroups striding over the tiles (flat_small = 0, several
-    tiles per workgroup) and one workgroup per work item -- bit-exact on the same layouts."""
+    tiles per workgroup), one workgroup per work item (mid_bpc = 0), and the 8-slot mid-size
+    persistent grid of mid_bpc workgroups per CU -- bit-exact on the same layouts."""
     saved = pkg.engine.mix_tuning()
     try:
-        pkg.engine.set_mix_tuning(flat_small=flat, blocks_per_cu=bpc, rows=2)
+        pkg.engine.set_mix_tuning(flat_small=flat, blocks_per_cu=bpc, rows=2, mid_bpc=mid)
         _layouts_bit_exact(pkg, O)
     finally:
         pkg.engine.set_mix_tuning(**saved)
