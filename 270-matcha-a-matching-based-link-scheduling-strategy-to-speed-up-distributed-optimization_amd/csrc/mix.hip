@@ -28,6 +28,8 @@
 // LDS) and the LDS-column kernel (mix_kernel: per-lane columns, every row to the max degree).
 #include "mx_common.h"
 
+#include <type_traits>
+
 namespace {
 constexpr int kTPB = 256;
 constexpr int kMaxM = 32;
@@ -652,7 +654,7 @@ template <int VEC, bool BIG, int TPB>
 constexpr int wide_regs() {
     return ((BIG ? kWideMaxSlots : VEC == 4 ? 40 : VEC == 2 ? 80 : kWideMaxSlots) + TPB / 64 - 1) / (TPB / 64);
 }
-template <int VEC, bool NT, bool BIG, bool PLDS, int TPB>
+template <int VEC, bool NT, bool BIG, bool PLDS, int TPB, bool PF2 = false>
 __global__ __launch_bounds__(TPB) void mix_kernel_wide(float* const* __restrict__ seg_ptrs,
                                                         const int64_t* __restrict__ seg_len,
                                                         const int64_t* __restrict__ tile_off,
@@ -710,106 +712,140 @@ __global__ __launch_bounds__(TPB) void mix_kernel_wide(float* const* __restrict_
     auto needed = [&](int k) {
         return k < n_local ? (deg[k] > 0 || idle) : (k - n_local < n_remote);
     };
-    F R[NR];
-    auto stage = [&](const Geo& g) {
+    F RS[PF2 ? 2 : 1][NR];
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, PF2 ? 1 : 0>;
+    auto stage_to = [&](auto setc, const Geo& g) {
+        constexpr int S = decltype(setc)::value;
 #pragma unroll
         for (int j = 0; j < NR; ++j) {
             const int k = wave + WV * j;                    // wave-uniform slot
             if (j < nj && k < n_slots && needed(k)) {
                 const int64_t c = g.col0 + (int64_t)lane * VEC;
                 if (g.vec_ok && c + VEC <= g.lim) {
-                    R[j] = ld<NT, F>(g.ptrs[k] + c);
+                    RS[S][j] = ld<NT, F>(g.ptrs[k] + c);
                 } else {
 #pragma unroll
-                    for (int t = 0; t < VEC; ++t) R[j][t] = (c + t < g.lim) ? ld1(g.ptrs[k] + c + t) : 0.0f;
+                    for (int t = 0; t < VEC; ++t) RS[S][j][t] = (c + t < g.lim) ? ld1(g.ptrs[k] + c + t) : 0.0f;
                 }
             }
         }
     };
-    int64_t wi = blockIdx.x;
-    if (wi >= work) return;
-    Geo cur = geo(wi);
-    stage(cur);
-    for (; wi < work; wi += gridDim.x) {
+    auto park = [&](auto setc) {
+        constexpr int S = decltype(setc)::value;
 #pragma unroll
         for (int j = 0; j < NR; ++j) {
             const int k = wave + WV * j;
-            if (j < nj && k < n_slots && needed(k)) wlds[k * 64 + lane] = R[j];
+            if (j < nj && k < n_slots && needed(k)) wlds[k * 64 + lane] = RS[S][j];
         }
-        __syncthreads();
-        Geo nxt = cur;
-        if (wi + gridDim.x < work) {           // the next piece's loads fly while this one is mixed
-            nxt = geo(wi + gridDim.x);
-            stage(nxt);
-        }
-        // this wave's rows in pairs (r, r + WV): the two partner walks interleaved, two partners per
-        // step, so four slot reads and four piece reads are in flight at once (no branch between
-        // them); each row's FMA order is unchanged (partners in matching order, then the self term)
-        const int64_t c = cur.col0 + (int64_t)lane * VEC;
-        const bool vok = cur.vec_ok && c + VEC <= cur.lim;
-        auto finish = [&](int r, F acc) {
-            const F xs = wlds[r * 64 + lane];
-            const float s = sw[r];
-#pragma unroll
-            for (int t = 0; t < VEC; ++t) acc[t] = __builtin_fmaf(s, xs[t], acc[t]);
-            if (c < cur.lim) store_one<VEC, NT>(cur.ptrs[r], c, cur.lim, vok, acc);
-        };
-        auto tail = [&](const int32_t* sr, int e, int d, F& acc) {
-            for (; e + 2 <= d; e += 2) {
-                const int s0 = __builtin_amdgcn_readfirstlane(sr[e]);
-                const int s1 = __builtin_amdgcn_readfirstlane(sr[e + 1]);
-                const F x0 = wlds[s0 * 64 + lane];
-                const F x1 = wlds[s1 * 64 + lane];
-#pragma unroll
-                for (int t = 0; t < VEC; ++t) acc[t] = __builtin_fmaf(alpha, x0[t], acc[t]);
-#pragma unroll
-                for (int t = 0; t < VEC; ++t) acc[t] = __builtin_fmaf(alpha, x1[t], acc[t]);
-            }
-            if (e < d) {
-                const F x0 = wlds[__builtin_amdgcn_readfirstlane(sr[e]) * 64 + lane];
-#pragma unroll
-                for (int t = 0; t < VEC; ++t) acc[t] = __builtin_fmaf(alpha, x0[t], acc[t]);
-            }
-        };
-        for (int ra = wave; ra < n_local; ra += 2 * WV) {
-            const int rb = ra + WV;
-            const bool hb = rb < n_local;
-            const int da = __builtin_amdgcn_readfirstlane(deg[ra]);
-            const int db = hb ? __builtin_amdgcn_readfirstlane(deg[rb]) : 0;
-            const int32_t* sa = src + (int64_t)ra * M;
-            const int32_t* sb = src + (int64_t)rb * M;
-            F a, b;
-#pragma unroll
-            for (int t = 0; t < VEC; ++t) a[t] = b[t] = 0.0f;
-            const int dm = da < db ? da : db;
-            int e = 0;
-            for (; e + 2 <= dm; e += 2) {
-                const int a0 = __builtin_amdgcn_readfirstlane(sa[e]);
-                const int a1 = __builtin_amdgcn_readfirstlane(sa[e + 1]);
-                const int b0 = __builtin_amdgcn_readfirstlane(sb[e]);
-                const int b1 = __builtin_amdgcn_readfirstlane(sb[e + 1]);
-                const F xa0 = wlds[a0 * 64 + lane];
-                const F xa1 = wlds[a1 * 64 + lane];
-                const F xb0 = wlds[b0 * 64 + lane];
-                const F xb1 = wlds[b1 * 64 + lane];
-#pragma unroll
-                for (int t = 0; t < VEC; ++t) {
-                    a[t] = __builtin_fmaf(alpha, xa0[t], a[t]);
-                    b[t] = __builtin_fmaf(alpha, xb0[t], b[t]);
+    };
+    auto mix_piece = [&](const Geo& cur) {
+            // this wave's rows in pairs (r, r + WV): the two partner walks interleaved, two partners per
+            // step, so four slot reads and four piece reads are in flight at once (no branch between
+            // them); each row's FMA order is unchanged (partners in matching order, then the self term)
+            const int64_t c = cur.col0 + (int64_t)lane * VEC;
+            const bool vok = cur.vec_ok && c + VEC <= cur.lim;
+            auto finish = [&](int r, F acc) {
+                const F xs = wlds[r * 64 + lane];
+                const float s = sw[r];
+    #pragma unroll
+                for (int t = 0; t < VEC; ++t) acc[t] = __builtin_fmaf(s, xs[t], acc[t]);
+                if (c < cur.lim) store_one<VEC, NT>(cur.ptrs[r], c, cur.lim, vok, acc);
+            };
+            auto tail = [&](const int32_t* sr, int e, int d, F& acc) {
+                for (; e + 2 <= d; e += 2) {
+                    const int s0 = __builtin_amdgcn_readfirstlane(sr[e]);
+                    const int s1 = __builtin_amdgcn_readfirstlane(sr[e + 1]);
+                    const F x0 = wlds[s0 * 64 + lane];
+                    const F x1 = wlds[s1 * 64 + lane];
+    #pragma unroll
+                    for (int t = 0; t < VEC; ++t) acc[t] = __builtin_fmaf(alpha, x0[t], acc[t]);
+    #pragma unroll
+                    for (int t = 0; t < VEC; ++t) acc[t] = __builtin_fmaf(alpha, x1[t], acc[t]);
                 }
-#pragma unroll
-                for (int t = 0; t < VEC; ++t) {
-                    a[t] = __builtin_fmaf(alpha, xa1[t], a[t]);
-                    b[t] = __builtin_fmaf(alpha, xb1[t], b[t]);
+                if (e < d) {
+                    const F x0 = wlds[__builtin_amdgcn_readfirstlane(sr[e]) * 64 + lane];
+    #pragma unroll
+                    for (int t = 0; t < VEC; ++t) acc[t] = __builtin_fmaf(alpha, x0[t], acc[t]);
                 }
+            };
+            for (int ra = wave; ra < n_local; ra += 2 * WV) {
+                const int rb = ra + WV;
+                const bool hb = rb < n_local;
+                const int da = __builtin_amdgcn_readfirstlane(deg[ra]);
+                const int db = hb ? __builtin_amdgcn_readfirstlane(deg[rb]) : 0;
+                const int32_t* sa = src + (int64_t)ra * M;
+                const int32_t* sb = src + (int64_t)rb * M;
+                F a, b;
+    #pragma unroll
+                for (int t = 0; t < VEC; ++t) a[t] = b[t] = 0.0f;
+                const int dm = da < db ? da : db;
+                int e = 0;
+                for (; e + 2 <= dm; e += 2) {
+                    const int a0 = __builtin_amdgcn_readfirstlane(sa[e]);
+                    const int a1 = __builtin_amdgcn_readfirstlane(sa[e + 1]);
+                    const int b0 = __builtin_amdgcn_readfirstlane(sb[e]);
+                    const int b1 = __builtin_amdgcn_readfirstlane(sb[e + 1]);
+                    const F xa0 = wlds[a0 * 64 + lane];
+                    const F xa1 = wlds[a1 * 64 + lane];
+                    const F xb0 = wlds[b0 * 64 + lane];
+                    const F xb1 = wlds[b1 * 64 + lane];
+    #pragma unroll
+                    for (int t = 0; t < VEC; ++t) {
+                        a[t] = __builtin_fmaf(alpha, xa0[t], a[t]);
+                        b[t] = __builtin_fmaf(alpha, xb0[t], b[t]);
+                    }
+    #pragma unroll
+                    for (int t = 0; t < VEC; ++t) {
+                        a[t] = __builtin_fmaf(alpha, xa1[t], a[t]);
+                        b[t] = __builtin_fmaf(alpha, xb1[t], b[t]);
+                    }
+                }
+                tail(sa, e, da, a);
+                tail(sb, e, db, b);
+                if (da > 0 || idle) finish(ra, a);
+                if (hb && (db > 0 || idle)) finish(rb, b);
             }
-            tail(sa, e, da, a);
-            tail(sb, e, db, b);
-            if (da > 0 || idle) finish(ra, a);
-            if (hb && (db > 0 || idle)) finish(rb, b);
+    };
+    int64_t wi = blockIdx.x;
+    if (wi >= work) return;
+    Geo cur = geo(wi);
+    stage_to(I0{}, cur);
+    if constexpr (!PF2) {
+        for (; wi < work; wi += gridDim.x) {
+            park(I0{});
+            __syncthreads();
+            Geo nxt = cur;
+            if (wi + gridDim.x < work) {       // the next piece's loads fly while this one is mixed
+                nxt = geo(wi + gridDim.x);
+                stage_to(I0{}, nxt);
+            }
+            mix_piece(cur);
+            __syncthreads();                  // the piece is read by every wave before restaging
+            cur = nxt;
         }
-        __syncthreads();                      // the piece is read by every wave before restaging
-        cur = nxt;
+    } else {
+        // piece i in register set i % 2; after it is parked in LDS the set takes piece i + 2
+        Geo cur2 = cur;
+        if (wi + gridDim.x < work) {
+            cur2 = geo(wi + gridDim.x);
+            stage_to(I1{}, cur2);
+        }
+        auto step = [&](auto setc, Geo& gi, int64_t w) {
+            park(setc);
+            __syncthreads();
+            const Geo here = gi;
+            if (w + 2 * (int64_t)gridDim.x < work) {
+                gi = geo(w + 2 * (int64_t)gridDim.x);
+                stage_to(setc, gi);
+            }
+            mix_piece(here);
+            __syncthreads();
+        };
+        for (; wi < work; wi += 2 * (int64_t)gridDim.x) {
+            step(I0{}, cur, wi);
+            if (wi + gridDim.x < work) step(I1{}, cur2, wi + gridDim.x);
+        }
     }
 }
 
@@ -851,7 +887,8 @@ struct Tune {
                          // the persistent grid), 1 / 2 / 4 = forced (capped by the geometry)
     int wide_lds_kb = 158;  // wide kernel (65-156 slots): LDS per piece (KB); more -> wider pieces, fewer WGs per CU
     int rows_tpb = 256;     // row kernel, 32-64 slots (unsplit tiles): workgroup size 256 / 512 / 1024
-    int wide_tpb = 1024;    // wide kernel: workgroup size (256 / 512 / 1024)
+    int wide_tpb = 1024;
+    int wide_pf2 = 1;       // wide kernel, 1024 threads: two pieces' loads in flight (two register sets)    // wide kernel: workgroup size (256 / 512 / 1024)
     int wide_per_cu = 0;    // wide kernel: workgroups per CU cap (0 = 4; fewer when the LDS does not fit)
     int wide_plan_lds = 1;  // wide kernel: the plan record in LDS (when <= 32 KB) instead of global loads
     int rows_pf2 = 2;    // row kernel, persistent grids of 32-64 slots: two tiles' loads in flight -- 1 on,
@@ -1011,6 +1048,9 @@ extern "C" int mx_mix_set(const char* key, int value) {
     } else if (!strcmp(key, "rows_tpb")) {
         MX_CHECK(value == 256 || value == 512 || value == 1024, "mx_mix_set: rows_tpb %d", value);
         slot = &g_tune.rows_tpb;
+    } else if (!strcmp(key, "wide_pf2")) {
+        MX_CHECK(value == 0 || value == 1, "mx_mix_set: wide_pf2 %d", value);
+        slot = &g_tune.wide_pf2;
     } else if (!strcmp(key, "wide_tpb")) {
         MX_CHECK(value == 256 || value == 512 || value == 1024, "mx_mix_set: wide_tpb %d", value);
         slot = &g_tune.wide_tpb;
@@ -1061,6 +1101,7 @@ extern "C" int mx_mix_get(const char* key) {
     if (!strcmp(key, "wide_plan_lds")) return g_tune.wide_plan_lds;
     if (!strcmp(key, "wide_per_cu")) return g_tune.wide_per_cu;
     if (!strcmp(key, "wide_tpb")) return g_tune.wide_tpb;
+    if (!strcmp(key, "wide_pf2")) return g_tune.wide_pf2;
     if (!strcmp(key, "rows_tpb")) return g_tune.rows_tpb;
     if (!strcmp(key, "ns48")) return g_ns48;
     mx::set_error("mx_mix_get: unknown key '%s'", key);
@@ -1185,23 +1226,24 @@ int gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev, const int
         const bool nt = g_tune.nontemporal != 0;
         const bool big = (vec == 4 && n_slots > 40) || (vec == 2 && n_slots > 80);
         MX_CHECK(n_slots <= (big || vec == 1 ? kWideMaxSlots : vec == 4 ? 40 : 80), "mx_gossip_mix: wide staging");
-#define MX_WIDE1(V, N, B, PL, T)                                                                               \
+#define MX_WIDE1(V, N, B, PL, T, F2)                                                                           \
     do {                                                                                                      \
         static bool big_lds = false;          /* once per instantiation: the most the kernel may ask */   \
         if (lds > 64 * 1024 && !big_lds) {                                                                    \
-            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(mix_kernel_wide<V, N, B, PL, T>),         \
+            (void)hipFuncSetAttribute(reinterpret_cast<const void*>(mix_kernel_wide<V, N, B, PL, T, F2>),     \
                                       hipFuncAttributeMaxDynamicSharedMemorySize, 158 * 1024);               \
             big_lds = true;                                                                                   \
         }                                                                                                     \
-        hipLaunchKernelGGL((mix_kernel_wide<V, N, B, PL, T>), dim3((unsigned)(grid < 1 ? 1 : grid)), dim3(T),  \
-                           lds, st, seg_ptrs_dev, seg_len_dev, tile_off_dev, seg_vec_dev, nseg, total_tiles,  \
-                           tile_cols, n_slots, plan_dev, iter, iter_dev, n_local, M, alpha);                  \
+        hipLaunchKernelGGL((mix_kernel_wide<V, N, B, PL, T, F2>), dim3((unsigned)(grid < 1 ? 1 : grid)),      \
+                           dim3(T), lds, st, seg_ptrs_dev, seg_len_dev, tile_off_dev, seg_vec_dev, nseg,      \
+                           total_tiles, tile_cols, n_slots, plan_dev, iter, iter_dev, n_local, M, alpha);     \
     } while (0)
 #define MX_WIDE2(V, N, B, PL)                                                                                 \
     do {                                                                                                      \
-        if (tpb == 1024) MX_WIDE1(V, N, B, PL, 1024);                                                        \
-        else if (tpb == 512) MX_WIDE1(V, N, B, PL, 512);                                                     \
-        else MX_WIDE1(V, N, B, PL, 256);                                                                     \
+        if (tpb == 1024 && g_tune.wide_pf2) MX_WIDE1(V, N, B, PL, 1024, true);                               \
+        else if (tpb == 1024) MX_WIDE1(V, N, B, PL, 1024, false);                                            \
+        else if (tpb == 512) MX_WIDE1(V, N, B, PL, 512, false);                                              \
+        else MX_WIDE1(V, N, B, PL, 256, false);                                                              \
     } while (0)
 #define MX_WIDE(V, N, B)                                                                                      \
     do {                                                                                                      \

@@ -138,6 +138,7 @@ int mx_mix_tile(int n_slots);
  *                  1024 -- the tile's items dealt to 4 / 8 / 16 waves (measured neutral, r3)
  *   wide_tpb       wide kernel: workgroup size 256 / 512 / 1024 (default 1024: 16 waves walk the rows of
  *                  one staged piece)
+ *   wide_pf2       wide kernel, 1024-thread workgroups: two pieces' loads in flight (default 1)
  *   wide_lds_kb    wide kernel: LDS budget per staged piece, 8-158 KB (default 158: 64 x 4 columns of
  *                  every slot up to 156 slots); smaller -> narrower pieces, more workgroups per CU
  *   wide_per_cu    wide kernel: workgroups per CU cap, 0 = auto (LDS- and wave-limited, <= 4)

@@ -142,16 +142,18 @@ def test_er64_shares_slot_classes(pkg, O, nranks, P, ns48, pf2, tpb):
         pkg.engine.set_mix_tuning(**saved)
 
 
-@pytest.mark.parametrize("lds_kb,plan_lds,tpb,nt", [(40, 0, 256, 2), (80, 1, 256, 2), (158, 1, 256, 2),
-                                                    (158, 0, 256, 2), (40, 1, 1024, 2), (158, 1, 1024, 2),
-                                                    (80, 0, 512, 2), (40, 1, 512, 2), (158, 1, 1024, 0),
-                                                    (40, 1, 256, 0)])
+@pytest.mark.parametrize("lds_kb,plan_lds,tpb,nt,pf2", [(40, 0, 256, 2, 0), (80, 1, 256, 2, 0), (158, 1, 256, 2, 0),
+                                                        (158, 0, 256, 2, 0), (40, 1, 1024, 2, 0), (158, 1, 1024, 2, 0),
+                                                        (80, 0, 512, 2, 0), (40, 1, 512, 2, 0), (158, 1, 1024, 0, 0),
+                                                        (40, 1, 256, 0, 0), (158, 1, 1024, 2, 1), (80, 0, 1024, 0, 1),
+                                                        (40, 1, 1024, 2, 1)])
 @pytest.mark.parametrize("n,p,seed,P", [(96, 0.06, 1, 9_001), (150, 0.04, 3, 3_001), (72, 0.08, 6, 70_003)])
-def test_wide_lds_budget(pkg, O, n, p, seed, P, lds_kb, plan_lds, tpb, nt):
+def test_wide_lds_budget(pkg, O, n, p, seed, P, lds_kb, plan_lds, tpb, nt, pf2):
     """mix_kernel_wide with a bigger LDS budget per piece (mx_mix_set "wide_lds_kb"): 128- / 256-column
     pieces of every slot (VEC 2 / 4 past 40 / 80 slots, fewer workgroups per CU), and with the plan
     record read from global memory instead of LDS ("wide_plan_lds" 0), and with 512 / 1024-thread
-    workgroups ("wide_tpb"), and with ordinary instead of streaming accesses; 4 MATCHA-like rounds,
+    workgroups ("wide_tpb"), with ordinary instead of streaming accesses, and with two pieces' loads
+    in flight ("wide_pf2"); 4 MATCHA-like rounds,
     ragged P, bit-exact vs the oracle."""
     partner = _er(pkg, n, p, seed)
     M = partner.shape[0]
@@ -160,7 +162,7 @@ def test_wide_lds_budget(pkg, O, n, p, seed, P, lds_kb, plan_lds, tpb, nt):
     flags[0] = 1
     topo = Topo(partner, 0.5 / M, flags)
     saved = pkg.engine.mix_tuning()
-    pkg.engine.set_mix_tuning(wide_lds_kb=lds_kb, wide_plan_lds=plan_lds, wide_tpb=tpb, nontemporal=nt)
+    pkg.engine.set_mix_tuning(wide_lds_kb=lds_kb, wide_plan_lds=plan_lds, wide_tpb=tpb, nontemporal=nt, wide_pf2=pf2)
     try:
         grp = pkg.VirtualWorkerGroup(topo, numel=P)
         X = np.stack([O.synth(23 * seed + i, P) for i in range(n)])
