@@ -887,8 +887,8 @@ struct Tune {
                          // the persistent grid), 1 / 2 / 4 = forced (capped by the geometry)
     int wide_lds_kb = 158;  // wide kernel (65-156 slots): LDS per piece (KB); more -> wider pieces, fewer WGs per CU
     int rows_tpb = 256;     // row kernel, 32-64 slots (unsplit tiles): workgroup size 256 / 512 / 1024
-    int wide_tpb = 1024;
-    int wide_pf2 = 1;       // wide kernel, 1024 threads: two pieces' loads in flight (two register sets)    // wide kernel: workgroup size (256 / 512 / 1024)
+    int wide_tpb = 1024;    // wide kernel: workgroup size (256 / 512 / 1024)
+    int wide_pf2 = 1;       // wide kernel, 1024 threads: two pieces' loads in flight (two register sets)
     int wide_per_cu = 0;    // wide kernel: workgroups per CU cap (0 = 4; fewer when the LDS does not fit)
     int wide_plan_lds = 1;  // wide kernel: the plan record in LDS (when <= 32 KB) instead of global loads
     int rows_pf2 = 2;    // row kernel, persistent grids of 32-64 slots: two tiles' loads in flight -- 1 on,
