@@ -37,6 +37,7 @@ SIGNATURES = {
     "mx_iter_expand": (c_int, [c_p, c_p, c_int, c_p]),
     "mx_topk_set": (c_int, [ctypes.c_char_p, c_i64]),
     "mx_topk_get": (c_i64, [ctypes.c_char_p]),
+    "mx_topk_check": (c_int, [c_p, c_i64, c_int, c_i64, c_p]),
     "mx_topk_abs_diff": (c_int, [c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p]),
     "mx_topk_abs_diff_rows": (c_int, [c_p, c_p, c_i64, c_int, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_p]),
     "mx_choco_msg_bytes": (c_i64, [c_i64, c_i64]),
@@ -50,6 +51,8 @@ SIGNATURES = {
     "mx_rccl_init_timeout": (c_int, [c_p, c_int, c_int, c_i64, c_p, c_p]),
     "mx_rccl_abort": (c_int, [c_p]),
     "mx_rccl_destroy": (c_int, [c_p]),
+    "mx_rccl_count": (c_int, [c_p, c_p]),
+    "mx_rccl_wait": (c_int, [c_p, c_p, c_i64]),
     "mx_exchange_plan": (c_int, [c_p, c_int, c_p, c_int, c_p, c_int, c_int, c_int, c_p, c_int, c_p]),
     "mx_exchange_post": (c_int, [c_p, c_p, c_int, c_p, c_int, c_p, c_i64, c_i64, c_p]),
     "mx_exchange_round": (c_int, [c_p, c_p, c_int, c_p, c_int, c_p, c_int, c_int, c_int, c_p, c_p, c_i64,
@@ -58,8 +61,11 @@ SIGNATURES = {
     "mx_allreduce_mean_ordered": (c_int, [c_p, c_p, c_i64, c_p, c_int, c_p]),
     "mx_allgather": (c_int, [c_p, c_p, c_i64, c_p, c_p]),
     "mx_mean_rows": (c_int, [c_p, c_int, c_i64, c_i64, c_int, c_p, c_p]),
+    "mx_mean_rows_to": (c_int, [c_p, c_int, c_i64, c_i64, c_int, c_p, c_int, c_i64, c_p]),
     "mx_synth_fill": (c_int, [c_p, c_i64, c_u64, c_p]),
     "mx_max_weight_matching": (c_int, [c_int, c_p, c_p, c_p, c_int, c_p, c_p, c_p]),
+    "mx_snapshot_publish": (c_int, [c_p, c_p, c_i64, c_p]),
+    "mx_plan_set_peer_reads": (c_int, [c_p, c_i64, c_int, c_int, c_int, c_p]),
     "mx_ipc_handle_bytes": (c_int, []),
     "mx_ipc_alloc": (c_int, [c_i64, c_p, c_p]),
     "mx_ipc_open": (c_int, [c_p, c_p]),

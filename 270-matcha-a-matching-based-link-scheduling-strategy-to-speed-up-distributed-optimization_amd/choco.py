@@ -12,7 +12,7 @@ import numpy as np
 import torch
 
 from ._lib import check, lib, require_device, stream_ptr
-from .engine import GossipEngine, PullTransport, ROW_ALIGN, default_comm, owner_table, partition
+from .engine import GossipEngine, PullTransport, ROW_ALIGN, default_comm, owner_table, partition, wait_round
 
 
 def topk_count(P, ratio):
@@ -98,6 +98,12 @@ class ChocoWorkerGroup:
                                         self.bnd_off, self.work.data_ptr(), self.work_ld, stream_ptr(stream)),
               "mx_topk_abs_diff_rows")
 
+    def check_topk(self, stream=None):
+        """Synchronise and raise MXError if a top-k row barrier's bounded wait expired since the
+        last check (mx_topk_check: that round's messages are undefined; never a GPU hang)."""
+        check(lib.mx_topk_check(self.work.data_ptr(), self.work_ld, self.n_local, self.numel, stream_ptr(stream)),
+              "mx_topk_check")
+
     def average(self, it, stream=None):
         """averaging (communicator.py:200-230): receive partner messages ([N > 1] over the
         transport into the message slots after the local ones), then the s / x_hat scatters and
@@ -168,5 +174,7 @@ class ChocoWorkerGroup:
         torch.cuda.synchronize()
         tic = time.time()
         self.step(it)
-        torch.cuda.synchronize()
-        return time.time() - tic
+        wait_round(self.engine.comm)
+        toc = time.time()
+        self.check_topk()
+        return toc - tic

@@ -25,7 +25,7 @@ import torch
 from ._lib import check, lib, require_device, stream_ptr
 from .choco import ChocoWorkerGroup
 from .comm_helpers import flatten_tensors, unflatten_tensors
-from .engine import VirtualWorkerGroup, default_comm
+from .engine import VirtualWorkerGroup, default_comm, wait_round
 
 
 def _same_params(model, params):
@@ -257,8 +257,11 @@ class decenCommunicator(Communicator):
             self._model_params = None
 
     def __del__(self):
+        # a pull group's close() is collective (a barrier): never from a finalizer -- its IPC
+        # buffers go with the process
         try:
-            self.close()
+            if self._group is not None and not self._group.pulls:
+                self.close()
         except Exception:                        # interpreter teardown: nothing left to release
             pass
 
@@ -274,7 +277,7 @@ class decenCommunicator(Communicator):
         torch.cuda.synchronize()
         tic = time.time()
         self._group.step(it)
-        torch.cuda.synchronize()
+        wait_round(self._group.engine.comm)
         toc = time.time()
         self._stage.store()
         return toc - tic
@@ -335,7 +338,7 @@ class ChocoCommunicator(Communicator):
         torch.cuda.synchronize()
         tic = time.time()
         self._group.step(it)
-        torch.cuda.synchronize()
+        wait_round(self._group.engine.comm)
         toc = time.time()
         self._stage.store()
         return toc - tic
@@ -400,7 +403,7 @@ class centralizedCommunicator(Communicator):
         tic = time.time()
         if self.size > 1 and flat.numel():
             self._average(flat)
-        torch.cuda.synchronize()
+        wait_round(self._comm())
         toc = time.time()
         with torch.no_grad():
             for f, t in zip(unflatten_tensors(flat, tensors), tensors):

@@ -40,5 +40,7 @@ def get_top_k(x, ratio):
         check(lib.mx_topk_abs_diff(x_data.data_ptr(), None, P, k, vals.data_ptr(), idx.data_ptr(),
                                    work.data_ptr(), stream_ptr()), "mx_topk_abs_diff")
     if host:
+        # the host copy synchronises anyway: also confirm no bounded row-barrier wait expired
+        check(lib.mx_topk_check(work.data_ptr(), 0, 1, P, stream_ptr()), "mx_topk_check")
         return vals.to(x.device), idx.to(x.device)
     return vals, idx

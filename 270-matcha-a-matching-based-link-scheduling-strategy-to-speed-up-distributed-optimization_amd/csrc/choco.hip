@@ -777,16 +777,21 @@ __global__ __launch_bounds__(kTPB) void compact_wave_kernel(Rows R, int64_t S, d
 // Every block of this row's grid has arrived (rare path only: the fallback compaction inside the
 // first candidate pass).  Producers: every wave's stores drained and released at agent scope, then
 // one arrival per block on the row's counter; the poller's agent-scope acquire then covers the
-// workgroup behind the barrier.  The grid of that pass is a few hundred blocks per row, far below
-// what the chip holds at once, so every block of a row is resident while it waits.
+// workgroup behind the barrier.  A grid barrier needs every block of the row co-resident: the host
+// caps this pass's grid (all rows together) at 7/8 of what the chip holds of this kernel at once
+// (occupancy query x CUs; the margin leaves room for e.g. RCCL's kernels beside it, N > 1), and
+// the wait itself is BOUNDED: past kSpinTicks (~2.7 s) the row's sticky `err` word is set and the
+// block goes on (the row's output is then undefined, never a hang; mx_topk_check reports it).
 __device__ void row_grid_barrier(SelState* st, unsigned blocks) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __hip_atomic_fetch_add(&st->bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        while (__hip_atomic_load(&st->bar, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < blocks)
-            __builtin_amdgcn_s_sleep(4);
+        if (!wait_count(&st->bar, blocks)) st_sc1(&st->err, 1u);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     __syncthreads();
 }
@@ -1763,6 +1768,9 @@ int g_cand_chunks = 0;        // chunk regions per wave of cand_hist / cand_mark
                               // flush of cand_hist<10>'s 1024 bins measured +3.7 us on one row; same-box
                               // sweep 2 -> 4 / 8: one row 121.7 -> 119.6 us, 8 rows 655 -> 640 us)
 
+unsigned g_hist_grid = 0;      // the last call's cand_hist<10> grid per row, and the co-resident cap it
+unsigned g_hist_capacity = 0;  // was held to (blocks of that instantiation the chip holds, x 7/8): mx_topk_get
+
 int g_select = 0;             // selection after the compaction: 0 = the four passes (cand_hist<10>,
                               // cand_hist<9>, cand_mark, write_cand), 1 = one launch (select_kernel; same-box
                               // A/B: one row 100.6 -> 103.9 us, 8 rows 608 -> 638 us per round, not the default)
@@ -1784,6 +1792,24 @@ int select_capacity() {
         cached[dev] = cus / 2;
     }
     return cached[dev];
+}
+
+// blocks of a cand_hist<10> instantiation the chip holds at once, x 7/8 (room for a neighbour
+// kernel such as RCCL's at N > 1), per device and instantiation
+int64_t hist_capacity(const void* fn) {
+    struct Entry { int dev; const void* fn; int64_t cap; };
+    static Entry cache[32];
+    static int used = 0;
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    for (int i = 0; i < used; ++i)
+        if (cache[i].dev == dev && cache[i].fn == fn) return cache[i].cap;
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kTPB, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus < 1) cus = 1;
+    const int64_t cap = (int64_t)per_cu * cus * 7 / 8 > 0 ? (int64_t)per_cu * cus * 7 / 8 : 1;
+    if (used < 32) cache[used++] = Entry{dev, fn, cap};
+    return cap;
 }
 
 int64_t sample_stride(int64_t P) {
@@ -1879,6 +1905,8 @@ extern "C" int64_t mx_topk_get(const char* key) {
     if (key && !strcmp(key, "select")) return g_select;
     if (key && !strcmp(key, "select_blocks")) return g_select_blocks;
     if (key && !strcmp(key, "select_trace")) return g_select_trace;
+    if (key && !strcmp(key, "hist_grid")) return g_hist_grid;
+    if (key && !strcmp(key, "hist_capacity")) return g_hist_capacity;
     mx::set_error("mx_topk_get: unknown key '%s'", key ? key : "(null)");
     return MX_ERR_INVALID;
 }
@@ -1956,15 +1984,54 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
         }
         return MX_OK;
     }
-    // the fallback compaction (S > 1, rare) runs inside the first candidate pass
+    // the fallback compaction (S > 1, rare) runs inside the first candidate pass, behind a row grid
+    // barrier: that pass's blocks (every row's) must all be resident at once, so with sampling its
+    // grid is capped at 7/8 of the chip's capacity for the instantiation (occupancy query, cached)
     auto h10 = nrows == 1 ? (g_compact_store ? cand_hist<kMidBits, true, true> : cand_hist<kMidBits, true, false>)
                           : (g_compact_store ? cand_hist<kMidBits, false, true> : cand_hist<kMidBits, false, false>);
-    MX_L(h10, dim3(cgrid, nrows), kTPB, S, frac);
+    unsigned hgrid = cgrid;
+    if (S > 1) {
+        const int64_t cap = hist_capacity(reinterpret_cast<const void*>(h10));
+        MX_CHECK(cap >= nrows, "mx_topk_abs_diff_rows: %d rows exceed the %lld co-resident blocks of the candidate "
+                 "pass (its sampled-floor fallback needs every block of a row resident)", nrows, (long long)cap);
+        if ((int64_t)hgrid * nrows > cap) hgrid = (unsigned)(cap / nrows);
+        g_hist_capacity = (unsigned)cap;
+    } else {
+        g_hist_capacity = 0;
+    }
+    g_hist_grid = hgrid;
+    MX_L(h10, dim3(hgrid, nrows), kTPB, S, frac);
     MX_L((cand_hist<kLowBits, false, false>), dim3(cgrid, nrows), kTPB, S, frac);
     const int64_t G = (nc + cgrid - 1) / cgrid;    // chunks per cand_mark block
     MX_L(cand_mark, dim3(cgrid, nrows), kTPB, G);
     MX_L(write_cand, dim3(wgrid, nrows), kTPB, G);
 #undef MX_L
+    return MX_OK;
+}
+
+// The rows' sticky error words (a bounded row-barrier wait that expired: the sampled-floor fallback
+// in cand_hist<10>, or select_kernel): synchronises `stream`, reads and clears them.
+extern "C" int mx_topk_check(void* work, int64_t work_ld_bytes, int nrows, int64_t P, void* stream) {
+    MX_CHECK(work && nrows >= 1 && P >= 1 && (nrows == 1 || work_ld_bytes >= (int64_t)layout(P).total),
+             "mx_topk_check: bad arguments");
+    hipStream_t st = mx::as_stream(stream);
+    MX_HIP(hipStreamSynchronize(st));
+    const size_t off = layout(P).state + offsetof(SelState, err);
+    int bad = -1;
+    for (int r = 0; r < nrows; ++r) {
+        char* p = static_cast<char*>(work) + (int64_t)r * work_ld_bytes + off;
+        uint32_t e = 0;
+        MX_HIP(hipMemcpy(&e, p, sizeof(e), hipMemcpyDeviceToHost));
+        if (e) {
+            if (bad < 0) bad = r;
+            MX_HIP(hipMemset(p, 0, sizeof(e)));
+        }
+    }
+    if (bad >= 0) {
+        mx::set_error("mx_topk: a row barrier's bounded wait expired (row %d): not every block of the row was "
+                      "resident; that call's output is undefined", bad);
+        return MX_ERR_HIP;
+    }
     return MX_OK;
 }
 

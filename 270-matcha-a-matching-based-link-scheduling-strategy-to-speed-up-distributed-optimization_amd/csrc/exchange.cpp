@@ -127,12 +127,61 @@ extern "C" int mx_rccl_init_timeout(const void* id, int nranks, int rank, int64_
         *comm_out = comm;
         return MX_OK;
     }
+    if (comm) (void)ncclCommAbort(comm);          // a half-built communicator is not leaked
     mx::set_error("mx_rccl_init: ncclCommInitRankConfig(blocking = 0) -> %s", ncclGetErrorString(r));
     return MX_ERR_RCCL;
 }
 
 extern "C" int mx_rccl_init(const void* id, int nranks, int rank, void** comm_out) {
     return mx_rccl_init_timeout(id, nranks, rank, env_timeout_ms(), comm_out, nullptr);
+}
+
+extern "C" int mx_rccl_count(void* comm, int* nranks_out) {
+    MX_CHECK(comm && nranks_out, "mx_rccl_count: null pointer");
+    MX_NCCL(ncclCommCount(reinterpret_cast<ncclComm_t>(comm), nranks_out));
+    return MX_OK;
+}
+
+// The deadlines above cover getting an operation ENQUEUED (a peer that never joins an init or a
+// group's connection setup).  Once the point-to-point connections exist, a peer that dies or skips
+// an exchange leaves the RCCL kernel waiting on the GPU, and the hang would surface at the next
+// stream / event synchronisation, which has no limit.  mx_rccl_wait is that synchronisation with
+// the deadline: an event recorded on `stream` behind everything enqueued so far, polled
+// (hipEventQuery) until it completes or timeout_ms passes; on expiry the communicator is aborted
+// (ncclCommAbort: its kernels see the abort flag and exit, the stream drains) and MX_ERR_RCCL
+// "timed out" is returned -- the caller must not use the communicator again.
+extern "C" int mx_rccl_wait(void* comm, void* stream, int64_t timeout_ms) {
+    MX_CHECK(comm, "mx_rccl_wait: null communicator");
+    if (timeout_ms <= 0) timeout_ms = g_op_timeout_ms.load();
+    hipEvent_t ev;
+    MX_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    hipError_t e = hipEventRecord(ev, mx::as_stream(stream));
+    if (e != hipSuccess) {
+        (void)hipEventDestroy(ev);
+        mx::set_error("mx_rccl_wait: hipEventRecord -> %s", hipGetErrorString(e));
+        return MX_ERR_HIP;
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int spin = 0;; ++spin) {
+        e = hipEventQuery(ev);
+        if (e != hipErrorNotReady) break;
+        const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
+        if (ms >= timeout_ms) {
+            (void)ncclCommAbort(reinterpret_cast<ncclComm_t>(comm));
+            (void)hipEventSynchronize(ev);      // the aborted kernels have left the stream
+            (void)hipEventDestroy(ev);
+            mx::set_error("mx_rccl_wait: the stream did not drain within %lld ms (a peer rank died or skipped an "
+                          "exchange); the communicator was aborted", (long long)timeout_ms);
+            return MX_ERR_RCCL;
+        }
+        if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(spin > 4096 ? 1000 : 20));
+    }
+    (void)hipEventDestroy(ev);
+    if (e != hipSuccess) {
+        mx::set_error("mx_rccl_wait: hipEventQuery -> %s", hipGetErrorString(e));
+        return MX_ERR_HIP;
+    }
+    return MX_OK;
 }
 
 extern "C" int mx_rccl_abort(void* comm) {
@@ -330,6 +379,61 @@ __global__ __launch_bounds__(256) void mean_rows_kernel(const float* rows, int n
     }
 }
 
+// mean_rows_kernel with the mean written to ndst destination rows (dst + d * dst_ld) instead of
+// one: the all-reduce of centralizedCommunicator for workers held as rows of one arena (every
+// worker's row becomes the mean) in ONE pass -- each lane reads a column of every row, then writes
+// that column of every destination row, so dst == rows (in place) is safe.  V = a 4-float vector
+// (16-byte non-temporal accesses; TREE 1 over <= 8 rows, or rank order), or float (any other case).
+typedef float f4v __attribute__((ext_vector_type(4)));
+
+template <typename V, int TREE, int MAXR>
+__global__ __launch_bounds__(256) void mean_to_kernel(const V* rows, int nrows, int64_t ld, int64_t count,
+                                                      float size, V* dst, int ndst, int64_t dst_ld) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x) {
+        V acc;
+        if (TREE == 2) {                          // binary counter of partial sums (see mean_rows_kernel)
+            constexpr int L = 24;
+            V stack[L];
+#pragma unroll
+            for (int l = 0; l < L; ++l) stack[l] = V(0.0f);
+            for (int r = 0; r < nrows; ++r) {
+                V p = rows[(int64_t)r * ld + i];
+                bool carry = true;
+#pragma unroll
+                for (int l = 0; l < L; ++l) {
+                    const bool set = (r >> l) & 1;
+                    if (carry && set) p = stack[l] + p;
+                    else if (carry) { stack[l] = p; carry = false; }
+                }
+            }
+            bool have = false;
+            acc = V(0.0f);
+#pragma unroll
+            for (int l = 0; l < L; ++l)
+                if ((nrows >> l) & 1) {
+                    acc = have ? stack[l] + acc : stack[l];
+                    have = true;
+                }
+        } else if (TREE) {
+            V v[MAXR];
+#pragma unroll
+            for (int r = 0; r < MAXR; ++r)
+                v[r] = r < nrows ? __builtin_nontemporal_load(rows + (int64_t)r * ld + i) : V(0.0f);
+#pragma unroll
+            for (int m = 1; m < MAXR; m <<= 1)
+#pragma unroll
+                for (int r = 0; r + m < MAXR; r += 2 * m)
+                    if (r + m < nrows) v[r] = v[r] + v[r + m];
+            acc = v[0];
+        } else {
+            acc = __builtin_nontemporal_load(rows + i);
+            for (int r = 1; r < nrows; ++r) acc = acc + __builtin_nontemporal_load(rows + (int64_t)r * ld + i);
+        }
+        const V m = acc / size;
+        for (int d = 0; d < ndst; ++d) __builtin_nontemporal_store(m, dst + (int64_t)d * dst_ld + i);
+    }
+}
+
 inline unsigned grid_of(int64_t count) {
     int64_t g = (count + 255) / 256;
     return (unsigned)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
@@ -367,6 +471,58 @@ extern "C" int mx_mean_rows(const float* rows, int nrows, int64_t ld, int64_t co
     } else {
         hipLaunchKernelGGL((mean_rows_kernel<2, 1>), dim3(grid_of(count)), dim3(256), 0, st, rows, nrows, ld, count, d,
                            out);
+    }
+    MX_LAUNCH_CHECK();
+    return MX_OK;
+}
+
+extern "C" int mx_mean_rows_to(const float* rows, int nrows, int64_t ld, int64_t count, int order, float* dst,
+                               int ndst, int64_t dst_ld, void* stream) {
+    MX_CHECK(rows && dst && nrows >= 1 && nrows <= (1 << 24) && ld >= count && count >= 0 && ndst >= 0 &&
+                 (ndst <= 1 || dst_ld >= count),
+             "mx_mean_rows_to: nrows=%d ld=%lld count=%lld ndst=%d dst_ld=%lld", nrows, (long long)ld,
+             (long long)count, ndst, (long long)dst_ld);
+    MX_CHECK(order == 0 || order == 1, "mx_mean_rows_to: order %d (0 tree, 1 rank order)", order);
+    MX_CHECK(dst == rows ? (dst_ld == ld || ndst <= 1) : true, "mx_mean_rows_to: in place needs dst_ld == ld");
+    if (count == 0 || ndst == 0) return MX_OK;
+    hipStream_t st = mx::as_stream(stream);
+    const float d = (float)nrows;
+    const bool vec = count >= 4 && ld % 4 == 0 && (ndst <= 1 || dst_ld % 4 == 0) &&
+                     ((uintptr_t)rows | (uintptr_t)dst) % 16 == 0 && (order == 1 || nrows <= 8);
+    if (vec) {
+        const int64_t c4 = count / 4, tail = count - 4 * c4;
+        if (tail) {                               // the last 1-3 columns: scalar lanes, same order
+            const int64_t o = 4 * c4;
+            if (order == 1)
+                hipLaunchKernelGGL((mean_to_kernel<float, 0, 1>), dim3(1), dim3(256), 0, st, rows + o, nrows, ld,
+                                   tail, d, dst + o, ndst, dst_ld);
+            else
+                hipLaunchKernelGGL((mean_to_kernel<float, 1, 8>), dim3(1), dim3(256), 0, st, rows + o, nrows, ld,
+                                   tail, d, dst + o, ndst, dst_ld);
+            MX_LAUNCH_CHECK();
+        }
+        int64_t g = (c4 + 255) / 256;
+        if (g > 4096) g = 4096;
+        const f4v* r4 = reinterpret_cast<const f4v*>(rows);
+        f4v* d4 = reinterpret_cast<f4v*>(dst);
+        if (order == 1)
+            hipLaunchKernelGGL((mean_to_kernel<f4v, 0, 1>), dim3((unsigned)g), dim3(256), 0, st, r4, nrows, ld / 4, c4,
+                               d, d4, ndst, dst_ld / 4);
+        else
+            hipLaunchKernelGGL((mean_to_kernel<f4v, 1, 8>), dim3((unsigned)g), dim3(256), 0, st, r4, nrows, ld / 4, c4,
+                               d, d4, ndst, dst_ld / 4);
+    } else if (order == 1) {
+        hipLaunchKernelGGL((mean_to_kernel<float, 0, 1>), dim3(grid_of(count)), dim3(256), 0, st, rows, nrows, ld,
+                           count, d, dst, ndst, dst_ld);
+    } else if (nrows <= 8) {
+        hipLaunchKernelGGL((mean_to_kernel<float, 1, 8>), dim3(grid_of(count)), dim3(256), 0, st, rows, nrows, ld,
+                           count, d, dst, ndst, dst_ld);
+    } else if (nrows <= 64) {
+        hipLaunchKernelGGL((mean_to_kernel<float, 1, 64>), dim3(grid_of(count)), dim3(256), 0, st, rows, nrows, ld,
+                           count, d, dst, ndst, dst_ld);
+    } else {
+        hipLaunchKernelGGL((mean_to_kernel<float, 2, 1>), dim3(grid_of(count)), dim3(256), 0, st, rows, nrows, ld,
+                           count, d, dst, ndst, dst_ld);
     }
     MX_LAUNCH_CHECK();
     return MX_OK;

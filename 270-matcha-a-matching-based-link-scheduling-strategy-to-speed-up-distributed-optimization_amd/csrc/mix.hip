@@ -86,17 +86,40 @@ __device__ __forceinline__ int64_t round_of(int64_t iter, const int64_t* iter_de
     return (v >= 0 && v < iter) ? v : -1;
 }
 
+// Remote-slot load path (PullTransport, plan word [2] bit 1 -- mx_plan_set_peer_reads): the receive
+// slots point at a peer GPU's IPC-mapped snapshot buffer, which this GPU's L2 holds as non-local
+// (MTYPE NC) lines.  The same two snapshot buffers are re-read every other round, so a line cached
+// here in round r - 2 could be served stale in round r: nothing on this GPU invalidates it when the
+// peer rewrites its HBM (LLVM AMDGPUUsage, memory model GFX942 -- gfx950 shares it: only a
+// system-scope acquire, buffer_inv sc0 sc1, "ensures that following loads will not see stale
+// MTYPE NC global data").  So before the first load of any slot, one lane of every workgroup issues
+// that acquire (invalidating its CU's L1 and the non-local lines of its XCD's L2) and waits for it,
+// and the workgroup meets at a barrier (MI355X_MICROARCH.md, "Consumer, always").  Every later load
+// of the launch is then fresh: the peer's snapshot was written back to its HBM by a system-scope
+// release (mx_snapshot_publish) before the round's host barrier.  Cost: one invalidate per
+// workgroup per round (~2 us), nothing per byte; rounds without peer slots skip it.
+__device__ __forceinline__ void peer_acquire(int32_t mode_word) {
+    if (mode_word & 2) {                         // block-uniform
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");       // system scope: buffer_inv sc0 sc1
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+    }
+}
+
 template <int NS>
 __device__ __forceinline__ uint64_t load_plan(PlanLds<NS>& sp, const int32_t* plan, int64_t iter,
                                               int n_local, int M) {
     if (iter < 0) return 0;                      // block-uniform: no barrier is skipped unevenly
     const int64_t W = mx::plan_words(n_local, M);
     const int32_t* rec = plan + iter * W;
-    for (int i = threadIdx.x; i < W; i += kTPB) sp.w[i] = rec[i];
+    for (int i = threadIdx.x; i < W; i += blockDim.x) sp.w[i] = rec[i];
     __syncthreads();
     if (sp.w[0] == 0) return 0;
+    peer_acquire(sp.w[2]);
     const int n_remote = sp.w[1];
-    const bool idle = sp.w[2] != 0;
+    const bool idle = (sp.w[2] & 1) != 0;
     const int32_t* deg = sp.w + mx::kPlanHeader;
     uint64_t need = 0;
     for (int r = 0; r < n_local; ++r)
@@ -680,8 +703,9 @@ __global__ __launch_bounds__(TPB) void mix_kernel_wide(float* const* __restrict_
         __syncthreads();
         rec = pl;
     }
+    peer_acquire(rec[2]);
     const int n_remote = rec[1];
-    const bool idle = rec[2] != 0;
+    const bool idle = (rec[2] & 1) != 0;
     const int32_t* deg = rec + mx::kPlanHeader;
     const float* sw = reinterpret_cast<const float*>(deg + n_local);
     const int32_t* src = deg + 2 * n_local;

@@ -61,7 +61,7 @@ __global__ __launch_bounds__(256) void plan_kernel(const uint8_t* __restrict__ f
     }
     rec[0] = any;
     rec[1] = remote;
-    rec[2] = 0;                                // idle rows skipped (mx_plan_set_idle)
+    rec[2] = 0;                                // idle rows skipped, local receive slots (mode bits)
     rec[3] = overflow;
     if (overflow) atomicOr(any_overflow, 1);   // read back by mx_plan_build
     for (int r = 0; r < n_local; ++r) {
@@ -73,9 +73,19 @@ __global__ __launch_bounds__(256) void plan_kernel(const uint8_t* __restrict__ f
 }  // namespace
 
 namespace {
-__global__ void idle_kernel(int32_t* __restrict__ plan, int64_t T, int64_t W, int32_t mode) {
+// word [2] of a record: bit 0 = idle-row mode (mx_plan_set_idle), bit 1 = receive slots are peer
+// GPUs' IPC-mapped memory (mx_plan_set_peer_reads); `bit` selects which one is set to `on`
+__global__ void mode_kernel(int32_t* __restrict__ plan, int64_t T, int64_t W, int32_t bit, int32_t on) {
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t < T) plan[t * W + 2] = mode;
+    if (t < T) plan[t * W + 2] = (plan[t * W + 2] & ~bit) | (on ? bit : 0);
+}
+
+int set_mode_bit(int32_t* plan_dev, int64_t T, int n_local, int M, int32_t bit, int on, void* stream) {
+    if (T == 0) return MX_OK;
+    hipLaunchKernelGGL(mode_kernel, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, mx::as_stream(stream),
+                       plan_dev, T, mx::plan_words(n_local, M), bit, (int32_t)on);
+    MX_LAUNCH_CHECK();
+    return MX_OK;
 }
 }  // namespace
 
@@ -84,11 +94,13 @@ extern "C" int64_t mx_plan_words(int n_local, int M) { return mx::plan_words(n_l
 extern "C" int mx_plan_set_idle(int32_t* plan_dev, int64_t T, int n_local, int M, int mode, void* stream) {
     MX_CHECK(plan_dev && T >= 0 && n_local >= 1 && M >= 1, "mx_plan_set_idle: bad arguments");
     MX_CHECK(mode == 0 || mode == 1, "mx_plan_set_idle: mode %d", mode);
-    if (T == 0) return MX_OK;
-    hipLaunchKernelGGL(idle_kernel, dim3((unsigned)((T + 255) / 256)), dim3(256), 0, mx::as_stream(stream),
-                       plan_dev, T, mx::plan_words(n_local, M), (int32_t)mode);
-    MX_LAUNCH_CHECK();
-    return MX_OK;
+    return set_mode_bit(plan_dev, T, n_local, M, 1, mode, stream);
+}
+
+extern "C" int mx_plan_set_peer_reads(int32_t* plan_dev, int64_t T, int n_local, int M, int on, void* stream) {
+    MX_CHECK(plan_dev && T >= 0 && n_local >= 1 && M >= 1, "mx_plan_set_peer_reads: bad arguments");
+    MX_CHECK(on == 0 || on == 1, "mx_plan_set_peer_reads: on %d", on);
+    return set_mode_bit(plan_dev, T, n_local, M, 2, on, stream);
 }
 
 extern "C" int mx_plan_build(const uint8_t* flags_dev, int64_t T, int M, const int32_t* partner_dev,

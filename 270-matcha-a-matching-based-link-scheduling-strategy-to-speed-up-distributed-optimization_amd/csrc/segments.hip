@@ -60,6 +60,28 @@ __global__ __launch_bounds__(kTPB) void synth_kernel(float* __restrict__ dst, in
     }
 }
 
+// PullTransport snapshot (engine._step_pull): dst[i] = src[i], 16-byte accesses, then every
+// workgroup makes its stores visible to OTHER GPUs before the kernel ends.  A peer reads the
+// snapshot over xGMI from this GPU's HBM; plain stores may still sit dirty in this XCD's L2
+// (write-back), and nothing in the round protocol (kernel end, synchronize, host barrier) is
+// documented to write them back at system scope.  So, per workgroup (MI355X_MICROARCH.md, "Valid
+// forms", producer): every wave waits for its stores (vmcnt(0)), a workgroup barrier, then one
+// lane's system-scope release fence (buffer_wbl2 sc0 sc1 + wait: the XCD L2's dirty lines reach
+// HBM) -- the release half of the protocol whose acquire half is the mixing kernels'
+// peer_acquire (mix.hip).
+typedef float f4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(kTPB) void publish_kernel(const f4* __restrict__ src, f4* __restrict__ dst,
+                                                        int64_t n4) {
+    for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kTPB)
+        __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");        // system scope: buffer_wbl2 sc0 sc1
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+
 unsigned grid_for(int64_t total) {
     int64_t g = (total + kTile - 1) / kTile;
     if (g > 4096) g = 4096;
@@ -99,6 +121,26 @@ extern "C" int mx_synth_fill(float* dst, int64_t n, uint64_t seed, void* stream)
     int64_t g = (n + kTPB - 1) / kTPB;
     if (g > 8192) g = 8192;
     hipLaunchKernelGGL(synth_kernel, dim3((unsigned)g), dim3(kTPB), 0, mx::as_stream(stream), dst, n, seed);
+    MX_LAUNCH_CHECK();
+    return MX_OK;
+}
+
+extern "C" int mx_snapshot_publish(const float* src, float* dst, int64_t n, void* stream) {
+    MX_CHECK(n >= 0, "mx_snapshot_publish: n < 0");
+    if (n == 0) return MX_OK;
+    MX_CHECK(src && dst, "mx_snapshot_publish: null pointer");
+    MX_CHECK(n % 4 == 0 && ((uintptr_t)src | (uintptr_t)dst) % 16 == 0,
+             "mx_snapshot_publish: n (%lld) must be a multiple of 4 and both buffers 16-byte aligned", (long long)n);
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) cus = v;
+    }
+    const int64_t n4 = n / 4;
+    int64_t g = (n4 + kTPB - 1) / kTPB;
+    if (g > 4 * (int64_t)cus) g = 4 * (int64_t)cus;    // persistent: one release per workgroup at its end
+    hipLaunchKernelGGL(publish_kernel, dim3((unsigned)g), dim3(kTPB), 0, mx::as_stream(stream),
+                       reinterpret_cast<const f4*>(src), reinterpret_cast<f4*>(dst), n4);
     MX_LAUNCH_CHECK();
     return MX_OK;
 }

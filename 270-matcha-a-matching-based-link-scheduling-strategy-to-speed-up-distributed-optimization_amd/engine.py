@@ -96,9 +96,12 @@ class RcclComm:
     torch.distributed (which must be initialised; any backend) for the unique-id broadcast.
 
     The communicator is non-blocking with a deadline (mx_rccl_init_timeout): if a peer never
-    joins -- the init, or any later exchange / all-reduce of the process -- the call raises
+    joins the init, or the connection setup of a later exchange / all-reduce, the call raises
     MXError ("timed out") after `timeout_s` (default $MX_RCCL_TIMEOUT_S or 300 s) instead of
-    hanging; abort() then releases the communicator."""
+    hanging; abort() then releases the communicator.  A peer that dies or skips an exchange
+    AFTER the connections exist leaves the RCCL kernel waiting on the GPU: wait() is the stream
+    synchronisation with the same deadline (mx_rccl_wait: on expiry the communicator is aborted
+    and MXError raised) -- use it instead of torch.cuda.synchronize() where a peer may be gone."""
 
     def __init__(self, group=None, timeout_s=None):
         import os
@@ -123,6 +126,24 @@ class RcclComm:
         self.handle = h
         self.nonblocking = bool(nb.value)
 
+    def count(self):
+        """ncclCommCount: the ranks RCCL holds in this communicator."""
+        n = ctypes.c_int(0)
+        check(lib.mx_rccl_count(self.handle, ctypes.byref(n)), "mx_rccl_count")
+        return int(n.value)
+
+    def wait(self, stream=None, timeout_s=None):
+        """Block until everything enqueued on `stream` (default: the current stream) has run, or
+        raise MXError after timeout_s (default: the communicator's deadline) -- the communicator is
+        then aborted (mx_rccl_wait)."""
+        if not self.handle:
+            raise MXError("RcclComm.wait: communicator closed or aborted")
+        ms = int(1000 * (self.timeout_s if timeout_s is None else float(timeout_s)))
+        rc = lib.mx_rccl_wait(self.handle, stream_ptr(stream), max(1, ms))
+        if rc:
+            self.handle = None                  # aborted by mx_rccl_wait
+            check(rc, "mx_rccl_wait")
+
     def abort(self):
         """Release a communicator whose peers are gone (ncclCommAbort; after a timed-out call)."""
         if self.handle:
@@ -141,14 +162,20 @@ class PullTransport:
     IPC-shared device buffer (mx_ipc_alloc); its peers map it (mx_ipc_open) and their mixing
     kernel reads the partner rows straight from this GPU's HBM over xGMI (communicator.py:110's
     sendrecv becomes a remote load inside the FMA chain).  Round protocol (VirtualWorkerGroup):
-        1. copy the local rows into snapshot buffer `round % 2` (local HBM copy);
+        1. copy the local rows into snapshot buffer `round % 2` (mx_snapshot_publish: a local HBM
+           copy whose workgroups end with a system-scope release, so the bytes are in HBM, not
+           only in this GPU's write-back L2, when the kernel completes);
         2. synchronize + barrier: every rank's snapshot of this round is complete;
-        3. point the receive slots of this round's plan at the peers' snapshot rows and mix.
+        3. point the receive slots of this round's plan at the peers' snapshot rows and mix; the
+           plan records carry the peer-reads bit (mx_plan_set_peer_reads), so every workgroup of
+           the mixing kernel first acquires at system scope (buffer_inv sc0 sc1): lines of the
+           same snapshot buffer cached on THIS GPU in round r - 2 are not served.
     Snapshots alternate between two buffers, so round r+1's copy never overwrites what a slower
     peer still reads in round r; round r+2's copy comes after round r+1's barrier, which every
     rank passes only once its round-r mix has finished.  Needs one process per GPU of ONE node
     (the peers' HBM must be mappable) -- or, for tests, several processes sharing a GPU.
-    Bootstrap and barrier use torch.distributed (any backend)."""
+    Bootstrap and barrier use torch.distributed (any backend).  VirtualWorkerGroup.close() is
+    collective under this transport (a barrier before the buffers are freed)."""
 
     handle = None
 
@@ -216,6 +243,16 @@ class _PullState:
         if self.own:
             lib.mx_ipc_free(self.own)
             self.own = 0
+
+
+def wait_round(comm, stream=None):
+    """The end-of-round synchronisation of communicate(): with the library's RCCL communicator a
+    deadline-bounded wait (RcclComm.wait -- a peer gone mid-exchange raises instead of hanging),
+    otherwise torch.cuda.synchronize()."""
+    if isinstance(comm, RcclComm) and comm.handle:
+        comm.wait(stream)
+    else:
+        torch.cuda.synchronize()
 
 
 _DEFAULT_COMM = None
@@ -498,12 +535,13 @@ class VirtualWorkerGroup:
         elif isinstance(comm, PullTransport):
             # receive slots point at the peers' snapshot rows, set per round (_step_pull); no slab
             self._pull = comm.bind(self)
+            # receive slots will be peers' memory: the mixing kernels acquire at system scope first
+            check(lib.mx_plan_set_peer_reads(self.engine.plan.data_ptr(), self.engine.T, self.n_local,
+                                             self.engine.M, 1, stream_ptr()), "mx_plan_set_peer_reads")
             self._pull_table = np.zeros((1, self.engine.n_slots), np.int64)
             self._pull_table[0, :self.n_local] = self._row_ptrs
             self._pull_table[0, self.n_local:] = self._pull.own
             self.layout = Layout([self.numel], [[int(p)] for p in self._pull_table[0]], self.engine.n_slots)
-            self._pull_seg = torch.tensor([self.arena.data_ptr()], dtype=torch.int64, device="cuda")
-            self._pull_off = torch.tensor([0, self.n_local * self.ld], dtype=torch.int64, device="cuda")
             self._blocks = partition(n, nranks)
         else:
             slot_ptrs = [[p] for p in self._row_ptrs]
@@ -538,8 +576,9 @@ class VirtualWorkerGroup:
         par = st.round & 1
         st.round += 1
         total = self.n_local * self.ld
-        check(lib.mx_gather(self._pull_seg.data_ptr(), self._pull_off.data_ptr(), 1, total, st.own + par * st.half,
-                            stream_ptr(stream)), "mx_gather")
+        # the copy ends with a system-scope release per workgroup (visible to the peers' loads)
+        check(lib.mx_snapshot_publish(self.arena.data_ptr(), st.own + par * st.half, total, stream_ptr(stream)),
+              "mx_snapshot_publish")
         torch.cuda.synchronize()
         dist.barrier(group=st.transport.group)
         eng = self.engine
@@ -556,10 +595,20 @@ class VirtualWorkerGroup:
         eng.mix(it, self.layout, stream)
         return True
 
+    @property
+    def pulls(self):
+        """True when the receive slots are peers' IPC-mapped snapshots (PullTransport)."""
+        return self._pull is not None
+
     def close(self):
-        """Release the pull transport's shared buffers (collective use ends; see PullTransport)."""
+        """Release the pull transport's shared buffers.  COLLECTIVE under PullTransport: every
+        rank's snapshot buffer may still be read by a slower peer's last round, so all ranks first
+        meet at a barrier (after their own last mix has finished), then unmap and free.  Not to be
+        called from a finalizer (decenCommunicator.__del__ leaves a pull group to process exit)."""
         if self._pull is not None:
+            import torch.distributed as dist
             torch.cuda.synchronize()
+            dist.barrier(group=self._pull.transport.group)
             self._pull.close()
             self._pull = None
 
@@ -635,5 +684,5 @@ class VirtualWorkerGroup:
         torch.cuda.synchronize()
         tic = time.time()
         self.step(it)
-        torch.cuda.synchronize()
+        wait_round(self.engine.comm)
         return time.time() - tic

@@ -174,10 +174,9 @@ def sync_rows(rows, order=0):
         return
     if rows.stride(1) != 1:
         raise ValueError("sync_rows: rows must be contiguous along the parameter axis")
-    check(lib.mx_mean_rows(rows.data_ptr(), n, rows.stride(0), count, int(order), rows[0].data_ptr(),
-                           stream_ptr()), "mx_mean_rows")
-    with torch.no_grad():
-        rows[1:].copy_(rows[0].expand(n - 1, count))
+    # one pass: every column of every row read, then the mean written to that column of every row
+    check(lib.mx_mean_rows_to(rows.data_ptr(), n, rows.stride(0), count, int(order), rows.data_ptr(), n,
+                              rows.stride(0), stream_ptr()), "mx_mean_rows_to")
 
 
 class VirtualTrainer:

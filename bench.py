@@ -439,30 +439,92 @@ def matcha_figure(pkg, args, rank, world, n, P, K, W, comm, dev):
     return out
 
 
-def allreduce_figure(group, n, world, dev, K, W):
-    """Context figure: the all-reduce averaging the paper compares gossip against
-    (centralizedCommunicator, communicator.py:46-76 / sync_allreduce): every worker's row becomes
-    the mean of all workers' rows -- local row sum, torch.distributed all_reduce (RCCL at N > 1),
-    / n, written back to every local row.  torch ops, not the product path; rounds/s like `value`."""
-    import torch.distributed as dist
-    rows = group.rows
+def allreduce_figure(pkg, args, rank, world, n, P, K, W, comm, dev, arena=None):
+    """The centralized all-reduce averaging the paper compares gossip against
+    (centralizedCommunicator.communicate, communicator.py:46-76; sync_allreduce, train_mpi.py:34-56):
+    every worker's row becomes the fp32 sum of all workers' rows in the reference's order (mpi4py's
+    binomial tree) divided by n -- through the product kernels:
+      N = 1: mx_mean_rows_to over the n arena rows, in place (harness.sync_rows): ONE pass,
+             2 * n * P * 4 bytes of HBM per round -> an HBM roofline like the headline's;
+      N > 1: mx_allgather of each rank's rows (RCCL; the gloo test transport stages through the
+             host) + mx_mean_rows_to into the rank's own rows (centralizedCommunicator._average /
+             mx_allreduce_mean_ordered's kernels).
+    Workers sit in contiguous id blocks (the tree order is by worker id).  Parity: every worker's
+    64 sampled columns after the W + K rounds vs the oracle's central_mean applied W + K times."""
+    from importlib import import_module
+    E = import_module(PKG_NAME + ".engine")
+    L = pkg.lib
+    row_base, n_local = E.partition(n, world)[rank]
+    if n % world:
+        raise RuntimeError(f"allreduce figure: {n} workers do not split evenly over {world} ranks")
+    ld = (P + 63) // 64 * 64
+    rows = arena if arena is not None and tuple(arena.shape) == (n_local, ld) else \
+        torch.empty((n_local, ld), dtype=torch.float32, device="cuda")
+    for r in range(n_local):
+        pkg._lib.check(L.mx_synth_fill(rows[r].data_ptr(), P, 1234 + row_base + r, None))
+    gather = torch.empty((n, ld), dtype=torch.float32, device="cuda") if world > 1 else None
+    sp = pkg._lib.stream_ptr
+    ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    timing = [False]
 
-    def one(_):
-        acc = rows.sum(0)
-        if world > 1:
-            if dev == "cpu":                     # gloo test transport: host staging
-                h = acc.cpu()
-                dist.all_reduce(h)
-                acc.copy_(h)
-            else:
-                dist.all_reduce(acc)
-        rows.copy_((acc / n).expand_as(rows))
+    def one(j):
+        if world == 1:
+            if timing[0] and j == 0:
+                ev[0].record()
+            pkg._lib.check(L.mx_mean_rows_to(rows.data_ptr(), n, ld, P, 0, rows.data_ptr(), n, ld, sp()),
+                           "mx_mean_rows_to")
+            if timing[0] and j == K - 1:
+                ev[1].record()
+            return
+        flat = rows.view(-1)
+        if hasattr(comm, "allgather"):                # gloo test transport
+            comm.allgather(flat, gather.view(-1))
+        else:
+            pkg._lib.check(L.mx_allgather(comm.handle, flat.data_ptr(), flat.numel(), gather.data_ptr(), sp()),
+                           "mx_allgather")
+        pkg._lib.check(L.mx_mean_rows_to(gather.data_ptr(), n, ld, P, 0, rows.data_ptr(), n_local, ld, sp()),
+                       "mx_mean_rows_to")
 
     for j in range(W):
         one(j)
+    torch.cuda.synchronize()
+    timing[0] = True
     el = timed_loop(one, 0, K, world, dev)
-    return {"rounds_per_s": K / el, "ms_per_round": 1e3 * el / K,
-            "how": "row sum + torch.distributed all_reduce (RCCL at N > 1) + / n + copy back; torch ops"}
+    cols = sample_columns(P)
+    loc = rows[:, :P].index_select(1, torch.from_numpy(cols).cuda()).cpu().numpy()
+    objs = [(row_base, loc)]
+    if world > 1:
+        import torch.distributed as dist
+        objs = [None] * world
+        dist.all_gather_object(objs, (row_base, loc))
+    del gather
+    if arena is None:
+        del rows
+    torch.cuda.empty_cache()
+    out = {"rounds_per_s": K / el, "ms_per_round": 1e3 * el / K, "rounds": K, "order": "tree (mpi4py default)",
+           "how": ("mx_mean_rows_to in place over the arena rows: one pass (harness.sync_rows)" if world == 1 else
+                   "mx_allgather (RCCL) of every rank's rows + mx_mean_rows_to into this rank's rows")}
+    if world == 1:
+        alg = 2 * n * P * 4
+        kern_ms = ev[0].elapsed_time(ev[1]) / K
+        out["roofline"] = {"bound": "hbm", "kernel": "mean_to_kernel (mx_mean_rows_to)", "bytes_per_launch": alg,
+                           "avg_launch_ms": kern_ms, "achieved": alg / (kern_ms * 1e-3) / 1e9,
+                           "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": alg / (kern_ms * 1e-3) / HBM_PEAK,
+                           "note": "algorithmic bytes 2 x n x P x 4 (every row read once, the mean written to "
+                                   "every row) / HIP events over the K timed launches"}
+    if rank == 0:
+        O = _oracle()
+        got = np.zeros((n, len(cols)), np.float32)
+        for base, blk in objs:
+            got[base:base + blk.shape[0]] = blk
+        X = np.stack([O.synth_at(1234 + w, cols) for w in range(n)])
+        for _ in range(W + K):
+            X = np.ascontiguousarray(np.broadcast_to(O.central_mean(X, "tree"), X.shape))
+        out["parity_ok"] = bool(np.array_equal(got.view(np.uint32), X.view(np.uint32)))
+        out["parity"] = (f"every worker's {len(cols)} sampled columns after {W + K} rounds vs the oracle's "
+                         f"centralizedCommunicator round (orc_central_mean, mpi4py tree order) from the same "
+                         f"synthetic rows, uint32")
+    return out
 
 
 def _choco_state(grp):
@@ -809,15 +871,87 @@ def timed_rounds(run, group, first, K):
 
 
 # ----------------------------------------------------------------------------------- main
+def _free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def self_launch(args, argv, popen=None):
+    """`bench.py --gpus N` (N > 1) started WITHOUT a launcher (no WORLD_SIZE): run the N ranks
+    as a child `python -m torch.distributed.run --nproc-per-node N bench.py ...` and relay rank 0's
+    JSON line; returns the exit status for the parent to exit with.
+
+    The parent never initialises HIP: it counts devices with torch.cuda.device_count() (which on
+    this image does not initialise the GPU) and starts the launcher as a CHILD process -- never an
+    exec from this process.  With the RCCL transport it refuses (non-zero, with a message) when
+    fewer than N GPUs are visible, instead of silently timing N = 1.  SIGTERM / SIGINT to the
+    parent are forwarded to the child's process group (each rank then prints its line so far)."""
+    import signal
+    import subprocess
+    n = int(args.gpus)
+    if args.transport == "rccl":
+        have = torch.cuda.device_count()
+        if have < n:
+            sys.stderr.write(f"bench.py --gpus {n}: only {have} GPU(s) visible -- the RCCL transport needs one GPU "
+                             f"per rank (run the N = {n} scaling bench on a node with {n} GPUs, or --transport gloo "
+                             f"to exercise the multi-process path on fewer)\n")
+            return 2
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("MASTER_ADDR", "127.0.0.1")
+    popen = popen or subprocess.Popen
+    proc = popen(cmd, stdout=subprocess.PIPE, env=env, start_new_session=True, text=True, bufsize=1)
+
+    def forward(signum, _frame):
+        try:
+            os.killpg(proc.pid, signum)
+        except (ProcessLookupError, PermissionError, OSError):
+            pass
+
+    old = {s: signal.signal(s, forward) for s in (signal.SIGTERM, signal.SIGINT)}
+    printed = False
+    try:
+        for raw in proc.stdout:
+            s = raw.strip()
+            if s.startswith("{") and not printed:
+                try:
+                    d = json.loads(s)
+                except ValueError:
+                    d = None
+                if isinstance(d, dict) and "metric" in d:
+                    d["launcher"] = {"self_launched": True, "nproc_per_node": n,
+                                     "how": "bench.py (no WORLD_SIZE) started torch.distributed.run as a child "
+                                            "process; this is rank 0's line"}
+                    print(json.dumps(d), flush=True)
+                    printed = True
+                    continue
+            sys.stderr.write(raw)
+        rc = proc.wait()
+    finally:
+        for s, h in old.items():
+            signal.signal(s, h)
+    if not printed and rc == 0:
+        sys.stderr.write("bench.py self-launch: the ranks exited without a JSON line\n")
+        return 1
+    return rc
+
+
 def main():
     """The run happens on a worker thread; the main thread only waits, so it stays free to take
     SIGTERM -- what the launcher (torchrun) sends every rank when one rank dies -- and rank 0
     then prints the line measured so far with an "error" field before leaving."""
     import signal
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(self_launch(args, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    if args.gpus != world and world > 1:
+    if args.gpus != world:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
     line = Line(rank)
     wd = Watchdog(rank, line.emit)
@@ -873,6 +1007,9 @@ def run(args, world, rank, line, wd):
             comm = GlooTransport(pkg)
         else:
             comm = pkg.engine.RcclComm(timeout_s=min(args.figure_timeout, args.headline_timeout) * 0.8)
+    # the ranks RCCL itself holds (ncclCommCount on the library's communicator): proof that the
+    # exchange really spans N processes / GPUs
+    rccl_ranks = comm.count() if isinstance(comm, pkg.engine.RcclComm) else None
     wd.arm("headline", args.headline_timeout)
 
     n, P = args.workers, args.params
@@ -983,6 +1120,10 @@ def run(args, world, rank, line, wd):
     timed_events_ms = tev[0].elapsed_time(tev[1]) / K
     elapsed = max_over_ranks(elapsed, world, dev)
     timed_first = it
+    if overlap is not None and getattr(timed, "pulls", False):
+        # rounds the pull group ran on its two alternating snapshot buffers (each reused >= 3 times
+        # when this is >= 6); parity_ok below covers every one of them
+        overlap["pull_rounds"] = int(timed._pull.round)
     final_cols = gather_columns(timed, cols_dev, world, dev)
     # mixing kernel alone (N > 1: without the RCCL exchange, so rows go stale) -> its HBM roofline
     stream = torch.cuda.current_stream()
@@ -1047,6 +1188,7 @@ def run(args, world, rank, line, wd):
                                    overlap.get("chosen_form") else ""),
                    "placement": group.placement if world > 1 else None,
                    "transport": args.transport if world > 1 else None},
+        "rccl_ranks": rccl_ranks,
         "parity_ok": None,
         "round_us": {"events_min": 1e3 * float(step_ms.min()), "events_median": 1e3 * float(np.median(step_ms)),
                      "events_mean": 1e3 * avg_ms, "events_last_block_mean": 1e3 * float(step_ms[-K:].mean()),
@@ -1154,8 +1296,9 @@ def run(args, world, rank, line, wd):
                                                                            args.cpu_seconds))
     out["matcha_schedule"] = figure("matcha", lambda: matcha_figure(pkg, args, rank, world, n, P, K, W, comm, dev),
                                     args.budget >= 1.0)
-    out["allreduce_baseline"] = figure("allreduce", lambda: allreduce_figure(group, n, world, dev, max(5, K // 5), 2),
-                                       bool(args.allreduce))
+    out["allreduce_baseline"] = figure("allreduce", lambda: allreduce_figure(
+        pkg, args, rank, world, n, P, max(5, K), 2, comm, dev,
+        arena=group.arena if world == 1 else None), bool(args.allreduce))
     # the headline groups are done: release them before the large figures
     for g in {id(g): g for g in (timed, group)}.values():
         g.close()

@@ -63,8 +63,9 @@ int mx_flags_binomial_sequential(const uint32_t* key_in, int pos_in, const doubl
  *   partner_dev  int32 [M][n_global]   (GraphProcessor.neighbors_info, graph_manager.py:157-180)
  *   owner_dev    int32 [n_global]      rank owning each worker; NULL = all local
  *   plan_dev     int32 [T][mx_plan_words(n_local, M)]
- * Plan record layout (int32 words): [0] any flag set, [1] n_remote, [2] idle-row mode
- *   (mx_plan_set_idle; 0 after mx_plan_build), [3] 1 if the round has more than 156 distinct
+ * Plan record layout (int32 words): [0] any flag set, [1] n_remote, [2] mode
+ *   bits (0 after mx_plan_build): bit 0 idle-row mode (mx_plan_set_idle), bit 1 receive slots in
+ *   peer GPUs' memory (mx_plan_set_peer_reads), [3] 1 if the round has more than 156 distinct
  *   remote partners (not representable: mx_plan_build then returns MX_ERR_INVALID after one
  *   4-byte read-back and a stream synchronize at build time),
  *   [4, 4+n_local) degree, [4+n_local, 4+2n_local) selfweight (f32 bits),
@@ -217,9 +218,16 @@ size_t mx_topk_work_bytes(int64_t P);
  * "select_blocks" = select_kernel workgroups per row (0 = auto: the fewest whose LDS caches every
  * candidate region, at most 32); "select_trace" = 1: select_kernel stores stage clocks in the
  * scratch (diagnostic, tools/select_trace.py).
- * Knobs tune speed only, never results. */
+ * Knobs tune speed only, never results.
+ * mx_topk_get also reads "hist_grid" (the last call's first-candidate-pass grid per row) and
+ * "hist_capacity" (the co-resident block cap that grid was held to with sampling on, 0 without). */
 int mx_topk_set(const char* key, int64_t value);
 int64_t mx_topk_get(const char* key);
+/* The rows' sticky error words: a row barrier (the sampled-floor fallback of the first candidate
+ * pass, or select_kernel) whose BOUNDED wait expired -- its blocks were not all resident -- leaves
+ * that call's output undefined instead of hanging the GPU.  Synchronises `stream`, reads and clears
+ * the words; MX_ERR_HIP if any was set.  (work, work_ld_bytes, nrows, P) as in the call checked. */
+int mx_topk_check(void* work, int64_t work_ld_bytes, int nrows, int64_t P, void* stream);
 int mx_topk_abs_diff(const float* x, const float* x_hat, int64_t P, int64_t k, float* vals,
                      int64_t* idx, void* work, void* stream);
 /* Batched form (one set of launches for every local worker): row r reads x + r*ld (and
@@ -289,6 +297,16 @@ int mx_rccl_init_timeout(const void* id, int nranks, int rank, int64_t timeout_m
 int mx_rccl_abort(void* comm);
 /* ncclCommFinalize (waited for with the deadline; aborted on expiry) + ncclCommDestroy. */
 int mx_rccl_destroy(void* comm);
+/* ncclCommCount: the ranks the communicator holds (the bench line's rccl_ranks). */
+int mx_rccl_count(void* comm, int* nranks_out);
+/* The deadlines above bound getting an operation enqueued (init, a group's connection setup).
+ * A peer that dies or skips an exchange after the connections exist leaves the RCCL kernel
+ * waiting on the GPU; mx_rccl_wait is the stream synchronisation with a deadline: an event behind
+ * everything enqueued on `stream`, polled until it completes or timeout_ms (<= 0: the init's
+ * deadline) passes -- then the communicator is ABORTED (its kernels exit, the stream drains; do not
+ * use it again) and MX_ERR_RCCL "timed out" is returned.  Replaces the blocking barriers that
+ * bracket averaging (communicator.py:94,119). */
+int mx_rccl_wait(void* comm, void* stream, int64_t timeout_ms);
 /* The ordered operations mx_exchange_round posts for this rank, host only (no GPU, no RCCL):
  * ops[4i..4i+3] = {kind (0 send / 1 recv), peer rank, local row (send) or slab slot (recv),
  * global id of the worker whose row travels}.  ops == NULL: count only. */
@@ -311,6 +329,14 @@ int mx_exchange_round(void* comm, const uint8_t* flags_row, int M, const int32_t
  * mixing kernel reads the partner rows straight from the owner's HBM over xGMI, in place of
  * comm.sendrecv (communicator.py:110).  mx_ipc_close unmaps a peer buffer, mx_ipc_free releases
  * one's own. */
+/* Snapshot of this GPU's rows for its peers: dst[i] = src[i] (n floats, n % 4 == 0, 16-byte
+ * aligned), and every workgroup ends with a system-scope release (its stores written back past
+ * this GPU's L2 to HBM), so a peer's load over xGMI after the round's barrier sees them. */
+int mx_snapshot_publish(const float* src, float* dst, int64_t n, void* stream);
+/* Plan word [2] bit 1: the receive slots of these records point at peer GPUs' IPC-mapped memory;
+ * the mixing kernels then start with a system-scope acquire per workgroup (buffer_inv sc0 sc1: no
+ * line of a peer's buffer cached on this GPU from an earlier round is served).  on = 1 / 0. */
+int mx_plan_set_peer_reads(int32_t* plan_dev, int64_t T, int n_local, int M, int on, void* stream);
 int mx_ipc_handle_bytes(void);
 int mx_ipc_alloc(int64_t bytes, void** ptr_out, void* handle_out);
 int mx_ipc_open(const void* handle, void** ptr_out);
@@ -334,6 +360,14 @@ int mx_allgather(void* comm, const float* send, int64_t count, float* gather, vo
  * the centralized communicator (communicator.py:61-62) and of sync_allreduce (train_mpi.py:46-55),
  * callable after any transport's gather. */
 int mx_mean_rows(const float* rows, int nrows, int64_t ld, int64_t count, int order, float* out, void* stream);
+/* The same mean (same order, same rounding) written to ndst rows dst + d * dst_ld (d < ndst) in one
+ * pass: centralizedCommunicator's all-reduce (communicator.py:56-67) / sync_allreduce (train_mpi.py:
+ * 34-56) for workers held as rows of one arena -- dst == rows (dst_ld == ld) rewrites every worker's
+ * row with the mean in place (each column of every row is read before that column is written);
+ * after an mx_allgather, dst = this rank's own rows.  16-byte accesses when everything is 16-byte
+ * aligned and the order is the <= 8-row tree or rank order. */
+int mx_mean_rows_to(const float* rows, int nrows, int64_t ld, int64_t count, int order, float* dst, int ndst,
+                    int64_t dst_ld, void* stream);
 
 /* ---------------------------------------------------------------- host: matching decomposition
  * nx.max_weight_matching (graph_manager.py:64, inside GraphProcessor.getSubGraphs 57-83) without

@@ -55,6 +55,8 @@ def lib():
                                           ctypes.c_int, _i32p, _u8p, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_double, _f32p, ctypes.c_int]
         L.orc_baseline_rounds.restype = ctypes.c_int
+        L.orc_central_mean.argtypes = [_f32p, ctypes.c_int, ctypes.c_int64, ctypes.c_int, _f32p]
+        L.orc_central_mean.restype = ctypes.c_int
         L.orc_synth.argtypes = [ctypes.c_uint64, ctypes.c_int64, _f32p]
         L.orc_num_threads.restype = ctypes.c_int
         _lib = L
@@ -130,6 +132,18 @@ def choco_round(X, XH, S, partner, flags, alpha, k, gamma):
     rc = lib().orc_choco_round(X, XH, S, n, P, partner, flags, partner.shape[0], float(alpha),
                                int(k), float(gamma))
     assert rc == 0, rc
+
+
+def central_mean(X, order="tree"):
+    """centralizedCommunicator round (communicator.py:46-76): every worker's vector becomes the
+    fp32 sum of all workers' vectors in mpi4py's object-allreduce order ("tree": binomial tree,
+    its default; "sequential": rank order), divided by n.  X: [n][P] f32 -> the mean [P]."""
+    X = np.ascontiguousarray(X, dtype=np.float32)
+    n, P = X.shape
+    out = np.empty(P, np.float32)
+    rc = lib().orc_central_mean(X, n, P, {"tree": 0, "sequential": 1}[order], out)
+    assert rc == 0, rc
+    return out
 
 
 def baseline_rounds(segs, partner, flags, alpha, threads=0):

@@ -8,6 +8,7 @@ import importlib
 import json
 import os
 import sys
+import time
 
 import numpy as np
 import torch
@@ -83,6 +84,19 @@ def main():
                                                      pkg._lib.stream_ptr()))
     torch.cuda.synchronize()
     out["allreduce_ordered_identity"] = bool(torch.equal(x, z) and torch.equal(gather, x))
+    out["count"] = comm.count()                     # ncclCommCount (the bench line's rccl_ranks)
+    comm.wait()                                     # a drained stream: returns at once
+    # the deadline-bounded stream wait: a kernel that outlives the deadline stands in
+    # for an RCCL kernel whose peer died after the connections existed -- MXError after the
+    # deadline (not a hang), the communicator aborted, the stream drained afterwards
+    torch.cuda._sleep(int(1e9))
+    t = time.time()
+    try:
+        comm.wait(timeout_s=0.1)
+        out["wait_deadline"] = False
+    except pkg.MXError as e:
+        out["wait_deadline"] = "did not drain" in str(e) and comm.handle is None
+    out["wait_deadline_s_ok"] = time.time() - t >= 0.1
     comm.close()
     dist.destroy_process_group()
     print(json.dumps(out), flush=True)

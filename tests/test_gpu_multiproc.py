@@ -111,11 +111,31 @@ def test_bench_multiprocess_overlap_forms(nproc, overlap, pull):
     if overlap == "on":
         assert out["overlap"]["chosen_form"] == "rccl_chunked" and "rccl_chunked" in out["config"]["parallelism"]
     elif pull == "on":
+        # the pull form's two snapshot buffers each reused >= 3 times within the rounds parity covers
+        # (a stale line of round r - 2 would break parity_ok)
         assert out["overlap"]["chosen_form"] == "pull" and out["overlap"]["pull_unavailable"] is None
+        assert out["overlap"]["pull_rounds"] >= 6, out["overlap"]
     elif overlap == "off" and pull == "off":
         assert out["overlap"] is None
     else:
         assert set(out["overlap"]["calib_ms"]) == {"rccl", "rccl_chunked", "pull"}
+
+
+def test_bench_self_launch_gloo():
+    """`python bench.py --gpus 2` WITHOUT torchrun: the parent starts the ranks
+    as a child torch.distributed.run and relays rank 0's line -- n_gpus 2, the oracle self-check
+    true, the launcher recorded (gloo transport: both ranks share this box's one GPU)."""
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--transport", "gloo", "--steps", "3",
+                        "--warmup", "1", "--params", "100000", "--choco", "0", "--cpu-seconds", "0", "--configs",
+                        "0", "--er", "0", "--allreduce", "1"], cwd=ROOT, capture_output=True, text=True,
+                       timeout=240, env=dict(os.environ, OMP_NUM_THREADS="2"))
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-3000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["parity_ok"] is True and out["launcher"]["self_launched"] is True
+    assert out["rccl_ranks"] is None                       # gloo transport: no RCCL communicator
+    assert out["allreduce_baseline"]["parity_ok"] is True
 
 
 def test_dropin_communicators_one_process_per_worker():
@@ -138,7 +158,8 @@ def test_rccl_single_rank_linkage():
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out == {"rank": 0, "nranks": 1, "nonblocking": True, "allreduce_identity": True, "decen_bit_exact": True,
                    "post_self_exchange": True, "post_validates": True, "post_validates_peer": True,
-                   "allreduce_ordered_identity": True}, out
+                   "allreduce_ordered_identity": True, "count": 1, "wait_deadline": True,
+                   "wait_deadline_s_ok": True}, out
 
 
 def test_bench_watchdog_line_on_stall():
