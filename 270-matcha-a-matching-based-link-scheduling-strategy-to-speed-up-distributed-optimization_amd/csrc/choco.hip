@@ -59,7 +59,12 @@ struct SelState {
     unsigned long long cand_n;   // candidates kept by the first compact_kernel pass (zero on entry)
     uint32_t bar;         // arrivals at the row's grid barriers (zeroed by the compaction pass)
     uint32_t err;         // sticky: a row barrier's bounded wait expired (select_kernel)
+    // floor hint (mx_topk_set "floor_hint"): the last call's exact k-th key's top digit and the
+    // row's adaptive margin below it, written by the call's threshold pass; call / fallback counts
+    uint32_t hint_digit, hint_ok, margin;
+    uint32_t n_calls, n_fallbacks;
 };
+static_assert(sizeof(SelState) <= 64, "SelState must fit its 64-byte slot");
 
 // Per-chunk counters and per-block totals are 64-byte records, each written whole by one store
 // instruction (a record half-written by two kernels / two blocks is a partial-sector write).  Padding
@@ -109,6 +114,7 @@ struct Rows {
     int64_t work_ld;
     int64_t P, k;
     int64_t bnd_off;      // int32 tile bounds at out + r*out_ld + bnd_off (< 0: not written)
+    int32_t hint;         // floor_hint margin in 12-bit bins (< 0: sampled floor)
 };
 
 struct RowView {
@@ -446,6 +452,44 @@ __device__ Resolved resolve(const RowView& v, int64_t k, int stages) {
 // shuffle scans (several rows: 650 vs 655 us with ballots, whose 64-bit masks spill SGPRs)
 // LOOP: candidate stores in a loop over the lane's kept elements (mx_topk_set "compact_store" 1)
 // PF2: two whole chunks in flight per wave instead of one (a second register buffer, +32 VGPRs)
+// The compaction's candidate floor (a 12-bit top digit; block-uniform, every thread calls it).
+// S >= 1: from the sampled histogram -- S = 1 the exact digit of the k-th largest key, S > 1 k scaled
+// to the sample with a 25 % + 4 sigma margin.  S = 0 (floor_hint): the previous call's exact k-th
+// key's digit lowered by the row's adaptive margin (no sampling launch); the first call on a scratch
+// has no hint and keeps every key.  A floor too high is caught by the candidate count (fallback).
+__device__ uint32_t floor_digit(const Rows& R, const RowView& v, int64_t S, double frac) {
+    if (S == 0) {
+        if (!v.st->hint_ok) return 0u;
+        const uint32_t m = v.st->margin ? v.st->margin : (uint32_t)(R.hint > 0 ? R.hint : 1);
+        const uint32_t d = v.st->hint_digit;
+        return d > m ? d - m : 0u;
+    }
+    int64_t want = R.k;
+    if (S > 1) {
+        const double e = (double)R.k * frac;
+        want = (int64_t)ceil(1.25 * e + 4.0 * sqrt(e) + 16.0);
+    }
+    int b;
+    int64_t rem, tot;
+    find_bin<kTopBins>(v.hs, want, &b, &rem, &tot);
+    return tot < want ? 0u : (uint32_t)b;                   // too few sampled keys: keep everything
+}
+
+// After the threshold pass resolved T (one thread per row): the next call's floor hint, the margin
+// adapted (a fallback widens it by 4 bins, a candidate set above 4 k narrows it by one), counts.
+__device__ void record_round(const Rows& R, SelState* st, uint32_t T) {
+    const unsigned long long cn = st->cand_n;
+    const bool fb = cn < (unsigned long long)R.k;
+    uint32_t m = st->margin ? st->margin : (uint32_t)(R.hint > 0 ? R.hint : 1);
+    if (fb) m = m + 4 < 255 ? m + 4 : 255;
+    else if (cn > 4ull * (unsigned long long)R.k && m > 1) m -= 1;
+    st->margin = m;
+    st->hint_digit = T >> kTopShift;
+    st->hint_ok = 1;
+    st->n_calls += 1;
+    st->n_fallbacks += fb ? 1u : 0u;
+}
+
 template <bool BAL, bool LOOP, bool PF2 = false>
 __device__ void compact_run(const Rows& R, const RowView& v, int64_t S, double frac, int fallback, int64_t bx,
                             int64_t gx) {
@@ -476,15 +520,7 @@ __device__ void compact_run(const Rows& R, const RowView& v, int64_t S, double f
 
     uint32_t b_lo = 0;
     if (!fallback) {
-        int64_t want = R.k;
-        if (S > 1) {
-            const double e = (double)R.k * frac;
-            want = (int64_t)ceil(1.25 * e + 4.0 * sqrt(e) + 16.0);
-        }
-        int b;
-        int64_t rem, tot;
-        find_bin<kTopBins>(v.hs, want, &b, &rem, &tot);
-        b_lo = tot < want ? 0u : (uint32_t)b;               // too few sampled keys: keep everything
+        b_lo = floor_digit(R, v, S, frac);
         if (bx == 0 && threadIdx.x == 0) {
             v.st->b0 = b_lo;
             v.st->bar = 0;                                  // the selection's row barriers start here
@@ -671,15 +707,7 @@ __global__ __launch_bounds__(kTPB) void compact_wave_kernel(Rows R, int64_t S, d
     if (chunk_of(0) < nfull) issue(0);             // in flight while b_lo is resolved
     uint32_t b_lo = 0;
     {
-        int64_t want = R.k;
-        if (S > 1) {
-            const double e = (double)R.k * frac;
-            want = (int64_t)ceil(1.25 * e + 4.0 * sqrt(e) + 16.0);
-        }
-        int b;
-        int64_t rem, tot;
-        find_bin<kTopBins>(v.hs, want, &b, &rem, &tot);
-        b_lo = tot < want ? 0u : (uint32_t)b;
+        b_lo = floor_digit(R, v, S, frac);
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             v.st->b0 = b_lo;
             v.st->bar = 0;
@@ -812,7 +840,7 @@ template <int BITS, bool BAL, bool LOOP>
 __global__ __launch_bounds__(kTPB) void cand_hist(Rows R, int64_t S, double frac) {
     const RowView v = row_view(R);
     if constexpr (BITS == kMidBits) {
-        if (S > 1 && v.st->cand_n < (unsigned long long)R.k) {     // block-uniform
+        if (S != 1 && v.st->cand_n < (unsigned long long)R.k) {    // block-uniform (sampled or hinted floor)
             compact_run<BAL, LOOP>(R, v, S, frac, 1, blockIdx.x, gridDim.x);
             row_grid_barrier(v.st, gridDim.x);
         }
@@ -892,6 +920,7 @@ __global__ __launch_bounds__(kTPB) void cand_mark(Rows R, int64_t G) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         v.st->T = T;
         v.st->need = z.need;
+        record_round(R, v.st, T);
     }
     __shared__ uint32_t sg[kWaves], se[kWaves];
     uint32_t wg = 0, we = 0;
@@ -1152,7 +1181,7 @@ __global__ __launch_bounds__(kSelTPB) void select_kernel(Rows R, int row0, int B
     Bins<kTopBins, kSelTPB> a12, f12;
     load_bins<kTopBins, kSelTPB>(v.h12, a12);
     load_bins<kTopBins, kSelTPB>(v.h12f, f12);
-    const bool fb = S > 1 && cand_n < (unsigned long long)R.k;   // row-uniform
+    const bool fb = S != 1 && cand_n < (unsigned long long)R.k;  // row-uniform
     uint32_t bar0 = 0;
     if (fb) {
         // keep every key of this block's chunks, in index order, digits into the fallback histogram
@@ -1329,6 +1358,7 @@ __global__ __launch_bounds__(kSelTPB) void select_kernel(Rows R, int row0, int B
     if (b == 0 && tid == 0) {
         v.st->T = T;
         v.st->need = need_eq;
+        record_round(R, v.st, T);
     }
 
     int32_t* bnd = R.bnd_off >= 0 ? reinterpret_cast<int32_t*>(R.out + (int64_t)r * R.out_ld + R.bnd_off) : nullptr;
@@ -1768,6 +1798,8 @@ int g_cand_chunks = 0;        // chunk regions per wave of cand_hist / cand_mark
                               // flush of cand_hist<10>'s 1024 bins measured +3.7 us on one row; same-box
                               // sweep 2 -> 4 / 8: one row 121.7 -> 119.6 us, 8 rows 655 -> 640 us)
 
+int g_floor_hint = -1;         // >= 0: candidate floor from the previous call's k-th key minus this many
+                               // 12-bit bins (adaptive per row), no sampling launch; -1: sampled floor
 unsigned g_hist_grid = 0;      // the last call's cand_hist<10> grid per row, and the co-resident cap it
 unsigned g_hist_capacity = 0;  // was held to (blocks of that instantiation the chip holds, x 7/8): mx_topk_get
 
@@ -1875,6 +1907,11 @@ extern "C" int mx_topk_set(const char* key, int64_t value) {
         g_select = (int)value;
         return MX_OK;
     }
+    if (!strcmp(key, "floor_hint")) {
+        MX_CHECK(value >= -1 && value <= 64, "mx_topk_set: floor_hint %lld (-1 off, 0..64 bins)", (long long)value);
+        g_floor_hint = (int)value;
+        return MX_OK;
+    }
     if (!strcmp(key, "select_trace")) {
         g_select_trace = value != 0;
         return MX_OK;
@@ -1906,6 +1943,7 @@ extern "C" int64_t mx_topk_get(const char* key) {
     if (key && !strcmp(key, "select_blocks")) return g_select_blocks;
     if (key && !strcmp(key, "select_trace")) return g_select_trace;
     if (key && !strcmp(key, "hist_grid")) return g_hist_grid;
+    if (key && !strcmp(key, "floor_hint")) return g_floor_hint;
     if (key && !strcmp(key, "hist_capacity")) return g_hist_capacity;
     mx::set_error("mx_topk_get: unknown key '%s'", key ? key : "(null)");
     return MX_ERR_INVALID;
@@ -1927,16 +1965,17 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
              "mx_topk_abs_diff_rows: work must be 256-byte aligned");
     hipStream_t st = mx::as_stream(stream);
     Rows R{x, x_hat, ld, static_cast<char*>(out), out_ld_bytes, idx_off_bytes, static_cast<char*>(work),
-           work_ld_bytes, P, k, bnd_off_bytes};
+           work_ld_bytes, P, k, bnd_off_bytes, (int32_t)g_floor_hint};
     const int64_t nc = n_chunks(P);
-    const int64_t S = sample_stride(P);
-    const int64_t nsamp = (n_subs(P) + S - 1) / S;
+    // S = 0: the floor comes from the previous call's k-th key (floor_hint), no sampling launch
+    const int64_t S = g_floor_hint >= 0 ? 0 : sample_stride(P);
+    const int64_t nsamp = S > 0 ? (n_subs(P) + S - 1) / S : 0;
     int64_t sampled = 0;                      // elements in the sampled pieces
     for (int64_t u = 0; u < nsamp; ++u) {
         const int64_t c0 = u * S * kSub;
         sampled += (P - c0 < kSub) ? P - c0 : kSub;
     }
-    const double frac = (double)sampled / (double)P;
+    const double frac = S > 0 ? (double)sampled / (double)P : 1.0;
     MX_CHECK(nc <= 0x7fffffff && P < ((int64_t)1 << 32), "mx_topk_abs_diff_rows: P too large (uint32 histograms)");
     const int cblocks = g_compact_blocks > 0 ? g_compact_blocks : (nrows == 1 ? 640 : 2560);
     unsigned bgrid = clamp_grid(nc, 1, (cblocks + nrows - 1) / nrows);   // persistent
@@ -1947,13 +1986,13 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
         bgrid = (unsigned)((nc + q - 1) / q);
     }
     const unsigned wgrid = (unsigned)((nc + kWaves - 1) / kWaves);          // one wave per chunk
-    const unsigned sgrid = clamp_grid(nsamp, (int64_t)g_sample_pieces * kWaves, (1024 + nrows - 1) / nrows);
+    const unsigned sgrid = clamp_grid(nsamp > 0 ? nsamp : 1, (int64_t)g_sample_pieces * kWaves, (1024 + nrows - 1) / nrows);
     const int cchunks = g_cand_chunks > 0 ? g_cand_chunks : (nrows == 1 ? 4 : 8);
     const unsigned cgrid = clamp_grid(nc, (int64_t)cchunks * kWaves, (2048 + nrows - 1) / nrows);
 #define MX_L(kern, grid, tpb, ...)                                                 \
     hipLaunchKernelGGL(kern, grid, dim3(tpb), 0, st, R, ##__VA_ARGS__);            \
     MX_LAUNCH_CHECK()
-    MX_L(sample_kernel, dim3(sgrid, nrows), kTPB, S);
+    if (S > 0) MX_L(sample_kernel, dim3(sgrid, nrows), kTPB, S);
     auto ck = nrows == 1 ? (g_compact_store ? (g_compact_pf2 ? compact_kernel<true, true, true> : compact_kernel<true, true>)
                                             : compact_kernel<true, false>)
                          : (g_compact_store ? (g_compact_pf2 ? compact_kernel<false, true, true> : compact_kernel<false, true>)
@@ -1990,7 +2029,7 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
     auto h10 = nrows == 1 ? (g_compact_store ? cand_hist<kMidBits, true, true> : cand_hist<kMidBits, true, false>)
                           : (g_compact_store ? cand_hist<kMidBits, false, true> : cand_hist<kMidBits, false, false>);
     unsigned hgrid = cgrid;
-    if (S > 1) {
+    if (S != 1) {
         const int64_t cap = hist_capacity(reinterpret_cast<const void*>(h10));
         MX_CHECK(cap >= nrows, "mx_topk_abs_diff_rows: %d rows exceed the %lld co-resident blocks of the candidate "
                  "pass (its sampled-floor fallback needs every block of a row resident)", nrows, (long long)cap);
@@ -2031,6 +2070,23 @@ extern "C" int mx_topk_check(void* work, int64_t work_ld_bytes, int nrows, int64
         mx::set_error("mx_topk: a row barrier's bounded wait expired (row %d): not every block of the row was "
                       "resident; that call's output is undefined", bad);
         return MX_ERR_HIP;
+    }
+    return MX_OK;
+}
+
+// Per row: {calls, fallback compactions, current floor-hint margin} (diagnostics of the floor choice).
+extern "C" int mx_topk_stats(const void* work, int64_t work_ld_bytes, int nrows, int64_t P, int64_t* out,
+                             void* stream) {
+    MX_CHECK(work && out && nrows >= 1 && P >= 1 && (nrows == 1 || work_ld_bytes >= (int64_t)layout(P).total),
+             "mx_topk_stats: bad arguments");
+    MX_HIP(hipStreamSynchronize(mx::as_stream(stream)));
+    for (int r = 0; r < nrows; ++r) {
+        SelState st;
+        MX_HIP(hipMemcpy(&st, static_cast<const char*>(work) + (int64_t)r * work_ld_bytes + layout(P).state, sizeof(st),
+                         hipMemcpyDeviceToHost));
+        out[3 * r] = st.n_calls;
+        out[3 * r + 1] = st.n_fallbacks;
+        out[3 * r + 2] = st.margin;
     }
     return MX_OK;
 }

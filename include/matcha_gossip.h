@@ -215,6 +215,11 @@ size_t mx_topk_work_bytes(int64_t P);
  * "select" = 0 (default): the selection after the compaction as four passes (candidate histograms
  * of the 10 and 9 low digits, threshold mark, placement), 1: as ONE launch (select_kernel: B
  * workgroups of 1024 threads per row meeting at two row barriers; measured slower);
+ * "floor_hint" = -1 (default): the compaction's candidate floor from a sampled histogram (one
+ * sampling launch per call); m >= 0: from the PREVIOUS call's exact k-th key on the same scratch,
+ * lowered by an adaptive per-row margin starting at m 12-bit bins (1 bin = 1/16 octave), and no
+ * sampling launch -- the first call on a scratch keeps every key; a floor too high re-runs the
+ * compaction keeping every key (the fallback), so results never change;
  * "select_blocks" = select_kernel workgroups per row (0 = auto: the fewest whose LDS caches every
  * candidate region, at most 32); "select_trace" = 1: select_kernel stores stage clocks in the
  * scratch (diagnostic, tools/select_trace.py).
@@ -228,6 +233,10 @@ int64_t mx_topk_get(const char* key);
  * that call's output undefined instead of hanging the GPU.  Synchronises `stream`, reads and clears
  * the words; MX_ERR_HIP if any was set.  (work, work_ld_bytes, nrows, P) as in the call checked. */
 int mx_topk_check(void* work, int64_t work_ld_bytes, int nrows, int64_t P, void* stream);
+/* Diagnostics of the candidate floor, per row r: out[3r] = calls made on this scratch, out[3r+1] =
+ * how many of them ran the fallback compaction (floor above the k-th key), out[3r+2] = the row's
+ * current floor_hint margin (bins).  Synchronises `stream`. */
+int mx_topk_stats(const void* work, int64_t work_ld_bytes, int nrows, int64_t P, int64_t* out, void* stream);
 int mx_topk_abs_diff(const float* x, const float* x_hat, int64_t P, int64_t k, float* vals,
                      int64_t* idx, void* work, void* stream);
 /* Batched form (one set of launches for every local worker): row r reads x + r*ld (and

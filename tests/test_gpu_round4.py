@@ -159,3 +159,58 @@ def test_mean_rows_to_matches_oracle(pkg, O, n, order, inplace):
         assert np.array_equal(_u32(got[d]), _u32(want)), d
     if not inplace:
         assert np.array_equal(rows[:, :P].cpu().numpy(), X)          # sources untouched
+
+
+@pytest.mark.parametrize("hint", [0, 3])
+def test_topk_floor_hint_exact_over_calls(pkg, O, hint):
+    """floor_hint (lever 1): the candidate floor of call t comes from call t-1's
+    exact k-th key on the same scratch (no sampling launch).  Six calls on 3 rows with x_hat
+    catching up (x_hat[idx] += vals, as ChocoCommunicator does) and drift; call 3 scales x by 100 (the
+    floor far too low: a huge candidate set), call 4 by 1e-4 with x_hat reset (the floor far too high:
+    the fallback compaction must run) -- every call's index set and values equal the oracle's, the first call
+    keeps every key (no hint yet), and the stats count 6 calls and >= 1 fallback per row."""
+    L = pkg.lib
+    n, P, ratio = 3, 2_000_001, 0.99
+    k = O.topk_k(P, ratio)
+    ld = (P + 63) // 64 * 64
+    X = np.stack([O.synth(40 + r, P) for r in range(n)])
+    XH = np.zeros_like(X)
+    x = torch.zeros((n, ld), dtype=torch.float32, device="cuda")
+    xh = torch.zeros_like(x)
+    kpad = (k + 1) // 2 * 2
+    msg_ld = (4 * kpad + 8 * k + 255) // 256 * 256
+    out = torch.zeros(n * msg_ld, dtype=torch.uint8, device="cuda")
+    wld = int(L.mx_topk_work_bytes(P))
+    work = torch.zeros(n * wld, dtype=torch.uint8, device="cuda")
+    saved = int(L.mx_topk_get(b"floor_hint"))
+    pkg._lib.check(L.mx_topk_set(b"floor_hint", hint))
+    try:
+        for t in range(6):
+            if t:
+                X = X + np.float32(0.01) * np.stack([O.synth(900 + 7 * t + r, P) for r in range(n)])
+            if t == 3:
+                X = X * np.float32(100.0)
+            if t == 4:                      # every key ~1e4 x smaller than the last k-th key
+                X = X * np.float32(1e-4)
+                XH[:] = 0
+            x[:, :P] = torch.from_numpy(X)
+            xh[:, :P] = torch.from_numpy(XH)
+            pkg._lib.check(L.mx_topk_abs_diff_rows(x.data_ptr(), xh.data_ptr(), ld, n, P, k, out.data_ptr(), msg_ld,
+                                                   4 * kpad, -1, work.data_ptr(), wld, None), "topk rows")
+            torch.cuda.synchronize()
+            for r in range(n):
+                vals = out[r * msg_ld:r * msg_ld + 4 * k].view(torch.float32).cpu().numpy()
+                idx = out[r * msg_ld + 4 * kpad:r * msg_ld + 4 * kpad + 8 * k].view(torch.int64).cpu().numpy()
+                D = np.subtract(X[r], XH[r], dtype=np.float32)
+                ov, oi = O.topk_abs(D, k)
+                assert np.array_equal(idx, oi), (t, r)
+                assert np.array_equal(_u32(vals), _u32(ov)), (t, r)
+                XH[r, oi] += ov
+        st = np.zeros(3 * n, np.int64)
+        pkg._lib.check(L.mx_topk_stats(work.data_ptr(), wld, n, P, st.ctypes.data, None))
+        assert L.mx_topk_check(work.data_ptr(), wld, n, P, None) == 0
+    finally:
+        L.mx_topk_set(b"floor_hint", saved)
+    st = st.reshape(n, 3)
+    print(f"\n[floor_hint {hint}] calls / fallbacks / margin per row: {st.tolist()}")
+    assert (st[:, 0] == 6).all() and (st[:, 1] >= 1).all(), st
