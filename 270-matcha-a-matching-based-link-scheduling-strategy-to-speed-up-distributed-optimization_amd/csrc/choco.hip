@@ -63,6 +63,7 @@ struct SelState {
     // row's adaptive margin below it, written by the call's threshold pass; call / fallback counts
     uint32_t hint_digit, hint_ok, margin;
     uint32_t n_calls, n_fallbacks;
+    uint32_t last_cand;   // the last call's candidate count (keys kept by its first compaction)
 };
 static_assert(sizeof(SelState) <= 64, "SelState must fit its 64-byte slot");
 
@@ -488,6 +489,7 @@ __device__ void record_round(const Rows& R, SelState* st, uint32_t T) {
     st->hint_ok = 1;
     st->n_calls += 1;
     st->n_fallbacks += fb ? 1u : 0u;
+    st->last_cand = (uint32_t)(cn < 0xffffffffull ? cn : 0xffffffffull);
 }
 
 template <bool BAL, bool LOOP, bool PF2 = false>
@@ -2074,7 +2076,8 @@ extern "C" int mx_topk_check(void* work, int64_t work_ld_bytes, int nrows, int64
     return MX_OK;
 }
 
-// Per row: {calls, fallback compactions, current floor-hint margin} (diagnostics of the floor choice).
+// Per row: {calls, fallback compactions, current floor-hint margin, the last call's threshold key T,
+// its candidate count} (diagnostics of the floor choice).
 extern "C" int mx_topk_stats(const void* work, int64_t work_ld_bytes, int nrows, int64_t P, int64_t* out,
                              void* stream) {
     MX_CHECK(work && out && nrows >= 1 && P >= 1 && (nrows == 1 || work_ld_bytes >= (int64_t)layout(P).total),
@@ -2084,9 +2087,11 @@ extern "C" int mx_topk_stats(const void* work, int64_t work_ld_bytes, int nrows,
         SelState st;
         MX_HIP(hipMemcpy(&st, static_cast<const char*>(work) + (int64_t)r * work_ld_bytes + layout(P).state, sizeof(st),
                          hipMemcpyDeviceToHost));
-        out[3 * r] = st.n_calls;
-        out[3 * r + 1] = st.n_fallbacks;
-        out[3 * r + 2] = st.margin;
+        out[5 * r] = st.n_calls;
+        out[5 * r + 1] = st.n_fallbacks;
+        out[5 * r + 2] = st.margin;
+        out[5 * r + 3] = st.T;
+        out[5 * r + 4] = st.last_cand;
     }
     return MX_OK;
 }

@@ -233,9 +233,10 @@ int64_t mx_topk_get(const char* key);
  * that call's output undefined instead of hanging the GPU.  Synchronises `stream`, reads and clears
  * the words; MX_ERR_HIP if any was set.  (work, work_ld_bytes, nrows, P) as in the call checked. */
 int mx_topk_check(void* work, int64_t work_ld_bytes, int nrows, int64_t P, void* stream);
-/* Diagnostics of the candidate floor, per row r: out[3r] = calls made on this scratch, out[3r+1] =
- * how many of them ran the fallback compaction (floor above the k-th key), out[3r+2] = the row's
- * current floor_hint margin (bins).  Synchronises `stream`. */
+/* Diagnostics of the candidate floor, per row r: out[5r] = calls made on this scratch, out[5r+1] =
+ * how many of them ran the fallback compaction (floor above the k-th key), out[5r+2] = the row's
+ * current floor_hint margin (bins), out[5r+3] = the last call's threshold key (bits of |k-th value|),
+ * out[5r+4] = its candidate count.  Synchronises `stream`. */
 int mx_topk_stats(const void* work, int64_t work_ld_bytes, int nrows, int64_t P, int64_t* out, void* stream);
 int mx_topk_abs_diff(const float* x, const float* x_hat, int64_t P, int64_t k, float* vals,
                      int64_t* idx, void* work, void* stream);

@@ -8,7 +8,7 @@ One row (a rank's share at N = 8, null transport, partner messages = copies of i
 (all workers on one GPU).  Per round: HIP events around the round only (the drift add is outside);
 fresh groups per variant (the hint lives in the scratch); interleaved repeats; the fallback count
 from mx_topk_stats.  Env: CHOCO_P, REPS, VARIANTS (comma list of floor_hint values, -1 = sampled),
-DRIFTS (comma list), ROUNDS."""
+DRIFTS (comma list), ROUNDS, TRACE."""
 import ctypes
 import importlib
 import json
@@ -29,6 +29,7 @@ REPS = int(os.environ.get("REPS", 2))
 VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "-1,2,4,8").split(",")]
 DRIFTS = [float(v) for v in os.environ.get("DRIFTS", "0.01,0").split(",")]
 ROUNDS = int(os.environ.get("ROUNDS", 40))
+TRACE = int(os.environ.get("TRACE", 0))        # 1: per round row 0's threshold key, candidates, fallbacks
 WARM = 5
 n = 8
 GP = pkg.MatchaProcessor(pkg.select_graph(0), 1.0, 0, n, ROUNDS + WARM + 2, True)
@@ -58,7 +59,7 @@ def make(kind):
 def run(kind, hint, drift, noise):
     pkg._lib.check(L.mx_topk_set(b"floor_hint", hint))
     c = make(kind)
-    us = []
+    us, trace = [], []
     for it in range(WARM + ROUNDS):
         if drift and it:
             c.rows.add_(noise[:c.n_local], alpha=drift)
@@ -69,12 +70,19 @@ def run(kind, hint, drift, noise):
         torch.cuda.synchronize()
         if it >= WARM:
             us.append(a.elapsed_time(b) * 1e3)
-    st = np.zeros(3 * c.n_local, np.int64)
+        if TRACE:
+            sr = np.zeros(5 * c.n_local, np.int64)
+            pkg._lib.check(L.mx_topk_stats(c.work.data_ptr(), c.work_ld, c.n_local, c.numel, sr.ctypes.data, None))
+            trace.append((float(np.uint32(sr[3]).view(np.float32)), int(sr[4]), int(sr[1])))
+    if TRACE:
+        print(json.dumps({"trace": kind, "drift": drift, "floor_hint": hint, "k": c.k,
+                          "T_cand_fb": [(round(t, 6), cn, fb) for t, cn, fb in trace]}), flush=True)
+    st = np.zeros(5 * c.n_local, np.int64)
     pkg._lib.check(L.mx_topk_stats(c.work.data_ptr(), c.work_ld, c.n_local, c.numel, st.ctypes.data, None))
     c.check_topk()
     del c
     torch.cuda.empty_cache()
-    st = st.reshape(-1, 3)
+    st = st.reshape(-1, 5)
     return {"round_us_median": float(np.median(us)), "round_us_mean": float(np.mean(us)),
             "calls": int(st[:, 0].max()), "fallbacks": int(st[:, 1].sum()), "margins": st[:, 2].tolist()}
 
