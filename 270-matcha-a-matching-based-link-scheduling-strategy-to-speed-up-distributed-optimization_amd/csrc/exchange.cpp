@@ -434,6 +434,62 @@ __global__ __launch_bounds__(256) void mean_to_kernel(const V* rows, int nrows, 
     }
 }
 
+// The 16-byte path with U columns (4-float vectors) per lane per step, U loads per row in flight:
+// columns base + u * 256 + lane of a U * 256-column block; blocks strided over the grid.
+template <int TREE, int U>
+__global__ __launch_bounds__(256) void mean4_kernel(const f4v* rows, int nrows, int64_t ld, int64_t count,
+                                                    float size, f4v* dst, int ndst, int64_t dst_ld) {
+    for (int64_t b0 = (int64_t)blockIdx.x * (U * 256); b0 < count; b0 += (int64_t)gridDim.x * (U * 256)) {
+        f4v acc[U];
+        if (TREE) {
+            f4v v[8][U];
+#pragma unroll
+            for (int r = 0; r < 8; ++r)
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int64_t i = b0 + u * 256 + threadIdx.x;
+                    v[r][u] = (r < nrows && i < count) ? __builtin_nontemporal_load(rows + (int64_t)r * ld + i)
+                                                       : f4v(0.0f);
+                }
+#pragma unroll
+            for (int m = 1; m < 8; m <<= 1)
+#pragma unroll
+                for (int r = 0; r + m < 8; r += 2 * m)
+                    if (r + m < nrows)
+#pragma unroll
+                        for (int u = 0; u < U; ++u) v[r][u] = v[r][u] + v[r + m][u];
+#pragma unroll
+            for (int u = 0; u < U; ++u) acc[u] = v[0][u];
+        } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = b0 + u * 256 + threadIdx.x;
+                acc[u] = i < count ? __builtin_nontemporal_load(rows + i) : f4v(0.0f);
+            }
+            for (int r = 1; r < nrows; ++r)
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const int64_t i = b0 + u * 256 + threadIdx.x;
+                    acc[u] = acc[u] + (i < count ? __builtin_nontemporal_load(rows + (int64_t)r * ld + i) : f4v(0.0f));
+                }
+        }
+        for (int d = 0; d < ndst; ++d)
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = b0 + u * 256 + threadIdx.x;
+                if (i < count) __builtin_nontemporal_store(acc[u] / size, dst + (int64_t)d * dst_ld + i);
+            }
+    }
+}
+
+int mean_variant() {               // A/B of the 16-byte path's geometry (MX_MEAN_VARIANT, experiment only)
+    static int v = [] {
+        const char* e = getenv("MX_MEAN_VARIANT");
+        return e ? atoi(e) : 0;
+    }();
+    return v;
+}
+
 inline unsigned grid_of(int64_t count) {
     int64_t g = (count + 255) / 256;
     return (unsigned)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
@@ -505,7 +561,18 @@ extern "C" int mx_mean_rows_to(const float* rows, int nrows, int64_t ld, int64_t
         if (g > 4096) g = 4096;
         const f4v* r4 = reinterpret_cast<const f4v*>(rows);
         f4v* d4 = reinterpret_cast<f4v*>(dst);
-        if (order == 1)
+        const int var = mean_variant();
+        if (var > 0) {
+            // 1: flat grid, U = 1; 2: flat, U = 2; 3: CUs x 8 persistent, U = 2; 4: flat, U = 4
+            const int U = var == 1 ? 1 : var == 4 ? 4 : 2;
+            int64_t gg = (c4 + U * 256 - 1) / (U * 256);
+            if (var == 3 && gg > 256 * 8) gg = 256 * 8;
+#define MX_M4(T, UU) hipLaunchKernelGGL((mean4_kernel<T, UU>), dim3((unsigned)gg), dim3(256), 0, st, r4, nrows, ld / 4, \
+                                        c4, d, d4, ndst, dst_ld / 4)
+            if (order == 1) { if (U == 1) MX_M4(0, 1); else if (U == 2) MX_M4(0, 2); else MX_M4(0, 4); }
+            else { if (U == 1) MX_M4(1, 1); else if (U == 2) MX_M4(1, 2); else MX_M4(1, 4); }
+#undef MX_M4
+        } else if (order == 1)
             hipLaunchKernelGGL((mean_to_kernel<f4v, 0, 1>), dim3((unsigned)g), dim3(256), 0, st, r4, nrows, ld / 4, c4,
                                d, d4, ndst, dst_ld / 4);
         else
