@@ -50,7 +50,11 @@ constexpr int kMidBits = 10, kMidShift = 9;  // bits 9..18
 constexpr int kLowBits = 9;                  // bits 0..8
 constexpr int64_t kSampleTarget = 1 << 18;   // sampled elements per row (auto stride)
 
-constexpr int kHistWords = 3 * kTopBins + (1 << kMidBits) + (1 << kLowBits);   // hs, h12, h12f, h10, h9
+// fine sampled floor ("fine_floor"): a window of kWinBins top digits around the last call's k-th
+// key, each split into kFineSub sub-bins (key bits 13..18), sampled beside the 12-bit histogram
+constexpr int kWinBins = 16, kFineSub = 64, kFineShift = 13;
+constexpr int kFineBins = kWinBins * kFineSub;
+constexpr int kHistWords = 3 * kTopBins + (1 << kMidBits) + (1 << kLowBits) + kFineBins;   // hs, h12, h12f, h10, h9, hsf
 
 struct SelState {
     uint32_t b0;          // lowest top digit kept as a candidate (b_lo)
@@ -116,6 +120,7 @@ struct Rows {
     int64_t P, k;
     int64_t bnd_off;      // int32 tile bounds at out + r*out_ld + bnd_off (< 0: not written)
     int32_t hint;         // floor_hint margin in 12-bit bins (< 0: sampled floor)
+    int32_t fine;         // fine_floor: 1 = refine the sampled floor inside the window (sub-bins)
 };
 
 struct RowView {
@@ -126,6 +131,7 @@ struct RowView {
     uint32_t* h12f;       // the same, of the fallback pass (keeps every key)
     uint32_t* h10;        // next 10 bits of the candidates in the threshold bin
     uint32_t* h9;         // last 9 bits
+    uint32_t* hsf;        // fine sampled sub-bins of the window (fine_floor)
     SelState* st;
     int64_t* cnt;
     int64_t* bt;          // cand_mark block totals (keys > T, keys == T)
@@ -146,6 +152,7 @@ __device__ __forceinline__ RowView row_view(const Rows& R, int r) {
     v.h12f = v.h12 + kTopBins;
     v.h10 = v.h12f + kTopBins;
     v.h9 = v.h10 + (1 << kMidBits);
+    v.hsf = v.h9 + (1 << kLowBits);
     v.st = reinterpret_cast<SelState*>(wb + w.state);
     v.cnt = reinterpret_cast<int64_t*>(wb + w.cnt);
     v.bt = reinterpret_cast<int64_t*>(wb + w.bt);
@@ -253,10 +260,23 @@ __device__ __forceinline__ int64_t lane63(int64_t v) {
     return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
+// The fine window's first top digit: kWinBins digits from 12 below the last call's k-th key's digit
+// (the floor sits a few digits below the k-th key); -1 = no window (fine_floor off, or no call yet).
+// The sampling pass and the compaction read the same state, so they agree.
+__device__ __forceinline__ int fine_window(const Rows& R, const RowView& v) {
+    if (!R.fine || !v.st->hint_ok) return -1;
+    const int d = (int)v.st->hint_digit - 12;
+    return d < 0 ? 0 : d > kTopBins - kWinBins ? kTopBins - kWinBins : d;
+}
+
 // ---- S: top-digit histogram over every S-th 1024-element piece, one wave per sampled piece;
-// this block takes pieces (bx + i gx) * kWaves + wave into its LDS histogram h (zeroed here)
-__device__ __forceinline__ void sample_into(const Rows& R, const RowView& v, int64_t S, int64_t bx, int64_t gx, uint32_t* h) {
+// this block takes pieces (bx + i gx) * kWaves + wave into its LDS histogram h (zeroed here), and
+// with a fine window w0 >= 0 the keys of digits [w0, w0 + kWinBins) also into the sub-bins hf
+__device__ __forceinline__ void sample_into(const Rows& R, const RowView& v, int64_t S, int64_t bx, int64_t gx, uint32_t* h,
+                                            uint32_t* hf = nullptr, int w0 = -1) {
     for (int i = threadIdx.x; i < kTopBins; i += kTPB) h[i] = 0;
+    if (w0 >= 0)
+        for (int i = threadIdx.x; i < kFineBins; i += kTPB) hf[i] = 0;
     __syncthreads();
     const bool vec = (((uintptr_t)v.x | (uintptr_t)v.xh) & 15) == 0;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -271,7 +291,13 @@ __device__ __forceinline__ void sample_into(const Rows& R, const RowView& v, int
         for (int j = 0; j < 4; ++j)
 #pragma unroll
             for (int c = 0; c < 4; ++c)
-                if (c < n[j]) atomicAdd(&h[key_of(d[j][c]) >> kTopShift], 1u);
+                if (c < n[j]) {
+                    const uint32_t key = key_of(d[j][c]);
+                    atomicAdd(&h[key >> kTopShift], 1u);
+                    const uint32_t wd = (key >> kTopShift) - (uint32_t)w0;
+                    if (w0 >= 0 && wd < (uint32_t)kWinBins)
+                        atomicAdd(&hf[wd * kFineSub + ((key >> kFineShift) & (kFineSub - 1))], 1u);
+                }
     }
     __syncthreads();
 }
@@ -279,9 +305,14 @@ __device__ __forceinline__ void sample_into(const Rows& R, const RowView& v, int
 __global__ __launch_bounds__(kTPB) void sample_kernel(Rows R, int64_t S) {
     const RowView v = row_view(R);
     __shared__ uint32_t h[kTopBins];
-    sample_into(R, v, S, blockIdx.x, gridDim.x, h);
+    __shared__ uint32_t hf[kFineBins];
+    const int w0 = fine_window(R, v);
+    sample_into(R, v, S, blockIdx.x, gridDim.x, h, hf, w0);
     for (int i = threadIdx.x; i < kTopBins; i += kTPB)
         if (h[i]) atomicAdd(&v.hs[i], h[i]);
+    if (w0 >= 0)
+        for (int i = threadIdx.x; i < kFineBins; i += kTPB)
+            if (hf[i]) atomicAdd(&v.hsf[i], hf[i]);
 }
 
 typedef __attribute__((address_space(1))) uint32_t g_u32;
@@ -458,12 +489,14 @@ __device__ Resolved resolve(const RowView& v, int64_t k, int stages) {
 // to the sample with a 25 % + 4 sigma margin.  S = 0 (floor_hint): the previous call's exact k-th
 // key's digit lowered by the row's adaptive margin (no sampling launch); the first call on a scratch
 // has no hint and keeps every key.  A floor too high is caught by the candidate count (fallback).
-__device__ uint32_t floor_digit(const Rows& R, const RowView& v, int64_t S, double frac) {
+// Returned as a KEY floor (keys >= it are kept): a digit's first key, or with fine_floor, when the
+// floor's digit falls in the window, that digit's sub-bin holding the wanted sampled rank.
+__device__ uint32_t floor_key(const Rows& R, const RowView& v, int64_t S, double frac) {
     if (S == 0) {
         if (!v.st->hint_ok) return 0u;
         const uint32_t m = v.st->margin ? v.st->margin : (uint32_t)(R.hint > 0 ? R.hint : 1);
         const uint32_t d = v.st->hint_digit;
-        return d > m ? d - m : 0u;
+        return (d > m ? d - m : 0u) << kTopShift;
     }
     int64_t want = R.k;
     if (S > 1) {
@@ -473,13 +506,21 @@ __device__ uint32_t floor_digit(const Rows& R, const RowView& v, int64_t S, doub
     int b;
     int64_t rem, tot;
     find_bin<kTopBins>(v.hs, want, &b, &rem, &tot);
-    return tot < want ? 0u : (uint32_t)b;                   // too few sampled keys: keep everything
+    if (tot < want) return 0u;                              // too few sampled keys: keep everything
+    const int w0 = fine_window(R, v);                       // block-uniform
+    if (w0 >= 0 && b >= w0 && b < w0 + kWinBins) {
+        int sb;
+        int64_t rem2, tot2;
+        find_bin<kFineSub>(v.hsf + (b - w0) * kFineSub, rem, &sb, &rem2, &tot2);
+        if (tot2 >= rem) return ((uint32_t)b << kTopShift) | ((uint32_t)sb << kFineShift);
+    }
+    return (uint32_t)b << kTopShift;
 }
 
 // After the threshold pass resolved T (one thread per row): the next call's floor hint, the margin
 // adapted (a fallback widens it by 4 bins, a candidate set above 4 k narrows it by one), counts.
-__device__ void record_round(const Rows& R, SelState* st, uint32_t T) {
-    const unsigned long long cn = st->cand_n;
+// cn = this call's candidate count (keys kept by the first compaction).
+__device__ void record_round(const Rows& R, SelState* st, uint32_t T, unsigned long long cn) {
     const bool fb = cn < (unsigned long long)R.k;
     uint32_t m = st->margin ? st->margin : (uint32_t)(R.hint > 0 ? R.hint : 1);
     if (fb) m = m + 4 < 255 ? m + 4 : 255;
@@ -520,9 +561,10 @@ __device__ void compact_run(const Rows& R, const RowView& v, int64_t S, double f
         if (c + gx < nc && whole(c + gx)) issue_to(px, ph, c + gx);
     }
 
-    uint32_t b_lo = 0;
+    uint32_t b_lo = 0, fkey = 0;                   // floor: keys >= fkey (digit b_lo) are kept
     if (!fallback) {
-        b_lo = floor_digit(R, v, S, frac);
+        fkey = floor_key(R, v, S, frac);
+        b_lo = fkey >> kTopShift;
         if (bx == 0 && threadIdx.x == 0) {
             v.st->b0 = b_lo;
             v.st->bar = 0;                                  // the selection's row barriers start here
@@ -548,8 +590,9 @@ __device__ void compact_run(const Rows& R, const RowView& v, int64_t S, double f
             wt[j] = 0;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const uint32_t dg = key_of(d[j][e]) >> kTopShift;
-                const bool f = e < n[j] && dg >= b_lo;
+                const uint32_t key = key_of(d[j][e]);
+                const uint32_t dg = key >> kTopShift;
+                const bool f = e < n[j] && key >= fkey;
                 keep |= (f ? 1u : 0u) << (4 * j + e);
                 if constexpr (BAL) {                    // ballots + mbcnt instead of a shuffle scan
                     const uint64_t b = __ballot(f);
@@ -707,9 +750,10 @@ __global__ __launch_bounds__(kTPB) void compact_wave_kernel(Rows R, int64_t S, d
     };
     int64_t s = 0;
     if (chunk_of(0) < nfull) issue(0);             // in flight while b_lo is resolved
-    uint32_t b_lo = 0;
+    uint32_t b_lo = 0, fkey = 0;
     {
-        b_lo = floor_digit(R, v, S, frac);
+        fkey = floor_key(R, v, S, frac);
+        b_lo = fkey >> kTopShift;
         if (blockIdx.x == 0 && threadIdx.x == 0) {
             v.st->b0 = b_lo;
             v.st->bar = 0;
@@ -729,8 +773,9 @@ __global__ __launch_bounds__(kTPB) void compact_wave_kernel(Rows R, int64_t S, d
             wt[j] = 0;
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const uint32_t dg = key_of(d[j][e]) >> kTopShift;
-                const bool f = e < n[j] && dg >= b_lo;
+                const uint32_t key = key_of(d[j][e]);
+                const uint32_t dg = key >> kTopShift;
+                const bool f = e < n[j] && key >= fkey;
                 keep |= (f ? 1u : 0u) << (4 * j + e);
                 if constexpr (BAL) {
                     const uint64_t b = __ballot(f);
@@ -922,7 +967,7 @@ __global__ __launch_bounds__(kTPB) void cand_mark(Rows R, int64_t G) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         v.st->T = T;
         v.st->need = z.need;
-        record_round(R, v.st, T);
+        record_round(R, v.st, T, v.st->cand_n);
     }
     __shared__ uint32_t sg[kWaves], se[kWaves];
     uint32_t wg = 0, we = 0;
@@ -1288,6 +1333,7 @@ __global__ __launch_bounds__(kSelTPB) void select_kernel(Rows R, int row0, int B
     stamp(3);
     if (b == 0) {                                // nothing reads the 12-bit histograms or the
         for (int i = tid; i < 3 * kTopBins; i += kSelTPB) v.hs[i] = 0;   // candidate total any more
+        for (int i = tid; i < kFineBins; i += kSelTPB) v.hsf[i] = 0;
         if (tid == 0) v.st->cand_n = 0;
     }
     {
@@ -1360,7 +1406,7 @@ __global__ __launch_bounds__(kSelTPB) void select_kernel(Rows R, int row0, int B
     if (b == 0 && tid == 0) {
         v.st->T = T;
         v.st->need = need_eq;
-        record_round(R, v.st, T);
+        record_round(R, v.st, T, cand_n);
     }
 
     int32_t* bnd = R.bnd_off >= 0 ? reinterpret_cast<int32_t*>(R.out + (int64_t)r * R.out_ld + R.bnd_off) : nullptr;
@@ -1800,6 +1846,8 @@ int g_cand_chunks = 0;        // chunk regions per wave of cand_hist / cand_mark
                               // flush of cand_hist<10>'s 1024 bins measured +3.7 us on one row; same-box
                               // sweep 2 -> 4 / 8: one row 121.7 -> 119.6 us, 8 rows 655 -> 640 us)
 
+int g_fine_floor = 0;          // 1: the sampled floor refined to 1/64 of a top digit inside a window around
+                               // the last call's k-th key (fewer candidates kept), 0: digit floor
 int g_floor_hint = -1;         // >= 0: candidate floor from the previous call's k-th key minus this many
                                // 12-bit bins (adaptive per row), no sampling launch; -1: sampled floor
 unsigned g_hist_grid = 0;      // the last call's cand_hist<10> grid per row, and the co-resident cap it
@@ -1909,6 +1957,11 @@ extern "C" int mx_topk_set(const char* key, int64_t value) {
         g_select = (int)value;
         return MX_OK;
     }
+    if (!strcmp(key, "fine_floor")) {
+        MX_CHECK(value == 0 || value == 1, "mx_topk_set: fine_floor %lld", (long long)value);
+        g_fine_floor = (int)value;
+        return MX_OK;
+    }
     if (!strcmp(key, "floor_hint")) {
         MX_CHECK(value >= -1 && value <= 64, "mx_topk_set: floor_hint %lld (-1 off, 0..64 bins)", (long long)value);
         g_floor_hint = (int)value;
@@ -1946,6 +1999,7 @@ extern "C" int64_t mx_topk_get(const char* key) {
     if (key && !strcmp(key, "select_trace")) return g_select_trace;
     if (key && !strcmp(key, "hist_grid")) return g_hist_grid;
     if (key && !strcmp(key, "floor_hint")) return g_floor_hint;
+    if (key && !strcmp(key, "fine_floor")) return g_fine_floor;
     if (key && !strcmp(key, "hist_capacity")) return g_hist_capacity;
     mx::set_error("mx_topk_get: unknown key '%s'", key ? key : "(null)");
     return MX_ERR_INVALID;
@@ -1967,7 +2021,7 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
              "mx_topk_abs_diff_rows: work must be 256-byte aligned");
     hipStream_t st = mx::as_stream(stream);
     Rows R{x, x_hat, ld, static_cast<char*>(out), out_ld_bytes, idx_off_bytes, static_cast<char*>(work),
-           work_ld_bytes, P, k, bnd_off_bytes, (int32_t)g_floor_hint};
+           work_ld_bytes, P, k, bnd_off_bytes, (int32_t)g_floor_hint, (int32_t)g_fine_floor};
     const int64_t nc = n_chunks(P);
     // S = 0: the floor comes from the previous call's k-th key (floor_hint), no sampling launch
     const int64_t S = g_floor_hint >= 0 ? 0 : sample_stride(P);

@@ -161,10 +161,11 @@ def test_mean_rows_to_matches_oracle(pkg, O, n, order, inplace):
         assert np.array_equal(rows[:, :P].cpu().numpy(), X)          # sources untouched
 
 
-@pytest.mark.parametrize("hint", [0, 3])
-def test_topk_floor_hint_exact_over_calls(pkg, O, hint):
+@pytest.mark.parametrize("hint,fine", [(0, 0), (3, 0), (-1, 1)])
+def test_topk_floor_hint_exact_over_calls(pkg, O, hint, fine):
     """floor_hint (lever 1): the candidate floor of call t comes from call t-1's
-    exact k-th key on the same scratch (no sampling launch).  Six calls on 3 rows with x_hat
+    exact k-th key on the same scratch (no sampling launch); fine_floor: the sampled floor refined
+    to 1/64 of a digit inside a window around call t-1's k-th key.  Six calls on 3 rows with x_hat
     catching up (x_hat[idx] += vals, as ChocoCommunicator does) and drift; call 3 scales x by 100 (the
     floor far too low: a huge candidate set), call 4 by 1e-4 with x_hat reset (the floor far too high:
     the fallback compaction must run) -- every call's index set and values equal the oracle's, the first call
@@ -182,8 +183,9 @@ def test_topk_floor_hint_exact_over_calls(pkg, O, hint):
     out = torch.zeros(n * msg_ld, dtype=torch.uint8, device="cuda")
     wld = int(L.mx_topk_work_bytes(P))
     work = torch.zeros(n * wld, dtype=torch.uint8, device="cuda")
-    saved = int(L.mx_topk_get(b"floor_hint"))
+    saved = int(L.mx_topk_get(b"floor_hint")), int(L.mx_topk_get(b"fine_floor"))
     pkg._lib.check(L.mx_topk_set(b"floor_hint", hint))
+    pkg._lib.check(L.mx_topk_set(b"fine_floor", fine))
     try:
         for t in range(6):
             if t:
@@ -210,7 +212,11 @@ def test_topk_floor_hint_exact_over_calls(pkg, O, hint):
         pkg._lib.check(L.mx_topk_stats(work.data_ptr(), wld, n, P, st.ctypes.data, None))
         assert L.mx_topk_check(work.data_ptr(), wld, n, P, None) == 0
     finally:
-        L.mx_topk_set(b"floor_hint", saved)
+        L.mx_topk_set(b"floor_hint", saved[0])
+        L.mx_topk_set(b"fine_floor", saved[1])
     st = st.reshape(n, 5)
-    print(f"\n[floor_hint {hint}] calls / fallbacks / margin per row: {st.tolist()}")
-    assert (st[:, 0] == 6).all() and (st[:, 1] >= 1).all(), st
+    print(f"\n[floor_hint {hint} fine_floor {fine}] calls / fallbacks / margin / T / candidates per row: "
+          f"{st.tolist()}")
+    assert (st[:, 0] == 6).all(), st
+    if hint >= 0:
+        assert (st[:, 1] >= 1).all(), st

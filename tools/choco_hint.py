@@ -7,8 +7,8 @@ VGG test's 0.01 x synth) -- and without drift (the bench figure).  VERDICT r03 i
 One row (a rank's share at N = 8, null transport, partner messages = copies of its own) and 8 rows
 (all workers on one GPU).  Per round: HIP events around the round only (the drift add is outside);
 fresh groups per variant (the hint lives in the scratch); interleaved repeats; the fallback count
-from mx_topk_stats.  Env: CHOCO_P, REPS, VARIANTS (comma list of floor_hint values, -1 = sampled),
-DRIFTS (comma list), ROUNDS, TRACE."""
+from mx_topk_stats.  Env: CHOCO_P, REPS, VARIANTS (s / f / h<m>, below), DRIFTS (comma list), ROUNDS,
+TRACE."""
 import ctypes
 import importlib
 import json
@@ -26,7 +26,9 @@ from nullcomm import NullComm  # noqa: E402
 
 P = int(os.environ.get("CHOCO_P", 14_774_436))
 REPS = int(os.environ.get("REPS", 2))
-VARIANTS = [int(v) for v in os.environ.get("VARIANTS", "-1,2,4,8").split(",")]
+# variants: "s" sampled digit floor (default), "f" sampled floor refined in a window (fine_floor),
+# "h<m>" floor from the previous call's k-th key, margin m bins (floor_hint m)
+VARIANTS = os.environ.get("VARIANTS", "s,f,h2,h4").split(",")
 DRIFTS = [float(v) for v in os.environ.get("DRIFTS", "0.01,0").split(",")]
 ROUNDS = int(os.environ.get("ROUNDS", 40))
 TRACE = int(os.environ.get("TRACE", 0))        # 1: per round row 0's threshold key, candidates, fallbacks
@@ -45,10 +47,11 @@ def make(kind):
     c = pkg.ChocoWorkerGroup(GP, numel=P, ratio=0.99, consensus_lr=0.1, rank=0, nranks=8, comm=NullComm(0, 8),
                              placement="auto")
     pkg._lib.check(L.mx_synth_fill(c.rows[0].data_ptr(), P, 1234 + c.workers[0], None))
-    saved = int(L.mx_topk_get(b"floor_hint"))
-    L.mx_topk_set(b"floor_hint", -1)
+    saved = (int(L.mx_topk_get(b"floor_hint")), int(L.mx_topk_get(b"fine_floor")))
+    knobs("s")
     c.compress(0)                               # stand-in partner messages (then a fresh scratch)
-    L.mx_topk_set(b"floor_hint", saved)
+    L.mx_topk_set(b"floor_hint", saved[0])
+    L.mx_topk_set(b"fine_floor", saved[1])
     torch.cuda.synchronize()
     for s in range(c.n_local, c.engine.n_slots):
         c.msgs[s * c.msg_ld:(s + 1) * c.msg_ld].copy_(c.msgs[:c.msg_ld])
@@ -56,8 +59,13 @@ def make(kind):
     return c
 
 
+def knobs(variant):
+    pkg._lib.check(L.mx_topk_set(b"floor_hint", int(variant[1:]) if variant.startswith("h") else -1))
+    pkg._lib.check(L.mx_topk_set(b"fine_floor", 1 if variant == "f" else 0))
+
+
 def run(kind, hint, drift, noise):
-    pkg._lib.check(L.mx_topk_set(b"floor_hint", hint))
+    knobs(hint)
     c = make(kind)
     us, trace = [], []
     for it in range(WARM + ROUNDS):
@@ -80,11 +88,13 @@ def run(kind, hint, drift, noise):
     st = np.zeros(5 * c.n_local, np.int64)
     pkg._lib.check(L.mx_topk_stats(c.work.data_ptr(), c.work_ld, c.n_local, c.numel, st.ctypes.data, None))
     c.check_topk()
+    c_k = c.k
     del c
     torch.cuda.empty_cache()
     st = st.reshape(-1, 5)
     return {"round_us_median": float(np.median(us)), "round_us_mean": float(np.mean(us)),
-            "calls": int(st[:, 0].max()), "fallbacks": int(st[:, 1].sum()), "margins": st[:, 2].tolist()}
+            "calls": int(st[:, 0].max()), "fallbacks": int(st[:, 1].sum()), "margins": st[:, 2].tolist(),
+            "last_candidates_per_k": [round(int(x) / c_k, 2) for x in st[:, 4]]}
 
 
 noise = torch.empty((n, P), dtype=torch.float32, device="cuda")
@@ -98,7 +108,7 @@ for rep in range(REPS):
                 r = run(kind, hint, drift, noise)
                 res.setdefault((kind, drift, hint), []).append(r)
                 print(json.dumps({"rep": rep, "group": kind, "drift": drift, "floor_hint": hint, **r}), flush=True)
-L.mx_topk_set(b"floor_hint", -1)
+knobs("s")
 for (kind, drift, hint), rs in res.items():
     print(json.dumps({"summary": True, "group": kind, "drift": drift, "floor_hint": hint,
                       "round_us_median": round(float(np.median([r["round_us_median"] for r in rs])), 2),
