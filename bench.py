@@ -579,8 +579,16 @@ def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99
     for it in range(W):
         grp.step(it)
     el = timed_loop(grp.step, W, K, world, dev)
+    st = np.zeros(5 * grp.n_local, np.int64)
+    pkg._lib.check(pkg.lib.mx_topk_stats(grp.work.data_ptr(), grp.work_ld, grp.n_local, grp.numel, st.ctypes.data,
+                                         None), "mx_topk_stats")
+    grp.check_topk()                              # no bounded row-barrier wait expired
+    st = st.reshape(-1, 5)
     out = {"config": f"P={P} (VGG-16 size by default), ratio {ratio} (k={grp.k}), gamma {gamma}, graph 0 full rounds",
-           "rounds_per_s": K / el, "ms_per_round": 1e3 * el / K, "rows_per_gpu": grp.n_local, "rounds": K}
+           "rounds_per_s": K / el, "ms_per_round": 1e3 * el / K, "rows_per_gpu": grp.n_local, "rounds": K,
+           "topk": {"calls_per_row": int(st[:, 0].max()), "fallback_compactions": int(st[:, 1].sum()),
+                    "candidates_per_k_last": [round(int(c) / grp.k, 2) for c in st[:, 4]],
+                    "floor": "fine sampled" if pkg.lib.mx_topk_get(b"fine_floor") == 1 else "sampled digit"}}
     out["parity_ok"] = choco_oracle_round(pkg, grp, GP, W + K, ratio, gamma, rank, world)
     out["parity"] = (f"round {W + K} (after the {W} warmup + {K} timed rounds) of every worker: x, x_hat, s vs the "
                      f"oracle's Choco round from the same state, uint32")
