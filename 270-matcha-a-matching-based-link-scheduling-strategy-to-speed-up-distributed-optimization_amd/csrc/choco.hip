@@ -1846,8 +1846,11 @@ int g_cand_chunks = 0;        // chunk regions per wave of cand_hist / cand_mark
                               // flush of cand_hist<10>'s 1024 bins measured +3.7 us on one row; same-box
                               // sweep 2 -> 4 / 8: one row 121.7 -> 119.6 us, 8 rows 655 -> 640 us)
 
-int g_fine_floor = 0;          // 1: the sampled floor refined to 1/64 of a top digit inside a window around
-                               // the last call's k-th key (fewer candidates kept), 0: digit floor
+int g_fine_floor = 1;          // 1: the sampled floor refined to 1/64 of a top digit inside a window around
+                               // the last call's k-th key, 0: the digit floor.  Same box, 3 interleaved
+                               // repeats (tools/choco_hint.py, profiles/r04b_choco_fine_floor.log): 8 rows
+                               // keep 1.35 k candidates instead of 1.5-4.2 k, 629-633 -> 598-613 us per
+                               // round with and without drift; one row neutral (102.0-103.2 us)
 int g_floor_hint = -1;         // >= 0: candidate floor from the previous call's k-th key minus this many
                                // 12-bit bins (adaptive per row), no sampling launch; -1: sampled floor
 unsigned g_hist_grid = 0;      // the last call's cand_hist<10> grid per row, and the co-resident cap it

@@ -382,8 +382,8 @@ __global__ __launch_bounds__(256) void mean_rows_kernel(const float* rows, int n
 // mean_rows_kernel with the mean written to ndst destination rows (dst + d * dst_ld) instead of
 // one: the all-reduce of centralizedCommunicator for workers held as rows of one arena (every
 // worker's row becomes the mean) in ONE pass -- each lane reads a column of every row, then writes
-// that column of every destination row, so dst == rows (in place) is safe.  V = a 4-float vector
-// (16-byte non-temporal accesses; TREE 1 over <= 8 rows, or rank order), or float (any other case).
+// that column of every destination row, so dst == rows (in place) is safe.  Scalar form (any row
+// count, order, alignment); the 16-byte form is mean4_kernel below.
 typedef float f4v __attribute__((ext_vector_type(4)));
 
 template <typename V, int TREE, int MAXR>
@@ -482,14 +482,6 @@ __global__ __launch_bounds__(256) void mean4_kernel(const f4v* rows, int nrows, 
     }
 }
 
-int mean_variant() {               // A/B of the 16-byte path's geometry (MX_MEAN_VARIANT, experiment only)
-    static int v = [] {
-        const char* e = getenv("MX_MEAN_VARIANT");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
-}
-
 inline unsigned grid_of(int64_t count) {
     int64_t g = (count + 255) / 256;
     return (unsigned)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
@@ -557,27 +549,20 @@ extern "C" int mx_mean_rows_to(const float* rows, int nrows, int64_t ld, int64_t
                                    tail, d, dst + o, ndst, dst_ld);
             MX_LAUNCH_CHECK();
         }
-        int64_t g = (c4 + 255) / 256;
-        if (g > 4096) g = 4096;
         const f4v* r4 = reinterpret_cast<const f4v*>(rows);
         f4v* d4 = reinterpret_cast<f4v*>(dst);
-        const int var = mean_variant();
-        if (var > 0) {
-            // 1: flat grid, U = 1; 2: flat, U = 2; 3: CUs x 8 persistent, U = 2; 4: flat, U = 4
-            const int U = var == 1 ? 1 : var == 4 ? 4 : 2;
-            int64_t gg = (c4 + U * 256 - 1) / (U * 256);
-            if (var == 3 && gg > 256 * 8) gg = 256 * 8;
-#define MX_M4(T, UU) hipLaunchKernelGGL((mean4_kernel<T, UU>), dim3((unsigned)gg), dim3(256), 0, st, r4, nrows, ld / 4, \
-                                        c4, d, d4, ndst, dst_ld / 4)
-            if (order == 1) { if (U == 1) MX_M4(0, 1); else if (U == 2) MX_M4(0, 2); else MX_M4(0, 4); }
-            else { if (U == 1) MX_M4(1, 1); else if (U == 2) MX_M4(1, 2); else MX_M4(1, 4); }
-#undef MX_M4
-        } else if (order == 1)
-            hipLaunchKernelGGL((mean_to_kernel<f4v, 0, 1>), dim3((unsigned)g), dim3(256), 0, st, r4, nrows, ld / 4, c4,
-                               d, d4, ndst, dst_ld / 4);
+        // a flat grid, 4 vectors per lane (16 loads in flight per lane for 4 rows): 0.285 ms for
+        // 8 x 25.6M in place = 0.72 of 8 TB/s, against 0.322 ms for a 4096-block persistent grid
+        // with one vector per lane per step, 0.287 with two, 0.31 with two on CUs x 8 blocks
+        // (tools/mean_ab.py, profiles/r04b_mean_rows_geometry.log)
+        constexpr int U = 4;
+        const int64_t gg = (c4 + U * 256 - 1) / (U * 256);
+        if (order == 1)
+            hipLaunchKernelGGL((mean4_kernel<0, U>), dim3((unsigned)gg), dim3(256), 0, st, r4, nrows, ld / 4, c4, d, d4,
+                               ndst, dst_ld / 4);
         else
-            hipLaunchKernelGGL((mean_to_kernel<f4v, 1, 8>), dim3((unsigned)g), dim3(256), 0, st, r4, nrows, ld / 4, c4,
-                               d, d4, ndst, dst_ld / 4);
+            hipLaunchKernelGGL((mean4_kernel<1, U>), dim3((unsigned)gg), dim3(256), 0, st, r4, nrows, ld / 4, c4, d, d4,
+                               ndst, dst_ld / 4);
     } else if (order == 1) {
         hipLaunchKernelGGL((mean_to_kernel<float, 0, 1>), dim3(grid_of(count)), dim3(256), 0, st, rows, nrows, ld,
                            count, d, dst, ndst, dst_ld);
