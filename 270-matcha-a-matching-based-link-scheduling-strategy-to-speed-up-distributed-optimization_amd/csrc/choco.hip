@@ -50,9 +50,9 @@ constexpr int kMidBits = 10, kMidShift = 9;  // bits 9..18
 constexpr int kLowBits = 9;                  // bits 0..8
 constexpr int64_t kSampleTarget = 1 << 18;   // sampled elements per row (auto stride)
 
-// fine sampled floor ("fine_floor"): a window of kWinBins top digits around the last call's k-th
-// key, each split into kFineSub sub-bins (key bits 13..18), sampled beside the 12-bit histogram
-constexpr int kWinBins = 16, kFineSub = 64, kFineShift = 13;
+// fine sampled floor ("fine_floor"): a window of kWinBins top digits around the last call's floor
+// digit, each split into kFineSub sub-bins (key bits 13..18), sampled beside the 12-bit histogram
+constexpr int kWinBins = 4, kFineSub = 64, kFineShift = 13;
 constexpr int kFineBins = kWinBins * kFineSub;
 constexpr int kHistWords = 3 * kTopBins + (1 << kMidBits) + (1 << kLowBits) + kFineBins;   // hs, h12, h12f, h10, h9, hsf
 
@@ -68,6 +68,8 @@ struct SelState {
     uint32_t hint_digit, hint_ok, margin;
     uint32_t n_calls, n_fallbacks;
     uint32_t last_cand;   // the last call's candidate count (keys kept by its first compaction)
+    uint32_t win_digit;   // the last call's floor digit (fine_floor's window; b0 itself is rewritten
+                          // by the compaction while its other blocks still read the window)
 };
 static_assert(sizeof(SelState) <= 64, "SelState must fit its 64-byte slot");
 
@@ -260,12 +262,13 @@ __device__ __forceinline__ int64_t lane63(int64_t v) {
     return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
-// The fine window's first top digit: kWinBins digits from 12 below the last call's k-th key's digit
-// (the floor sits a few digits below the k-th key); -1 = no window (fine_floor off, or no call yet).
-// The sampling pass and the compaction read the same state, so they agree.
+// The fine window's first top digit: kWinBins digits from one below the last call's floor digit (the
+// floor moves by a fraction of a digit per round; a miss just leaves that round's floor a whole
+// digit); -1 = no window (fine_floor off, or no call yet).  The sampling pass and the compaction
+// read the same state, so they agree.
 __device__ __forceinline__ int fine_window(const Rows& R, const RowView& v) {
     if (!R.fine || !v.st->hint_ok) return -1;
-    const int d = (int)v.st->hint_digit - 12;
+    const int d = (int)v.st->win_digit - 1;
     return d < 0 ? 0 : d > kTopBins - kWinBins ? kTopBins - kWinBins : d;
 }
 
@@ -531,6 +534,7 @@ __device__ void record_round(const Rows& R, SelState* st, uint32_t T, unsigned l
     st->n_calls += 1;
     st->n_fallbacks += fb ? 1u : 0u;
     st->last_cand = (uint32_t)(cn < 0xffffffffull ? cn : 0xffffffffull);
+    st->win_digit = st->b0;               // this call's floor digit (written by its compaction)
 }
 
 template <bool BAL, bool LOOP, bool PF2 = false>

@@ -216,7 +216,7 @@ size_t mx_topk_work_bytes(int64_t P);
  * of the 10 and 9 low digits, threshold mark, placement), 1: as ONE launch (select_kernel: B
  * workgroups of 1024 threads per row meeting at two row barriers; measured slower);
  * "fine_floor" = 1 (default): the sampled floor refined to 1/64 of a top digit (key bits 13..18)
- * when it falls in a 16-digit window around the previous call's k-th key on the same scratch (the
+ * when it falls in a 4-digit window around the previous call's floor digit on the same scratch (the
  * sampling pass histograms that window's sub-bins too): ~1.35 k candidates instead of 1.5-4 k;
  * 0: the floor is a whole top digit;
  * "floor_hint" = -1 (default): the compaction's candidate floor from a sampled histogram (one
