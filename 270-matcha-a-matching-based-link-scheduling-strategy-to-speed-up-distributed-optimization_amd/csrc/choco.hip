@@ -123,7 +123,6 @@ struct Rows {
     int64_t bnd_off;      // int32 tile bounds at out + r*out_ld + bnd_off (< 0: not written)
     int32_t hint;         // floor_hint margin in 12-bit bins (< 0: sampled floor)
     int32_t fine;         // fine_floor: 1 = refine the sampled floor inside the window (sub-bins)
-    int32_t xcd;          // candidate passes: chunk c on a block of XCD c % 8, as in the compaction
 };
 
 struct RowView {
@@ -920,11 +919,7 @@ __global__ __launch_bounds__(kTPB) void cand_hist(Rows R, int64_t S, double frac
         }
         return q;
     };
-    // xcd: chunk c's regions are read on the XCD whose L2 holds them dirty from the compaction (chunk
-    // c ran on block c % 8 there; blocks are dealt round-robin over the 8 XCDs -- speed only): block
-    // b takes chunks 8 (kWaves (b / 8) + wave) + b % 8 (+ multiples of the stride, a multiple of 8)
-    int64_t c = R.xcd ? 8 * ((int64_t)kWaves * (blockIdx.x / 8) + wave) + blockIdx.x % 8
-                      : (int64_t)blockIdx.x * kWaves + wave;
+    int64_t c = (int64_t)blockIdx.x * kWaves + wave;
     RegionPair cur = load(c);
     const Resolved z = resolve(v, R.k, stages);
     for (int i = threadIdx.x; i < NB; i += kTPB) h[i] = 0;
@@ -1855,7 +1850,6 @@ int g_cand_chunks = 0;        // chunk regions per wave of cand_hist / cand_mark
                               // flush of cand_hist<10>'s 1024 bins measured +3.7 us on one row; same-box
                               // sweep 2 -> 4 / 8: one row 121.7 -> 119.6 us, 8 rows 655 -> 640 us)
 
-int g_xcd_align = 1;           // candidate passes read chunk c on XCD c % 8, the compaction's (grids multiples of 8)
 int g_fine_floor = 1;          // 1: the sampled floor refined to 1/64 of a top digit inside a window around
                                // the last call's k-th key, 0: the digit floor.  Same box, 3 interleaved
                                // repeats (tools/choco_hint.py, profiles/r04b_choco_fine_floor.log): 8 rows
@@ -1970,11 +1964,6 @@ extern "C" int mx_topk_set(const char* key, int64_t value) {
         g_select = (int)value;
         return MX_OK;
     }
-    if (!strcmp(key, "xcd_align")) {
-        MX_CHECK(value == 0 || value == 1, "mx_topk_set: xcd_align %lld", (long long)value);
-        g_xcd_align = (int)value;
-        return MX_OK;
-    }
     if (!strcmp(key, "fine_floor")) {
         MX_CHECK(value == 0 || value == 1, "mx_topk_set: fine_floor %lld", (long long)value);
         g_fine_floor = (int)value;
@@ -2018,7 +2007,6 @@ extern "C" int64_t mx_topk_get(const char* key) {
     if (key && !strcmp(key, "hist_grid")) return g_hist_grid;
     if (key && !strcmp(key, "floor_hint")) return g_floor_hint;
     if (key && !strcmp(key, "fine_floor")) return g_fine_floor;
-    if (key && !strcmp(key, "xcd_align")) return g_xcd_align;
     if (key && !strcmp(key, "hist_capacity")) return g_hist_capacity;
     mx::set_error("mx_topk_get: unknown key '%s'", key ? key : "(null)");
     return MX_ERR_INVALID;
@@ -2040,7 +2028,7 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
              "mx_topk_abs_diff_rows: work must be 256-byte aligned");
     hipStream_t st = mx::as_stream(stream);
     Rows R{x, x_hat, ld, static_cast<char*>(out), out_ld_bytes, idx_off_bytes, static_cast<char*>(work),
-           work_ld_bytes, P, k, bnd_off_bytes, (int32_t)g_floor_hint, (int32_t)g_fine_floor, 0};
+           work_ld_bytes, P, k, bnd_off_bytes, (int32_t)g_floor_hint, (int32_t)g_fine_floor};
     const int64_t nc = n_chunks(P);
     // S = 0: the floor comes from the previous call's k-th key (floor_hint), no sampling launch
     const int64_t S = g_floor_hint >= 0 ? 0 : sample_stride(P);
@@ -2060,13 +2048,10 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
         const int64_t q = (nc + 360) / 720 > 1 ? (nc + 360) / 720 : 1;
         bgrid = (unsigned)((nc + q - 1) / q);
     }
-    auto up8 = [](unsigned g) { return g >= 8 ? (g + 7) / 8 * 8 : g; };
-    if (g_xcd_align) bgrid = up8(bgrid);   // compaction chunk c on block c % bgrid: XCD c % 8
     const unsigned wgrid = (unsigned)((nc + kWaves - 1) / kWaves);          // one wave per chunk
     const unsigned sgrid = clamp_grid(nsamp > 0 ? nsamp : 1, (int64_t)g_sample_pieces * kWaves, (1024 + nrows - 1) / nrows);
     const int cchunks = g_cand_chunks > 0 ? g_cand_chunks : (nrows == 1 ? 4 : 8);
-    unsigned cgrid = clamp_grid(nc, (int64_t)cchunks * kWaves, (2048 + nrows - 1) / nrows);
-    if (g_xcd_align) cgrid = up8(cgrid);
+    const unsigned cgrid = clamp_grid(nc, (int64_t)cchunks * kWaves, (2048 + nrows - 1) / nrows);
 #define MX_L(kern, grid, tpb, ...)                                                 \
     hipLaunchKernelGGL(kern, grid, dim3(tpb), 0, st, R, ##__VA_ARGS__);            \
     MX_LAUNCH_CHECK()
@@ -2111,22 +2096,14 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
         const int64_t cap = hist_capacity(reinterpret_cast<const void*>(h10));
         MX_CHECK(cap >= nrows, "mx_topk_abs_diff_rows: %d rows exceed the %lld co-resident blocks of the candidate "
                  "pass (its sampled-floor fallback needs every block of a row resident)", nrows, (long long)cap);
-        if ((int64_t)hgrid * nrows > cap) {
-            hgrid = (unsigned)(cap / nrows);
-            if (g_xcd_align && hgrid >= 8) hgrid = hgrid / 8 * 8;
-        }
+        if ((int64_t)hgrid * nrows > cap) hgrid = (unsigned)(cap / nrows);
         g_hist_capacity = (unsigned)cap;
     } else {
         g_hist_capacity = 0;
     }
     g_hist_grid = hgrid;
-    Rows Rh = R, R9 = R;                      // XCD-aligned chunk mapping where the grids allow it
-    Rh.xcd = g_xcd_align && bgrid % 8 == 0 && hgrid % 8 == 0;
-    R9.xcd = g_xcd_align && bgrid % 8 == 0 && cgrid % 8 == 0;
-    hipLaunchKernelGGL(h10, dim3(hgrid, nrows), dim3(kTPB), 0, st, Rh, S, frac);
-    MX_LAUNCH_CHECK();
-    hipLaunchKernelGGL((cand_hist<kLowBits, false, false>), dim3(cgrid, nrows), dim3(kTPB), 0, st, R9, S, frac);
-    MX_LAUNCH_CHECK();
+    MX_L(h10, dim3(hgrid, nrows), kTPB, S, frac);
+    MX_L((cand_hist<kLowBits, false, false>), dim3(cgrid, nrows), kTPB, S, frac);
     const int64_t G = (nc + cgrid - 1) / cgrid;    // chunks per cand_mark block
     MX_L(cand_mark, dim3(cgrid, nrows), kTPB, G);
     MX_L(write_cand, dim3(wgrid, nrows), kTPB, G);
