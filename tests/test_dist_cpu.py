@@ -1,4 +1,4 @@
-"""Multi-rank exchange contract on CPU (gloo, world_size 2 and 4).
+"""Multi-rank exchange contract on CPU (gloo, world_size 2, 4 and 8 -- the driver's 8-GPU layout).
 
 Each rank holds a contiguous block of the 8 workers of graph 0.  Per round it posts, in the
 order mx_exchange_plan (the native enumeration mx_exchange_round feeds to RCCL) returns, a
@@ -96,7 +96,7 @@ def _worker(rank, world, port, q):
         q.put((rank, traceback.format_exc()))
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_exchange_contract_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()

@@ -42,12 +42,13 @@ def test_multiprocess_rounds_match_oracle(nproc):
     assert res["world"] == nproc and all(v for k, v in res.items() if k != "world"), res
 
 
-@pytest.mark.parametrize("nproc", [2, 4])
+@pytest.mark.parametrize("nproc", [2, 4, 8])
 def test_bench_multiprocess_path(nproc):
     """bench.py's N > 1 branch (partition, exchange, barriers, max-over-ranks timing, xgmi object)
     end to end on one GPU, with EVERY figure at reduced size: the headline, MATCHA 0.5, Choco (VGG
     config 4), the WRN / ResNet configs 2-3 and the ER(64) budget sweep (config 5) -- each one's
-    oracle self-check must pass (configs 3-5 self-checking at N > 1)."""
+    oracle self-check must pass (configs 3-5 self-checking at N > 1).  nproc 8 is the
+    driver's 8-GPU layout (one worker per rank; ER(64): 8 workers per rank) on one GPU."""
     r = _torchrun(nproc, ["bench.py", "--gpus", str(nproc), "--transport", "gloo", "--steps", "3", "--warmup", "1",
                           "--params", "200000", "--choco-params", "300000", "--cpu-seconds", "0",
                           "--wrn-params", "70000", "--resnet-params", "30000", "--er-params", "20000",
