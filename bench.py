@@ -619,15 +619,20 @@ class _NullComm:
 def choco_row_share(pkg, GP, P, ratio, gamma, K, W):
     """Config 4's per-GPU work at N = 8 measured on this GPU: rank 0's single row (placement
     "auto") with a null transport -- top-k, then the apply pass over its own and its partners'
-    messages (copies of its own as stand-ins).  What every GPU adds to the message exchange in a
-    real 8-GPU Choco round; per-round HIP events."""
+    messages.  The partners' messages are stand-ins: the top-k messages of other synthetic rows
+    (distinct index sets, so the apply dirties as many s granules as real partner messages do;
+    until round 3 they were copies of the row's own message, which collide in the same granules).
+    What every GPU adds to the message exchange in a real 8-GPU Choco round; per-round HIP events."""
     c = pkg.ChocoWorkerGroup(GP, numel=P, ratio=ratio, consensus_lr=gamma, rank=0, nranks=8,
                              comm=_NullComm(0, 8), placement="auto")
-    pkg._lib.check(pkg.lib.mx_synth_fill(c.rows[0].data_ptr(), P, 1234 + c.workers[0], None))
-    c.compress(0)
-    torch.cuda.synchronize()
-    for s in range(c.n_local, c.engine.n_slots):
+    for s in range(c.n_local, c.engine.n_slots):            # a distinct synthetic row per partner slot
+        pkg._lib.check(pkg.lib.mx_synth_fill(c.rows[0].data_ptr(), P, 7000 + s, None))
+        c.compress(0)
+        torch.cuda.synchronize()
         c.msgs[s * c.msg_ld:(s + 1) * c.msg_ld].copy_(c.msgs[:c.msg_ld])
+    pkg._lib.check(pkg.lib.mx_synth_fill(c.rows[0].data_ptr(), P, 1234 + c.workers[0], None))
+    c.work.zero_()                                          # a fresh top-k scratch for the row itself
+    torch.cuda.synchronize()
     for it in range(W):
         c.step(it)
     torch.cuda.synchronize()
@@ -641,7 +646,8 @@ def choco_row_share(pkg, GP, P, ratio, gamma, K, W):
     out = {"rows": 1, "partners": int(c.engine.n_slots - c.n_local), "round_us_median": float(np.median(us)),
            "round_us_min": float(us.min()), "rounds": K,
            "hbm_GBps_alg": 24 * P / (np.median(us) * 1e-6) / 1e9,
-           "how": "rank 0's row of an 8-GPU layout, null transport, per-round HIP events"}
+           "how": "rank 0's row of an 8-GPU layout, null transport, partner messages = top-k of other synthetic "
+                  "rows, per-round HIP events"}
     del c
     torch.cuda.empty_cache()
     return out

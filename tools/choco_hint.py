@@ -46,15 +46,16 @@ def make(kind):
         return c
     c = pkg.ChocoWorkerGroup(GP, numel=P, ratio=0.99, consensus_lr=0.1, rank=0, nranks=8, comm=NullComm(0, 8),
                              placement="auto")
-    pkg._lib.check(L.mx_synth_fill(c.rows[0].data_ptr(), P, 1234 + c.workers[0], None))
     saved = (int(L.mx_topk_get(b"floor_hint")), int(L.mx_topk_get(b"fine_floor")))
     knobs("s")
-    c.compress(0)                               # stand-in partner messages (then a fresh scratch)
+    for s in range(c.n_local, c.engine.n_slots):      # partner stand-ins: top-k of other synthetic rows
+        pkg._lib.check(L.mx_synth_fill(c.rows[0].data_ptr(), P, 7000 + s, None))
+        c.compress(0)
+        torch.cuda.synchronize()
+        c.msgs[s * c.msg_ld:(s + 1) * c.msg_ld].copy_(c.msgs[:c.msg_ld])
     L.mx_topk_set(b"floor_hint", saved[0])
     L.mx_topk_set(b"fine_floor", saved[1])
-    torch.cuda.synchronize()
-    for s in range(c.n_local, c.engine.n_slots):
-        c.msgs[s * c.msg_ld:(s + 1) * c.msg_ld].copy_(c.msgs[:c.msg_ld])
+    pkg._lib.check(L.mx_synth_fill(c.rows[0].data_ptr(), P, 1234 + c.workers[0], None))
     c.work.zero_()
     return c
 

@@ -65,11 +65,13 @@ for i in range(n):
 groups["rows8"] = c8
 c1 = pkg.ChocoWorkerGroup(GP, numel=P, ratio=0.99, consensus_lr=0.1, rank=0, nranks=8, comm=NullComm(0, 8),
                           placement="auto")
-pkg._lib.check(pkg.lib.mx_synth_fill(c1.rows[0].data_ptr(), P, 1234 + c1.workers[0], None))
-c1.compress(0)
-torch.cuda.synchronize()
-for s in range(c1.n_local, c1.engine.n_slots):
+for s in range(c1.n_local, c1.engine.n_slots):      # partner stand-ins: top-k of other synthetic rows
+    pkg._lib.check(pkg.lib.mx_synth_fill(c1.rows[0].data_ptr(), P, 7000 + s, None))
+    c1.compress(0)
+    torch.cuda.synchronize()
     c1.msgs[s * c1.msg_ld:(s + 1) * c1.msg_ld].copy_(c1.msgs[:c1.msg_ld])
+pkg._lib.check(pkg.lib.mx_synth_fill(c1.rows[0].data_ptr(), P, 1234 + c1.workers[0], None))
+c1.work.zero_()
 groups["row1"] = c1
 
 res = {(g, v): [] for g in groups for v in VARIANTS}

@@ -22,11 +22,13 @@ if os.environ.get("CHOCO_GROUP", "row1") == "rows8":
 else:
     c = pkg.ChocoWorkerGroup(GP, numel=P, ratio=0.99, consensus_lr=0.1, rank=0, nranks=8, comm=NullComm(0, 8),
                              placement="auto")
-    pkg._lib.check(pkg.lib.mx_synth_fill(c.rows[0].data_ptr(), P, 1234 + c.workers[0], None))
-    c.compress(0)
-    torch.cuda.synchronize()
-    for s in range(c.n_local, c.engine.n_slots):
+    for s in range(c.n_local, c.engine.n_slots):      # partner stand-ins: top-k of other synthetic rows
+        pkg._lib.check(pkg.lib.mx_synth_fill(c.rows[0].data_ptr(), P, 7000 + s, None))
+        c.compress(0)
+        torch.cuda.synchronize()
         c.msgs[s * c.msg_ld:(s + 1) * c.msg_ld].copy_(c.msgs[:c.msg_ld])
+    pkg._lib.check(pkg.lib.mx_synth_fill(c.rows[0].data_ptr(), P, 1234 + c.workers[0], None))
+    c.work.zero_()
 for kv in filter(None, os.environ.get("TOPK_SET", "").split(":")):     # e.g. TOPK_SET=select=1:select_blocks=32
     k_, v_ = kv.split("=")
     pkg._lib.check(pkg.lib.mx_topk_set(k_.encode(), int(v_)))
