@@ -2113,22 +2113,38 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
 
 // The rows' sticky error words (a bounded row-barrier wait that expired: the sampled-floor fallback
 // in cand_hist<10>, or select_kernel): synchronises `stream`, reads and clears them.
+namespace {
+// one lane: the first row whose error word is set (or -1), and every set word cleared
+__global__ void err_scan_kernel(char* work, int64_t work_ld, int nrows, int64_t off, int32_t* out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    int32_t bad = -1;
+    for (int r = 0; r < nrows; ++r) {
+        uint32_t* e = reinterpret_cast<uint32_t*>(work + (int64_t)r * work_ld + off);
+        if (*e) {
+            if (bad < 0) bad = r;
+            *e = 0u;
+        }
+    }
+    *out = bad;
+}
+}  // namespace
+
 extern "C" int mx_topk_check(void* work, int64_t work_ld_bytes, int nrows, int64_t P, void* stream) {
     MX_CHECK(work && nrows >= 1 && P >= 1 && (nrows == 1 || work_ld_bytes >= (int64_t)layout(P).total),
              "mx_topk_check: bad arguments");
+    static int32_t* dev_out[64] = {nullptr};     // one word per device, allocated once
+    int dev = 0;
+    MX_HIP(hipGetDevice(&dev));
+    MX_CHECK(dev >= 0 && dev < 64, "mx_topk_check: device %d", dev);
+    if (!dev_out[dev]) MX_HIP(hipMalloc(&dev_out[dev], sizeof(int32_t)));
     hipStream_t st = mx::as_stream(stream);
+    const int64_t off = (int64_t)(layout(P).state + offsetof(SelState, err));
+    hipLaunchKernelGGL(err_scan_kernel, dim3(1), dim3(64), 0, st, static_cast<char*>(work), work_ld_bytes, nrows, off,
+                       dev_out[dev]);
+    MX_LAUNCH_CHECK();
+    int32_t bad = -1;
+    MX_HIP(hipMemcpyAsync(&bad, dev_out[dev], sizeof(bad), hipMemcpyDeviceToHost, st));
     MX_HIP(hipStreamSynchronize(st));
-    const size_t off = layout(P).state + offsetof(SelState, err);
-    int bad = -1;
-    for (int r = 0; r < nrows; ++r) {
-        char* p = static_cast<char*>(work) + (int64_t)r * work_ld_bytes + off;
-        uint32_t e = 0;
-        MX_HIP(hipMemcpy(&e, p, sizeof(e), hipMemcpyDeviceToHost));
-        if (e) {
-            if (bad < 0) bad = r;
-            MX_HIP(hipMemset(p, 0, sizeof(e)));
-        }
-    }
     if (bad >= 0) {
         mx::set_error("mx_topk: a row barrier's bounded wait expired (row %d): not every block of the row was "
                       "resident; that call's output is undefined", bad);
