@@ -38,6 +38,8 @@
 // caller zero-fills the scratch once; every call leaves it that way), so no zeroing launch runs.
 #include "mx_common.h"
 
+#include <mutex>
+
 namespace {
 constexpr int kTPB = 256;
 constexpr int kWaves = kTPB / 64;
@@ -1889,6 +1891,8 @@ int64_t hist_capacity(const void* fn) {
     struct Entry { int dev; const void* fn; int64_t cap; };
     static Entry cache[32];
     static int used = 0;
+    static std::mutex mu;                    // host threads may launch on several devices at once
+    std::lock_guard<std::mutex> lock(mu);
     int dev = 0;
     (void)hipGetDevice(&dev);
     for (int i = 0; i < used; ++i)
@@ -2133,10 +2137,14 @@ extern "C" int mx_topk_check(void* work, int64_t work_ld_bytes, int nrows, int64
     MX_CHECK(work && nrows >= 1 && P >= 1 && (nrows == 1 || work_ld_bytes >= (int64_t)layout(P).total),
              "mx_topk_check: bad arguments");
     static int32_t* dev_out[64] = {nullptr};     // one word per device, allocated once
+    static std::mutex mu;
     int dev = 0;
     MX_HIP(hipGetDevice(&dev));
     MX_CHECK(dev >= 0 && dev < 64, "mx_topk_check: device %d", dev);
-    if (!dev_out[dev]) MX_HIP(hipMalloc(&dev_out[dev], sizeof(int32_t)));
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        if (!dev_out[dev]) MX_HIP(hipMalloc(&dev_out[dev], sizeof(int32_t)));
+    }
     hipStream_t st = mx::as_stream(stream);
     const int64_t off = (int64_t)(layout(P).state + offsetof(SelState, err));
     hipLaunchKernelGGL(err_scan_kernel, dim3(1), dim3(64), 0, st, static_cast<char*>(work), work_ld_bytes, nrows, off,
