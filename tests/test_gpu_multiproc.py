@@ -64,6 +64,8 @@ def test_bench_multiprocess_path(nproc):
     assert ov["calib_ms_unchunked"] > 0 and ov["calib_ms_chunked"] > 0
     assert out["choco"]["rounds_per_s"] > 0 and out["cpu_baseline"] is None
     assert out["allreduce_baseline"]["rounds_per_s"] > 0
+    assert out["allreduce_baseline"]["parity_ok"] is True          # all-gather + mx_mean_rows_to, tree order
+    assert out["choco"]["topk"]["calls_per_row"] > 0
     # every self-check is the oracle's (checker) on the same inputs
     assert out["parity_ok"] is True and "oracle" in out["parity"]
     assert out["choco"]["parity_ok"] is True
@@ -214,3 +216,6 @@ def test_bench_single_gpu_line():
     assert all(v["rounds_per_s"] > 0 and v["hbm_TBps"] > 0 for v in cfg.values())
     cb = out["cpu_baseline"]
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["pickle"]["value"] > 0 and cb["pickle"]["cores"] >= 1
+    ar = out["allreduce_baseline"]
+    assert ar["parity_ok"] is True and 0 < ar["roofline"]["frac"] < 1 and out["rccl_ranks"] is None
+    assert out["choco"]["topk"]["fallback_compactions"] >= 0 and out["choco"]["topk"]["floor"] == "fine sampled"
