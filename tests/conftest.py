@@ -119,3 +119,20 @@ class LoopbackComm:
 
     def allreduce_mean(self, flat, size):
         raise NotImplementedError("loopback transport: all-reduce is not emulated")
+
+
+def special_values(P, seed, n_nan=5, n_inf=4):
+    """A float32 row with non-finite and edge values planted at random positions: quiet NaNs of
+    both signs and two payloads, +-Inf, +-0, denormals, +-FLT_MAX; the rest standard normal (no
+    two finite magnitudes equal, so a top-k boundary among them is unambiguous)."""
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal(P).astype(np.float32)
+    pos = rng.permutation(P)
+    nan = np.array([0x7FC00000, 0xFFC00000, 0x7FC00123, 0xFFC00001], np.uint32).view(np.float32)
+    j = 0
+    for v in [nan[i % 4] for i in range(n_nan)] + [np.float32(np.inf), np.float32(-np.inf)] * (n_inf // 2) + \
+             [np.float32(0.0), np.float32(-0.0), np.float32(1e-42), np.float32(-3e-41),
+              np.float32(3.4028235e38), np.float32(-3.4028235e38)]:
+        x[pos[j]] = v
+        j += 1
+    return x
