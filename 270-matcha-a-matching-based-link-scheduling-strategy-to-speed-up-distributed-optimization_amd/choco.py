@@ -108,9 +108,7 @@ class ChocoWorkerGroup:
         """averaging (communicator.py:200-230): receive partner messages ([N > 1] over the
         transport into the message slots after the local ones), then the s / x_hat scatters and
         the dense x update."""
-        it = int(it)
-        if not 0 <= it < self.engine.T:          # mx_choco_apply indexes the plan table by `it`
-            raise IndexError(f"iteration {it} outside the schedule's {self.engine.T} rows")
+        it = self.engine.round_index(it)         # mx_choco_apply indexes the plan table by `it`
         mbase = self.msgs.data_ptr()
         if self.engine.comm is not None:
             self.engine.exchange(it, [mbase + r * self.msg_ld for r in range(self.n_local)],

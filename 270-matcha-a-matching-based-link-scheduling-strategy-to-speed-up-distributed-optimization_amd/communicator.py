@@ -73,11 +73,14 @@ class _Staging:
 
     GPU models are adopted: every parameter's storage is a view of the group row, so a round
     mixes them in place and nothing is copied.  Host models (the reference's default) are staged:
-    copied to the row before and back after each round."""
+    copied to the row before and back after each round.  adopt=False (a plain tensor list, e.g.
+    the reference's `tensor_list` of `param.data` aliases, which cannot be re-homed): GPU tensors
+    already at their place in the row are used in place, others are copied in and back out."""
 
-    def __init__(self, params, row):
+    def __init__(self, params, row, adopt=True):
         self.params = params
         self.row = row
+        self.may_adopt = adopt
         self.on_gpu = all(p.device.type == "cuda" for p in params)
 
     def adopted(self):
@@ -139,7 +142,10 @@ class _Staging:
             if not self.adopted():
                 self.on_gpu = all(p.device.type == "cuda" for p in self.params)
                 if self.on_gpu:
-                    self.adopt()
+                    if self.may_adopt:
+                        self.adopt()
+                    else:
+                        self._copy_in()
             if self.on_gpu:
                 return
         # host model: flatten (comm_helpers.py:27-30's torch.cat) into a pinned staging buffer piece
@@ -152,8 +158,23 @@ class _Staging:
                 pin[d:d + hi - lo].copy_(src)
             self.row[a:b].copy_(pin[a:b], non_blocking=True)
 
+    def _copy_in(self):
+        off = 0
+        with torch.no_grad():
+            for p in self.params:
+                k = p.numel()
+                self.row[off:off + k].view(p.shape).copy_(p.data)
+                off += k
+
     def store(self):
         if self.on_gpu:
+            if not self.may_adopt and not self.adopted():
+                off = 0
+                with torch.no_grad():
+                    for p in self.params:
+                        k = p.numel()
+                        p.data.copy_(self.row[off:off + k].view(p.shape))
+                        off += k
             return
         # every piece's DMA back is queued at once; piece i is scattered into the parameters while
         # the later pieces are still in flight
@@ -266,6 +287,8 @@ class decenCommunicator(Communicator):
             pass
 
     def communicate(self, model):
+        """communicator.py:133-158: the three steps below fused, with the model's parameters
+        adopted into the arena row on the first call (no flatten / unflatten afterwards)."""
         active_flags = self.topology.active_flags[self.iter]
         it = self.iter
         self.iter += 1
@@ -281,6 +304,57 @@ class decenCommunicator(Communicator):
         toc = time.time()
         self._stage.store()
         return toc - tic
+
+    # ---- the reference's sub-steps (communicator.py:87-131), for callers that drive them directly
+    def _bind_list(self, tensors, make_group):
+        n = int(sum(t.numel() for t in tensors))
+        if self._group is None or self._group.numel != n:
+            self.close()
+            self._group = make_group(n)
+            self._model_params = None
+            self._stage = None
+        self._list_stage = _Staging(tensors, self._group.rows[0], adopt=False)
+        self._list_stage.load()
+        return self._group.rows[0]
+
+    def _round_of(self, active_flags):
+        """The plan record of `active_flags`: the schedule's row of the current iteration when they
+        are that row (the reference's communicate() passes exactly it), else a scratch record."""
+        eng = self._group.engine
+        f = np.asarray(active_flags)
+        i = self.iter - 1
+        if 0 <= i < eng.T and f.shape == eng.flags_host[i].shape and np.array_equal(f != 0, eng.flags_host[i] != 0):
+            return i
+        return eng.adhoc(f)
+
+    def prepare_comm_buffer(self):
+        """communicator.py:87-90.  `self.tensor_list` (set by the caller, as the reference's
+        communicate() does) is copied into this rank's arena row -- or used in place when it
+        already lives there (parameters adopted by an earlier communicate(model)) -- and
+        `send_buffer` is that row (flat, on the GPU).  The reference's zero `recv_buffer` has no
+        counterpart: the kernel accumulates in registers and writes the row in place, so after
+        averaging() `recv_buffer` names the same row."""
+        self.send_buffer = self._bind_list(list(self.tensor_list), lambda n: VirtualWorkerGroup(
+            self.topology, None, numel=n, rank=self.rank, nranks=self.size, comm=self._comm(),
+            idle_rows=self.idle_rows))
+        self.recv_buffer = None
+
+    def averaging(self, active_flags):
+        """communicator.py:92-122: one gossip round of send_buffer under `active_flags` (any row;
+        every rank passes the same one, as the reference's sendrecv pairs require); seconds."""
+        it = self._round_of(active_flags)
+        torch.cuda.synchronize()
+        tic = time.time()
+        self._group.step(it)
+        wait_round(self._group.engine.comm)
+        toc = time.time()
+        self.recv_buffer = self.send_buffer
+        return toc - tic
+
+    def reset_model(self):
+        """communicator.py:124-131: the averaged row back into tensor_list (nothing to do for
+        tensors that live in the row)."""
+        self._list_stage.store()
 
 
 class ChocoCommunicator(Communicator):
@@ -327,6 +401,8 @@ class ChocoCommunicator(Communicator):
         self.initialized = True
 
     def communicate(self, model):
+        """communicator.py:242-268: the three steps below fused (compression + averaging timed
+        together: the reference's encode_time + comm_time), parameters adopted into the arena."""
         active_flags = self.topology.active_flags[self.iter]
         it = self.iter
         self.iter += 1
@@ -340,8 +416,55 @@ class ChocoCommunicator(Communicator):
         self._group.step(it)
         wait_round(self._group.engine.comm)
         toc = time.time()
+        self._group.check_topk()
         self._stage.store()
         return toc - tic
+
+    # ---- the reference's sub-steps (communicator.py:175-240), for callers that drive them directly
+    _bind_list = decenCommunicator._bind_list
+    _round_of = decenCommunicator._round_of
+
+    def prepare_comm_buffer(self):
+        """communicator.py:175-196: `self.tensor_list` into this rank's x row (copied, or used in
+        place when it lives there), x_hat / s created zero on first use (they persist), then the
+        top-k of x - x_hat; `compressed` = {"values", "indices"} views of the message (GPU,
+        index-sorted).  Returns the compression seconds (the reference's encode time)."""
+        tensors = list(self.tensor_list)
+        n = int(sum(t.numel() for t in tensors))
+        if self._group is not None and self._group.numel != n:
+            raise ValueError(f"ChocoCommunicator: tensor_list holds {n} values, its x_hat / s hold {self._group.numel}")
+        self.x = self._bind_list(tensors, lambda n: ChocoWorkerGroup(
+            self.topology, None, numel=n, ratio=self.ratio, consensus_lr=self.consensus_lr, rank=self.rank,
+            nranks=self.size, comm=self._comm()))
+        self.initialized = True
+        torch.cuda.synchronize()
+        tic = time.time()
+        self._group.compress(self.iter)
+        self._group.check_topk()
+        toc = time.time()
+        vals, idx = self._group.message(0)
+        self.compressed = {"values": vals, "indices": idx}
+        return toc - tic
+
+    def averaging(self, active_flags):
+        """communicator.py:200-230: partner messages under `active_flags` (any row; every rank the
+        same), s / x_hat scatters and x += consensus_lr (s - x_hat), in place; seconds."""
+        it = self._round_of(active_flags)
+        torch.cuda.synchronize()
+        tic = time.time()
+        self._group.average(it)
+        wait_round(self._group.engine.comm)
+        toc = time.time()
+        return toc - tic
+
+    def reset_model(self):
+        """communicator.py:233-240: x back into tensor_list (nothing to do for tensors in the row)."""
+        self._list_stage.store()
+
+    def close(self):
+        self._group = None
+        self._stage = None
+        self._model_params = None
 
 
 ORDERS = {"tree": 0, "sequential": 1}
@@ -395,17 +518,34 @@ class centralizedCommunicator(Communicator):
             check(lib.mx_allreduce_mean_ordered(comm.handle, flat.data_ptr(), count, gather.data_ptr(),
                                                 ORDERS[self.order], stream_ptr()), "mx_allreduce_mean_ordered")
 
-    def communicate(self, model):
-        tensors = [p.data for p in model.parameters()]
+    def prepare_comm_buffer(self):
+        """communicator.py:52-54: `send_buffer` = the flattened tensor_list (on the GPU)."""
+        tensors = list(self.tensor_list)
         on_gpu = all(t.device.type == "cuda" for t in tensors)
-        flat = flatten_tensors([t if on_gpu else t.cuda() for t in tensors])
+        self.send_buffer = flatten_tensors([t if on_gpu else t.cuda() for t in tensors])
+
+    def averaging(self):
+        """communicator.py:56-67: the all-reduce mean of send_buffer, in place (recv_buffer names
+        it); seconds."""
         torch.cuda.synchronize()
         tic = time.time()
-        if self.size > 1 and flat.numel():
-            self._average(flat)
+        if self.size > 1 and self.send_buffer.numel():
+            self._average(self.send_buffer)
         wait_round(self._comm())
         toc = time.time()
-        with torch.no_grad():
-            for f, t in zip(unflatten_tensors(flat, tensors), tensors):
-                t.copy_(f)
+        self.recv_buffer = self.send_buffer
         return toc - tic
+
+    def reset_model(self):
+        """communicator.py:69-76: the averaged vector back into tensor_list."""
+        with torch.no_grad():
+            for f, t in zip(unflatten_tensors(self.recv_buffer, self.tensor_list), self.tensor_list):
+                t.copy_(f)
+
+    def communicate(self, model):
+        """communicator.py:18-33 (the base class's sequence)."""
+        self.tensor_list = [p.data for p in model.parameters()]
+        self.prepare_comm_buffer()
+        comm_time = self.averaging()
+        self.reset_model()
+        return comm_time

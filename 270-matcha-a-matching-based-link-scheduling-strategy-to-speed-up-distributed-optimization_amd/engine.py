@@ -352,15 +352,52 @@ class GossipEngine:
                           "the 156 a mixing tile holds in LDS: spread the workers over more GPUs")
         self.plan_words = int(lib.mx_plan_words(self.n_local, self.M))
         self.partner_dev = torch.from_numpy(self.partner).to("cuda")
-        self.plan = torch.empty(max(1, self.T) * self.plan_words, dtype=torch.int32, device="cuda")
+        # the schedule's T records + one scratch record (index T) for a round of arbitrary flags (adhoc)
+        self.plan = torch.empty((self.T + 1) * self.plan_words, dtype=torch.int32, device="cuda")
         check(lib.mx_plan_build(self.flags_dev.data_ptr(), self.T, self.M, self.partner_dev.data_ptr(),
                                 self.n, None, self.rank, self.row_base, self.n_local, self.alpha,
                                 self.plan.data_ptr(), stream_ptr()), "mx_plan_build")
         if IDLE_MODES[idle_rows]:
             check(lib.mx_plan_set_idle(self.plan.data_ptr(), self.T, self.n_local, self.M, IDLE_MODES[idle_rows],
                                        stream_ptr()), "mx_plan_set_idle")
+        self.flags_host = np.vstack([self.flags_host, np.zeros((1, self.M), np.uint8)])
         self.any_active = self.flags_host.any(axis=1).tolist()
         self._plan_ptr = self.plan.data_ptr()
+        self.peer_reads = False                  # set by a pull-transport group: applied to adhoc records too
+        self._adhoc_ready = False
+        self._adhoc_flags = None
+
+    def adhoc(self, active_flags):
+        """A round for an arbitrary flags row -- the reference's averaging(active_flags) takes any
+        row, not only the schedule's (communicator.py:92-122, 200-230): its plan record is built
+        into the scratch record after the schedule's T rows (stream-ordered, on the current
+        stream) and its index, T, returned; valid until the next adhoc() call.  Collective like the
+        reference's sendrecv: with N > 1 every rank passes the same row."""
+        f = np.asarray(active_flags)
+        if f.ndim != 1 or f.shape[0] != self.M:
+            raise ValueError(f"active_flags must hold one entry per matching ({self.M}), got shape {f.shape}")
+        f = np.ascontiguousarray((f != 0).astype(np.uint8))
+        self.flags_host[self.T] = f
+        self.any_active[self.T] = bool(f.any())
+        self._adhoc_flags = torch.from_numpy(f.copy()).to("cuda")
+        rec = self._plan_ptr + 4 * self.T * self.plan_words
+        check(lib.mx_plan_build(self._adhoc_flags.data_ptr(), 1, self.M, self.partner_dev.data_ptr(), self.n, None,
+                                self.rank, self.row_base, self.n_local, self.alpha, rec, stream_ptr()),
+              "mx_plan_build")
+        if IDLE_MODES[self.idle_rows]:
+            check(lib.mx_plan_set_idle(rec, 1, self.n_local, self.M, IDLE_MODES[self.idle_rows], stream_ptr()),
+                  "mx_plan_set_idle")
+        if self.peer_reads:
+            check(lib.mx_plan_set_peer_reads(rec, 1, self.n_local, self.M, 1, stream_ptr()), "mx_plan_set_peer_reads")
+        self._adhoc_ready = True
+        return self.T
+
+    def round_index(self, it):
+        """`it` checked against the plan table: a schedule row, or T after adhoc()."""
+        it = int(it)
+        if not (0 <= it < self.T or (it == self.T and self._adhoc_ready)):
+            raise IndexError(f"iteration {it} outside the schedule's {self.T} rows")
+        return it
 
     # ------------------------------------------------------------------ per round
     def exchange_plan(self, it):
@@ -396,9 +433,7 @@ class GossipEngine:
         return nrem.value
 
     def mix(self, it, layout, stream=None):
-        it = int(it)
-        if not 0 <= it < self.T:                 # the kernel indexes the plan table by `it`
-            raise IndexError(f"iteration {it} outside the schedule's {self.T} rows")
+        it = self.round_index(it)                # the kernel indexes the plan table by `it`
         if layout.tune_gen != _TUNE_GEN[0]:
             if layout.tile != lib.mx_mix_tile(layout.n_slots):
                 raise MXError("layout built for another mixing tile size (the unroll knob changed it)")
@@ -536,8 +571,9 @@ class VirtualWorkerGroup:
             # receive slots point at the peers' snapshot rows, set per round (_step_pull); no slab
             self._pull = comm.bind(self)
             # receive slots will be peers' memory: the mixing kernels acquire at system scope first
-            check(lib.mx_plan_set_peer_reads(self.engine.plan.data_ptr(), self.engine.T, self.n_local,
+            check(lib.mx_plan_set_peer_reads(self.engine.plan.data_ptr(), self.engine.T + 1, self.n_local,
                                              self.engine.M, 1, stream_ptr()), "mx_plan_set_peer_reads")
+            self.engine.peer_reads = True
             self._pull_table = np.zeros((1, self.engine.n_slots), np.int64)
             self._pull_table[0, :self.n_local] = self._row_ptrs
             self._pull_table[0, self.n_local:] = self._pull.own

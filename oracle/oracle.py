@@ -51,6 +51,8 @@ def lib():
                                       _u8p, ctypes.c_int, ctypes.c_double, ctypes.c_int64,
                                       ctypes.c_double]
         L.orc_choco_round.restype = ctypes.c_int
+        L.orc_choco_averaging.argtypes = L.orc_choco_round.argtypes
+        L.orc_choco_averaging.restype = ctypes.c_int
         L.orc_baseline_rounds.argtypes = [ctypes.POINTER(ctypes.c_void_p), _i64p, ctypes.c_int,
                                           ctypes.c_int, _i32p, _u8p, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_double, _f32p, ctypes.c_int]
@@ -122,15 +124,17 @@ def topk_abs(x, k, sort=False):
     return vals, idx
 
 
-def choco_round(X, XH, S, partner, flags, alpha, k, gamma):
-    """ChocoCommunicator round for all workers (communicator.py:175-268); state in place."""
+def choco_round(X, XH, S, partner, flags, alpha, k, gamma, skip_empty=True):
+    """ChocoCommunicator round for all workers (communicator.py:175-268); state in place.
+    skip_empty=False: prepare_comm_buffer + averaging(flags) called directly -- a row with no
+    active matching still applies every worker's own message (communicator.py:175-230)."""
     n, P = X.shape
     for a in (X, XH, S):
         assert a.dtype == np.float32 and a.flags.c_contiguous
     partner = np.ascontiguousarray(partner, dtype=np.int32)
     flags = np.ascontiguousarray(flags, dtype=np.uint8)
-    rc = lib().orc_choco_round(X, XH, S, n, P, partner, flags, partner.shape[0], float(alpha),
-                               int(k), float(gamma))
+    f = lib().orc_choco_round if skip_empty else lib().orc_choco_averaging
+    rc = f(X, XH, S, n, P, partner, flags, partner.shape[0], float(alpha), int(k), float(gamma))
     assert rc == 0, rc
 
 
