@@ -12,6 +12,7 @@ import subprocess
 import sys
 
 import pytest
+import torch
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -190,6 +191,20 @@ def test_rccl_init_deadline():
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["rc"] == -3 and out["handle_null"] and "never joined" in out["message"], out
     assert 3.5 <= out["seconds"] < 60, out
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (one RCCL rank each)")
+def test_rccl_peer_skips_exchange():
+    """Two ranks on two GPUs: after a first all-gather connected them, rank 1 skips the second.
+    Rank 0's bounded wait (RcclComm.wait -> mx_rccl_wait) raises MXError within ~3 s and aborts
+    the communicator instead of hanging.  Skipped on a one-GPU box: RCCL
+    refuses two ranks on one device."""
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr=127.0.0.1", f"--master-port={_port()}", os.path.join(HERE, "rccl_skip.py")],
+                       cwd=ROOT, capture_output=True, text=True, timeout=120)
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["first_ok"] and out["aborted"] and "did not drain" in (out["error"] or ""), out
+    assert 2.5 <= out["seconds"] < 30, out
 
 
 def test_bench_single_gpu_line():
