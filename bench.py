@@ -507,7 +507,7 @@ def allreduce_figure(pkg, args, rank, world, n, P, K, W, comm, dev, arena=None):
     if world == 1:
         alg = 2 * n * P * 4
         kern_ms = ev[0].elapsed_time(ev[1]) / K
-        out["roofline"] = {"bound": "hbm", "kernel": "mean_to_kernel (mx_mean_rows_to)", "bytes_per_launch": alg,
+        out["roofline"] = {"bound": "hbm", "kernel": "mean4_kernel<1, 4> (mx_mean_rows_to: 16-byte path, tree order)", "bytes_per_launch": alg,
                            "avg_launch_ms": kern_ms, "achieved": alg / (kern_ms * 1e-3) / 1e9,
                            "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": alg / (kern_ms * 1e-3) / HBM_PEAK,
                            "note": "algorithmic bytes 2 x n x P x 4 (every row read once, the mean written to "
