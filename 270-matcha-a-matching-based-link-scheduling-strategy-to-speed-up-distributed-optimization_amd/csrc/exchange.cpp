@@ -333,57 +333,11 @@ __global__ void div_kernel(float* __restrict__ x, int64_t n, float d) {
 //             stack[l] + carry while bit l of the count is set) and a right-to-left fold of the
 //             stack at the end -- ((x0 + x1) + (x2 + x3)) + ((x4 + x5) + x6) for 7 rows, exactly
 //             the mask loop's order (checked against it for 1..300 rows in tests/reforder.py).
-template <int TREE, int MAXR>
-__global__ __launch_bounds__(256) void mean_rows_kernel(const float* rows, int nrows, int64_t ld,
-                                                        int64_t count, float size, float* out) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x) {
-        float acc;
-        if (TREE == 2) {
-            constexpr int L = 24;                         // up to 2^24 rows
-            float stack[L];
-#pragma unroll
-            for (int l = 0; l < L; ++l) stack[l] = 0.0f;
-            for (int r = 0; r < nrows; ++r) {
-                float p = rows[(int64_t)r * ld + i];
-                bool carry = true;
-#pragma unroll
-                for (int l = 0; l < L; ++l) {
-                    const bool set = (r >> l) & 1;
-                    if (carry && set) p = stack[l] + p;
-                    else if (carry) { stack[l] = p; carry = false; }
-                }
-            }
-            bool have = false;
-            acc = 0.0f;
-#pragma unroll
-            for (int l = 0; l < L; ++l)
-                if ((nrows >> l) & 1) {
-                    acc = have ? stack[l] + acc : stack[l];
-                    have = true;
-                }
-        } else if (TREE) {
-            float v[MAXR];
-#pragma unroll
-            for (int r = 0; r < MAXR; ++r) v[r] = r < nrows ? rows[(int64_t)r * ld + i] : 0.0f;
-#pragma unroll
-            for (int m = 1; m < MAXR; m <<= 1)
-#pragma unroll
-                for (int r = 0; r + m < MAXR; r += 2 * m)
-                    if (r + m < nrows) v[r] = v[r] + v[r + m];
-            acc = v[0];
-        } else {
-            acc = rows[i];
-            for (int r = 1; r < nrows; ++r) acc = acc + rows[(int64_t)r * ld + i];
-        }
-        out[i] = acc / size;
-    }
-}
-
-// mean_rows_kernel with the mean written to ndst destination rows (dst + d * dst_ld) instead of
-// one: the all-reduce of centralizedCommunicator for workers held as rows of one arena (every
-// worker's row becomes the mean) in ONE pass -- each lane reads a column of every row, then writes
-// that column of every destination row, so dst == rows (in place) is safe.  Scalar form (any row
-// count, order, alignment); the 16-byte form is mean4_kernel below.
+// The mean written to ndst destination rows (dst + d * dst_ld; mx_mean_rows: one): the all-reduce
+// of centralizedCommunicator for workers held as rows of one arena (every worker's row becomes the
+// mean) in ONE pass -- each lane reads a column of every row, then writes that column of every
+// destination row, so dst == rows (in place) is safe.  Scalar form (any row count, order,
+// alignment); the 16-byte forms are mean4_kernel and mean_tile_kernel below.
 typedef float f4v __attribute__((ext_vector_type(4)));
 
 template <typename V, int TREE, int MAXR>
@@ -391,7 +345,7 @@ __global__ __launch_bounds__(256) void mean_to_kernel(const V* rows, int nrows, 
                                                       float size, V* dst, int ndst, int64_t dst_ld) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x) {
         V acc;
-        if (TREE == 2) {                          // binary counter of partial sums (see mean_rows_kernel)
+        if (TREE == 2) {                          // binary counter of partial sums (above)
             constexpr int L = 24;
             V stack[L];
 #pragma unroll
@@ -482,6 +436,49 @@ __global__ __launch_bounds__(256) void mean4_kernel(const f4v* rows, int nrows, 
     }
 }
 
+// The mixing kernel's tile geometry for up to 8 rows: one workgroup per 512-column tile (128
+// 4-float vectors).  The rows' 2 KB pieces are staged in LDS with 16-byte loads (each wave load is
+// 1 KB of one row), then every lane sums its column in the same order as mean4_kernel<TREE> (the
+// same adds, the same division: identical bits) and stores every other destination row.
+template <int TREE>
+__global__ __launch_bounds__(256) void mean_tile_kernel(const f4v* rows, int nrows, int64_t ld, float size,
+                                                        f4v* dst, int ndst, int64_t dst_ld) {
+    constexpr int C4 = 128;
+    __shared__ f4v lds[8 * C4];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t c0 = (int64_t)blockIdx.x * C4;
+    f4v R[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int e = wave * 64 + 256 * j;                 // wave-uniform row e / C4
+        R[j] = e / C4 < nrows ? __builtin_nontemporal_load(rows + (int64_t)(e / C4) * ld + c0 + e % C4 + lane)
+                              : f4v(0.0f);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) lds[wave * 64 + 256 * j + lane] = R[j];
+    __syncthreads();
+    const int c = tid % C4, h = tid / C4;
+    f4v v[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = lds[r * C4 + c];
+    f4v acc;
+    if (TREE) {
+#pragma unroll
+        for (int m = 1; m < 8; m <<= 1)
+#pragma unroll
+            for (int r = 0; r + m < 8; r += 2 * m)
+                if (r + m < nrows) v[r] = v[r] + v[r + m];
+        acc = v[0];
+    } else {
+        acc = v[0];
+#pragma unroll
+        for (int r = 1; r < 8; ++r)
+            if (r < nrows) acc = acc + v[r];
+    }
+    const f4v m = acc / size;
+    for (int d = h; d < ndst; d += 2) __builtin_nontemporal_store(m, dst + (int64_t)d * dst_ld + c0 + c);
+}
+
 inline unsigned grid_of(int64_t count) {
     int64_t g = (count + 255) / 256;
     return (unsigned)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
@@ -499,29 +496,16 @@ extern "C" int mx_allreduce_mean(void* comm_v, float* buf, int64_t count, int nr
     return MX_OK;
 }
 
+extern "C" int mx_mean_rows_to(const float* rows, int nrows, int64_t ld, int64_t count, int order, float* dst,
+                               int ndst, int64_t dst_ld, void* stream);
+
+// One destination row: the same kernels as mx_mean_rows_to (identical summation order and bits).
 extern "C" int mx_mean_rows(const float* rows, int nrows, int64_t ld, int64_t count, int order, float* out,
                             void* stream) {
     MX_CHECK(rows && out && nrows >= 1 && nrows <= (1 << 24) && ld >= count && count >= 0,
              "mx_mean_rows: nrows=%d (1..2^24) ld=%lld count=%lld", nrows, (long long)ld, (long long)count);
     MX_CHECK(order == 0 || order == 1, "mx_mean_rows: order %d (0 tree, 1 rank order)", order);
-    if (count == 0) return MX_OK;
-    hipStream_t st = mx::as_stream(stream);
-    const float d = (float)nrows;
-    if (order == 1) {
-        hipLaunchKernelGGL((mean_rows_kernel<0, 1>), dim3(grid_of(count)), dim3(256), 0, st, rows, nrows, ld, count, d,
-                           out);
-    } else if (nrows <= 8) {
-        hipLaunchKernelGGL((mean_rows_kernel<1, 8>), dim3(grid_of(count)), dim3(256), 0, st, rows, nrows, ld, count, d,
-                           out);
-    } else if (nrows <= 64) {
-        hipLaunchKernelGGL((mean_rows_kernel<1, 64>), dim3(grid_of(count)), dim3(256), 0, st, rows, nrows, ld, count, d,
-                           out);
-    } else {
-        hipLaunchKernelGGL((mean_rows_kernel<2, 1>), dim3(grid_of(count)), dim3(256), 0, st, rows, nrows, ld, count, d,
-                           out);
-    }
-    MX_LAUNCH_CHECK();
-    return MX_OK;
+    return mx_mean_rows_to(rows, nrows, ld, count, order, out, 1, count, stream);
 }
 
 extern "C" int mx_mean_rows_to(const float* rows, int nrows, int64_t ld, int64_t count, int order, float* dst,
@@ -555,14 +539,32 @@ extern "C" int mx_mean_rows_to(const float* rows, int nrows, int64_t ld, int64_t
         // 8 x 25.6M in place = 0.72 of 8 TB/s, against 0.322 ms for a 4096-block persistent grid
         // with one vector per lane per step, 0.287 with two, 0.31 with two on CUs x 8 blocks
         // (tools/mean_ab.py, profiles/r04b_mean_rows_geometry.log)
+        // up to 8 rows: whole 512-column tiles through LDS (mean_tile_kernel: 0.2768 vs 0.2838 ms
+        // for 8 x 25.6M in place, 0.74 vs 0.72 of 8 TB/s, 3 interleaved repeats,
+        // profiles/r04ac_mean_tile_ab.log); the remaining vectors (< 128) as before
+        int64_t done4 = 0;
+        if (nrows <= 8 && c4 >= 128) {
+            const int64_t nt = c4 / 128;
+            if (order == 1)
+                hipLaunchKernelGGL((mean_tile_kernel<0>), dim3((unsigned)nt), dim3(256), 0, st, r4, nrows, ld / 4, d, d4,
+                                   ndst, dst_ld / 4);
+            else
+                hipLaunchKernelGGL((mean_tile_kernel<1>), dim3((unsigned)nt), dim3(256), 0, st, r4, nrows, ld / 4, d, d4,
+                                   ndst, dst_ld / 4);
+            MX_LAUNCH_CHECK();
+            done4 = nt * 128;
+        }
+        if (done4 < c4) {
         constexpr int U = 4;
-        const int64_t gg = (c4 + U * 256 - 1) / (U * 256);
+        const int64_t rest = c4 - done4;
+        const int64_t gg = (rest + U * 256 - 1) / (U * 256);
         if (order == 1)
-            hipLaunchKernelGGL((mean4_kernel<0, U>), dim3((unsigned)gg), dim3(256), 0, st, r4, nrows, ld / 4, c4, d, d4,
-                               ndst, dst_ld / 4);
+            hipLaunchKernelGGL((mean4_kernel<0, U>), dim3((unsigned)gg), dim3(256), 0, st, r4 + done4, nrows, ld / 4, rest, d,
+                               d4 + done4, ndst, dst_ld / 4);
         else
-            hipLaunchKernelGGL((mean4_kernel<1, U>), dim3((unsigned)gg), dim3(256), 0, st, r4, nrows, ld / 4, c4, d, d4,
-                               ndst, dst_ld / 4);
+            hipLaunchKernelGGL((mean4_kernel<1, U>), dim3((unsigned)gg), dim3(256), 0, st, r4 + done4, nrows, ld / 4, rest, d,
+                               d4 + done4, ndst, dst_ld / 4);
+        }
     } else if (order == 1) {
         hipLaunchKernelGGL((mean_to_kernel<float, 0, 1>), dim3(grid_of(count)), dim3(256), 0, st, rows, nrows, ld,
                            count, d, dst, ndst, dst_ld);
