@@ -36,6 +36,8 @@ WARM = 5
 n = 8
 GP = pkg.MatchaProcessor(pkg.select_graph(0), 1.0, 0, n, ROUNDS + WARM + 2, True)
 L = pkg.lib
+if os.environ.get("COMPACT_BLOCKS"):                 # compaction grid (0 = auto)
+    pkg._lib.check(L.mx_topk_set(b"compact_blocks", int(os.environ["COMPACT_BLOCKS"])))
 
 
 def make(kind):
