@@ -372,14 +372,15 @@ int mx_allgather(void* comm, const float* send, int64_t count, float* gather, vo
  * are nrows x ld floats (device), 1 <= nrows <= 2^24 (the tree order for any count: a binary counter
  * of partial sums); out may be rows[0].  The division step of
  * the centralized communicator (communicator.py:61-62) and of sync_allreduce (train_mpi.py:46-55),
- * callable after any transport's gather. */
+ * callable after any transport's gather.  = mx_mean_rows_to with ndst = 1. */
 int mx_mean_rows(const float* rows, int nrows, int64_t ld, int64_t count, int order, float* out, void* stream);
 /* The same mean (same order, same rounding) written to ndst rows dst + d * dst_ld (d < ndst) in one
  * pass: centralizedCommunicator's all-reduce (communicator.py:56-67) / sync_allreduce (train_mpi.py:
  * 34-56) for workers held as rows of one arena -- dst == rows (dst_ld == ld) rewrites every worker's
  * row with the mean in place (each column of every row is read before that column is written);
  * after an mx_allgather, dst = this rank's own rows.  16-byte accesses when everything is 16-byte
- * aligned and the order is the <= 8-row tree or rank order. */
+ * aligned and the order is the <= 8-row tree or rank order; up to 8 rows in 512-column tiles
+ * staged in LDS. */
 int mx_mean_rows_to(const float* rows, int nrows, int64_t ld, int64_t count, int order, float* dst, int ndst,
                     int64_t dst_ld, void* stream);
 

@@ -21,7 +21,7 @@ def mpi4py_sum(rows, order):
 
 def binary_counter_sum(rows):
     """The binomial tree as mx_mean_rows computes it above 64 rows: a binary counter of partial
-    sums, folded right to left at the end (exchange.cpp, mean_rows_kernel TREE = 2)."""
+    sums, folded right to left at the end (exchange.cpp, mean_to_kernel TREE = 2)."""
     stack, c = {}, 0
     for r in rows:
         p, lvl = r.copy(), 0

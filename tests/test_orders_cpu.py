@@ -2,7 +2,7 @@
 
 mx_mean_rows runs mpi4py's binomial-tree order (communicator.py:61, comm.allreduce under
 rc.fast_reduce) over a register array up to 64 rows and as a binary counter of partial sums above
-(exchange.cpp mean_rows_kernel TREE = 2).  The two statements must be the same order: checked
+(exchange.cpp mean_to_kernel TREE = 2).  The two statements must be the same order: checked
 here bit for bit on fp32 rows of mixed magnitudes for every row count 1..300.  (The mpi4py order
 itself is restated from its published algorithm -- mpi4py is not installed: parity unpinned
 against mpi4py.)"""
