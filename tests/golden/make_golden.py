@@ -17,6 +17,8 @@ Fixtures (all small):
   decen.npz           decenCommunicator.communicate (communicator.py:79-158) over several rounds
   choco.npz           ChocoCommunicator.communicate (communicator.py:161-268) over several rounds
   topk.npz/json       compressors.get_top_k (compressors.py:3-19): k table + index sets
+  topk_special.npz/json  get_top_k on rows with NaN / +-Inf / +-0 / denormals / +-FLT_MAX
+                      (inputs stored with the index sets; `python tests/golden/make_golden.py topk_special`)
 """
 import contextlib
 import io
@@ -302,6 +304,41 @@ def gen_topk(ns):
     with open(os.path.join(HERE, "topk.json"), "w") as f:
         json.dump(ktab, f)
     print("topk", len(ktab), "k-table rows")
+
+
+def special(P, seed, n_nan=5, n_inf=4):
+    """A float32 row with quiet NaNs of both signs and two payloads, +-Inf, +-0, denormals and
+    +-FLT_MAX planted at random positions; the rest standard normal."""
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal(P).astype(np.float32)
+    pos = rng.permutation(P)
+    nan = np.array([0x7FC00000, 0xFFC00000, 0x7FC00123, 0xFFC00001], np.uint32).view(np.float32)
+    vals = [nan[i % 4] for i in range(n_nan)] + [np.float32(np.inf), np.float32(-np.inf)] * (n_inf // 2) + \
+        [np.float32(0.0), np.float32(-0.0), np.float32(1e-42), np.float32(-3e-41), np.float32(3.4028235e38),
+         np.float32(-3.4028235e38)]
+    for j, v in enumerate(vals):
+        x[pos[j]] = v
+    return x
+
+
+def gen_topk_special(ns):
+    """topk_special.npz/json: compressors.get_top_k on rows with non-finite and edge values (the
+    inputs are stored with the index sets); k = 1 goes through the reference's torch.max branch."""
+    gtk = ns.compressors.get_top_k
+    arrs, meta = {}, []
+    for P, ratio, seed, n_nan, n_inf in ((20_000, 0.99, 1, 5, 4), (4_099, 0.99, 2, 5, 4), (100_003, 0.99, 3, 5, 4),
+                                         (30_000, 1 - 12.5 / 30_000, 5, 6, 6), (50_000, 1 - 1.5 / 50_000, 4, 1, 2)):
+        x = special(P, seed, n_nan, n_inf)
+        v, idx = gtk(torch.from_numpy(x.copy()), ratio)
+        o = torch.argsort(idx)
+        c = len(meta)
+        arrs[f"case{c}_x"] = x
+        arrs[f"case{c}_idx"] = idx.reshape(-1)[o.reshape(-1)].numpy().astype(np.int64)
+        meta.append({"P": P, "ratio": ratio, "k": int(idx.numel()), "nan": n_nan, "inf": n_inf})
+    np.savez_compressed(os.path.join(HERE, "topk_special.npz"), **arrs)
+    with open(os.path.join(HERE, "topk_special.json"), "w") as f:
+        json.dump(meta, f)
+    print("topk_special", len(meta), "cases")
 
 
 if __name__ == "__main__":

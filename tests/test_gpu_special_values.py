@@ -92,3 +92,15 @@ def test_choco_special_values_vs_oracle(pkg, O):
         assert _same(grp.x_hat[:, :P].cpu().numpy(), XH), f"x_hat, round {t}"
         assert _same(grp.s[:, :P].cpu().numpy(), S), f"s, round {t}"
     assert np.isnan(X).any()
+
+
+def test_get_top_k_special_values_vs_reference_fixture(pkg):
+    """get_top_k (the product path, compressors.py's API) on the reference's own special-value
+    cases (tests/golden/topk_special.npz): the same index sets, values x[idx] bit for bit."""
+    from conftest import golden_json, golden_npz
+    g = golden_npz("topk_special")
+    for c, m in enumerate(golden_json("topk_special")):
+        x = g[f"case{c}_x"]
+        v, i = pkg.get_top_k(torch.from_numpy(x).cuda(), m["ratio"])
+        assert np.array_equal(i.cpu().numpy(), g[f"case{c}_idx"]), m
+        assert np.array_equal(v.cpu().numpy().view(np.uint32), x[g[f"case{c}_idx"]].view(np.uint32)), m

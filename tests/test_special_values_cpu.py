@@ -42,3 +42,15 @@ def test_oracle_topk_all_nonfinite_prefix_vs_torch(O):
     _, idx = O.topk_abs(x, 12)
     assert np.array_equal(idx, _ref_indices(x, 12))
     assert not np.isfinite(x[idx]).any()
+
+
+def test_oracle_topk_special_values_vs_reference_fixture(O):
+    """The reference's own get_top_k (tests/golden/topk_special.npz, make_golden.py topk_special),
+    incl. its torch.max branch at k = 1: the oracle's index sets equal it."""
+    from conftest import golden_json, golden_npz
+    g = golden_npz("topk_special")
+    for c, m in enumerate(golden_json("topk_special")):
+        x = g[f"case{c}_x"]
+        assert O.topk_k(m["P"], m["ratio"]) == m["k"]
+        _, idx = O.topk_abs(x, m["k"])
+        assert np.array_equal(idx, g[f"case{c}_idx"]), m
