@@ -330,6 +330,15 @@ class GossipEngine:
         if self.M > partner_all.shape[0]:
             raise IndexError(f"active_flags has {self.M} columns but only {partner_all.shape[0]} "
                              "matchings exist (neighbors_info[graph_id] would fail)")
+        if self.M < partner_all.shape[0]:
+            # FixedProcessor's table has two columns (graph_manager.py:208-225) while the
+            # reference's averaging(active_flags) walks whatever row it is given over
+            # neighbors_info: the table is padded with zero columns, so a round over every
+            # matching (adhoc) is expressible; schedule rounds are unchanged
+            pad = partner_all.shape[0] - self.M
+            self.flags_host = np.hstack([self.flags_host, np.zeros((self.T, pad), np.uint8)])
+            self.flags_dev = torch.from_numpy(np.ascontiguousarray(self.flags_host)).to("cuda")
+            self.M = partner_all.shape[0]
         self.partner = np.ascontiguousarray(partner_all[:self.M])
         validate_partner(self.partner)
         self.alpha = float(topology.neighbor_weight)

@@ -17,6 +17,8 @@ Fixtures (all small):
   decen.npz           decenCommunicator.communicate (communicator.py:79-158) over several rounds
   choco.npz           ChocoCommunicator.communicate (communicator.py:161-268) over several rounds
   topk.npz/json       compressors.get_top_k (compressors.py:3-19): k table + index sets
+  substeps.npz/json   decen / Choco prepare_comm_buffer + averaging(flags) + reset_model driven
+                      directly, flags rows given per call (incl. all-zero)
   topk_special.npz/json  get_top_k on rows with NaN / +-Inf / +-0 / denormals / +-FLT_MAX
                       (inputs stored with the index sets; `python tests/golden/make_golden.py topk_special`)
 """
@@ -304,6 +306,57 @@ def gen_topk(ns):
     with open(os.path.join(HERE, "topk.json"), "w") as f:
         json.dump(ktab, f)
     print("topk", len(ktab), "k-table rows")
+
+
+SUBSTEP_FLAGS = [[1, 0, 1, 0, 1], [0, 0, 0, 0, 0], [1, 1, 1, 1, 1], [0, 1, 1, 0, 0]]
+
+
+def gen_substeps(ns):
+    """substeps.npz/json: the communicators' sub-steps driven directly -- tensor_list set,
+    prepare_comm_buffer(), averaging(active_flags), reset_model() (communicator.py:87-131, 175-240)
+    -- on flags rows given per call, incl. an all-zero row (which communicate() would skip)."""
+    gm, cm = ns.graph_manager, ns.communicator
+    arrs, meta = {}, []
+    size, shapes = 8, [(23, 7), (9,)]
+    P = numel(shapes)
+    base = ns.util.select_graph(0)
+    GP = quiet(gm.FixedProcessor, base, 0.5, 0, size, 10, True)
+    M = len(GP.neighbors_info)
+    F = [r[:M] for r in SUBSTEP_FLAGS]
+    for kind in ("decen", "choco"):
+        X0 = np.stack([synth((77 if kind == "decen" else 88) + r, P) for r in range(size)])
+        H.new_world(size)
+        models = [Params(shapes, X0[r]) for r in range(size)]
+        if kind == "decen":
+            comms = [cm.decenCommunicator(r, size, GP) for r in range(size)]
+        else:
+            comms = [cm.ChocoCommunicator(r, size, GP, 0.9, 0.3) for r in range(size)]
+
+        def body(r):
+            outs = []
+            for f in F:
+                comms[r].tensor_list = [p.data for p in models[r].parameters()]
+                comms[r].prepare_comm_buffer()
+                comms[r].averaging(f)
+                comms[r].reset_model()
+                outs.append(flat_of(models[r]))
+            extra = (comms[r].x_hat.numpy().copy(), comms[r].s.numpy().copy()) if kind == "choco" else ()
+            return (np.stack(outs),) + extra
+
+        res = H.run_ranks(size, body)
+        arrs[f"{kind}_X0"] = X0
+        arrs[f"{kind}_Y"] = np.stack([r[0] for r in res], axis=1)      # [R][n][P]
+        if kind == "choco":
+            arrs["choco_xhat"] = np.stack([r[1] for r in res])
+            arrs["choco_s"] = np.stack([r[2] for r in res])
+        print("substeps", kind, "P =", P, "rounds =", len(F))
+    arrs["flags"] = np.asarray(F, dtype=np.uint8)
+    arrs["partner"] = np.asarray(GP.neighbors_info, dtype=np.int32)
+    meta = {"size": size, "shapes": [list(x) for x in shapes], "P": P, "alpha": float(GP.neighbor_weight),
+            "ratio": 0.9, "consensus_lr": 0.3, "k": max(1, int(P * (1 - 0.9)))}
+    np.savez_compressed(os.path.join(HERE, "substeps.npz"), **arrs)
+    with open(os.path.join(HERE, "substeps.json"), "w") as f:
+        json.dump(meta, f)
 
 
 def special(P, seed, n_nan=5, n_inf=4):

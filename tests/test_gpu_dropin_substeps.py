@@ -142,3 +142,50 @@ def test_choco_substeps_tensor_list(pkg, O):
         for r in range(n):
             assert np.array_equal(comms[r].x_hat.cpu().numpy().view(np.uint32), XH[r].view(np.uint32))
             assert np.array_equal(comms[r].s.cpu().numpy().view(np.uint32), S[r].view(np.uint32))
+
+
+@pytest.mark.parametrize("kind", ["decen", "choco"])
+def test_substeps_vs_reference_fixture(pkg, kind):
+    """The reference's own sub-step run (tests/golden/substeps.npz: tensor_list, prepare_comm_buffer,
+    averaging(flags), reset_model per given flags row, incl. an all-zero row) replayed through the
+    drop-in communicators with the reference's CPU models (staged to the GPU and back), 8 ranks
+    over the loopback transport: every round's parameters, and Choco's final x_hat / s, bit-exact."""
+    from conftest import golden_json, golden_npz
+    g, m = golden_npz("substeps"), golden_json("substeps")
+    n, shapes = m["size"], [tuple(s) for s in m["shapes"]]
+    np.random.seed(1234)
+    GP = pkg.FixedProcessor(pkg.select_graph(0), 0.5, 0, n, 10, True)
+    assert np.array_equal(np.asarray(GP.neighbors_info, np.int32), g["partner"])
+    X0 = g[f"{kind}_X0"]
+    models = []
+    for r in range(n):
+        ps, off = [], 0
+        for s in shapes:
+            k = int(np.prod(s))
+            ps.append(torch.nn.Parameter(torch.from_numpy(X0[r, off:off + k].copy()).view(*s)))
+            off += k
+        mod = torch.nn.Module()
+        mod.ps = torch.nn.ParameterList(ps)
+        models.append(mod)
+    hub = LoopbackHub(n)
+    if kind == "decen":
+        comms = [pkg.decenCommunicator(r, n, GP, transport=hub.comm(r)) for r in range(n)]
+    else:
+        comms = [pkg.ChocoCommunicator(r, n, GP, m["ratio"], m["consensus_lr"], transport=hub.comm(r))
+                 for r in range(n)]
+    for t, f in enumerate(g["flags"]):
+        for r in range(n):
+            comms[r].tensor_list = [p.data for p in models[r].parameters()]
+            comms[r].prepare_comm_buffer()
+            hub.register(r, [comms[r]._group.rows[0].data_ptr() if kind == "decen" else comms[r]._group.msgs.data_ptr()])
+        hub.snap.clear()
+        for r in range(n):
+            comms[r].averaging(f)
+            comms[r].reset_model()
+        got = _flat(models)
+        assert np.array_equal(got.view(np.uint32), g[f"{kind}_Y"][t].view(np.uint32)), t
+    if kind == "choco":
+        xh = np.stack([c.x_hat.cpu().numpy() for c in comms])
+        s = np.stack([c.s.cpu().numpy() for c in comms])
+        assert np.array_equal(xh.view(np.uint32), g["choco_xhat"].view(np.uint32))
+        assert np.array_equal(s.view(np.uint32), g["choco_s"].view(np.uint32))

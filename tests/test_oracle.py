@@ -133,3 +133,25 @@ def test_topk_select_equals_sort(O, P, k, pattern):
     v2, i2 = O.topk_abs(x, k, sort=True)
     assert np.array_equal(i1, i2)
     assert np.array_equal(v1.view(np.uint32), v2.view(np.uint32))
+
+
+def test_substeps_vs_reference(O):
+    """The reference's sub-steps driven directly (tests/golden/substeps.npz): decenCommunicator and
+    ChocoCommunicator prepare_comm_buffer + averaging(flags) + reset_model on given flags rows,
+    incl. an all-zero row -- which the reference's averaging still applies (Choco: every worker's
+    own message) though communicate() would skip it.  The oracle (decen_round; choco_round with
+    skip_empty=False) reproduces every round bit for bit."""
+    g, m = golden_npz("substeps"), golden_json("substeps")
+    partner, flags = g["partner"], g["flags"]
+    X = g["decen_X0"].copy()
+    for t, f in enumerate(flags):
+        if f.any():
+            X = O.decen_round(X, partner, f, m["alpha"])
+        assert np.array_equal(X.view(np.uint32), g["decen_Y"][t].view(np.uint32)), t
+    X = np.ascontiguousarray(g["choco_X0"].copy())
+    XH, S = np.zeros_like(X), np.zeros_like(X)
+    for t, f in enumerate(flags):
+        O.choco_round(X, XH, S, partner, f, m["alpha"], m["k"], m["consensus_lr"], skip_empty=False)
+        assert np.array_equal(X.view(np.uint32), g["choco_Y"][t].view(np.uint32)), t
+    assert np.array_equal(XH.view(np.uint32), g["choco_xhat"].view(np.uint32))
+    assert np.array_equal(S.view(np.uint32), g["choco_s"].view(np.uint32))
