@@ -1,6 +1,7 @@
 """mx_mean_rows_to (the centralized all-reduce over 8 arena rows x 25.6M fp32, in place) per-launch
-time under the geometry variant of MX_MEAN_VARIANT (read once per process: run one process per
-variant); prints the HBM fraction (2 x 8 x P x 4 bytes per launch) and a checksum of the result."""
+time of the library it loads (MX_GOSSIP_LIB selects another build for an A/B; the geometry
+experiments it timed are in profiles/r04b_mean_rows_geometry.log, r04w_*, r04ac_*); prints the HBM
+fraction (2 x 8 x P x 4 bytes per launch) and a checksum of the result."""
 import importlib
 import json
 import os
@@ -32,5 +33,5 @@ for _ in range(K):
 b.record()
 torch.cuda.synchronize()
 ms = a.elapsed_time(b) / K
-print(json.dumps({"variant": os.environ.get("MX_MEAN_VARIANT", "0"), "ms": round(ms, 4),
+print(json.dumps({"lib": os.environ.get("MX_GOSSIP_LIB") or "tree", "ms": round(ms, 4),
                   "frac_8TBps": round(2 * n * P * 4 / (ms * 1e-3) / 8e12, 4), "checksum": chk}), flush=True)
