@@ -321,9 +321,9 @@ class decenCommunicator(Communicator):
         """The plan record of `active_flags`: the schedule's row of the current iteration when they
         are that row (the reference's communicate() passes exactly it), else a scratch record."""
         eng = self._group.engine
-        f = np.asarray(active_flags)
+        f = eng.flags_row(active_flags)
         i = self.iter - 1
-        if 0 <= i < eng.T and f.shape == eng.flags_host[i].shape and np.array_equal(f != 0, eng.flags_host[i] != 0):
+        if 0 <= i < eng.T and np.array_equal(f, eng.flags_host[i]):
             return i
         return eng.adhoc(f)
 

@@ -382,10 +382,7 @@ class GossipEngine:
         into the scratch record after the schedule's T rows (stream-ordered, on the current
         stream) and its index, T, returned; valid until the next adhoc() call.  Collective like the
         reference's sendrecv: with N > 1 every rank passes the same row."""
-        f = np.asarray(active_flags)
-        if f.ndim != 1 or f.shape[0] != self.M:
-            raise ValueError(f"active_flags must hold one entry per matching ({self.M}), got shape {f.shape}")
-        f = np.ascontiguousarray((f != 0).astype(np.uint8))
+        f = self.flags_row(active_flags)
         self.flags_host[self.T] = f
         self.any_active[self.T] = bool(f.any())
         self._adhoc_flags = torch.from_numpy(f.copy()).to("cuda")
@@ -400,6 +397,17 @@ class GossipEngine:
             check(lib.mx_plan_set_peer_reads(rec, 1, self.n_local, self.M, 1, stream_ptr()), "mx_plan_set_peer_reads")
         self._adhoc_ready = True
         return self.T
+
+    def flags_row(self, active_flags):
+        """A flags row as the engine's uint8[M]: a shorter row (FixedProcessor's two columns) names
+        the first matchings only, like the reference's enumerate(active_flags) walk; a longer one
+        names matchings that do not exist (neighbors_info[graph_id] would fail there too)."""
+        f = np.asarray(active_flags)
+        if f.ndim != 1 or f.shape[0] > self.M:
+            raise IndexError(f"active_flags must hold at most one entry per matching ({self.M}), got shape {f.shape}")
+        row = np.zeros(self.M, np.uint8)
+        row[:f.shape[0]] = f != 0
+        return row
 
     def round_index(self, it):
         """`it` checked against the plan table: a schedule row, or T after adhoc()."""

@@ -189,3 +189,32 @@ def test_substeps_vs_reference_fixture(pkg, kind):
         s = np.stack([c.s.cpu().numpy() for c in comms])
         assert np.array_equal(xh.view(np.uint32), g["choco_xhat"].view(np.uint32))
         assert np.array_equal(s.view(np.uint32), g["choco_s"].view(np.uint32))
+
+
+def test_decen_substeps_fixed_schedule_rows(pkg, O):
+    """FixedProcessor's rows have two entries (graph_manager.py:208-225): averaging() takes them as
+    the reference does (matchings 0 and 1), from the schedule and as given rows alike."""
+    n = 8
+    np.random.seed(7)
+    GP = pkg.FixedProcessor(pkg.select_graph(0), 0.5, 0, n, 6, True)
+    assert len(GP.active_flags[0]) == 2 and len(GP.neighbors_info) > 2
+    models = _models(n, "cuda", 6)
+    X = _flat(models)
+    hub = LoopbackHub(n)
+    comms = [pkg.decenCommunicator(r, n, GP, transport=hub.comm(r)) for r in range(n)]
+    partner = np.asarray(GP.neighbors_info, np.int32)
+    for t in range(4):
+        f = list(GP.active_flags[t]) if t % 2 == 0 else [1, 1]
+        for r in range(n):
+            comms[r].iter = t + 1
+            comms[r].tensor_list = [p.data for p in models[r].parameters()]
+            comms[r].prepare_comm_buffer()
+            hub.register(r, [comms[r]._group.rows[0].data_ptr()])
+        hub.snap.clear()
+        for r in range(n):
+            comms[r].averaging(f)
+            comms[r].reset_model()
+        full = np.zeros(len(partner), np.uint8)
+        full[:2] = f
+        X = O.decen_round(X, partner, full, GP.neighbor_weight)
+        assert np.array_equal(_flat(models).view(np.uint32), X.view(np.uint32)), t
