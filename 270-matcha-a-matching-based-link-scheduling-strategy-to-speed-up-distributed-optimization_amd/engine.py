@@ -278,6 +278,18 @@ def topology_flags(topology):
     return torch.from_numpy(np.ascontiguousarray(host)).to("cuda"), host
 
 
+def flags_row(active_flags, M):
+    """A flags row as uint8[M]: a shorter row (FixedProcessor's two columns) names the first
+    matchings only, like the reference's enumerate(active_flags) walk (communicator.py:99-110); a
+    longer one names matchings that do not exist (neighbors_info[graph_id] would fail there too)."""
+    f = np.asarray(active_flags)
+    if f.ndim != 1 or f.shape[0] > M:
+        raise IndexError(f"active_flags must hold at most one entry per matching ({M}), got shape {f.shape}")
+    row = np.zeros(M, np.uint8)
+    row[:f.shape[0]] = f != 0
+    return row
+
+
 class Layout:
     """Pointer table of the mixing kernel: slot k's copy of segment s (include/matcha_gossip.h)."""
 
@@ -399,15 +411,7 @@ class GossipEngine:
         return self.T
 
     def flags_row(self, active_flags):
-        """A flags row as the engine's uint8[M]: a shorter row (FixedProcessor's two columns) names
-        the first matchings only, like the reference's enumerate(active_flags) walk; a longer one
-        names matchings that do not exist (neighbors_info[graph_id] would fail there too)."""
-        f = np.asarray(active_flags)
-        if f.ndim != 1 or f.shape[0] > self.M:
-            raise IndexError(f"active_flags must hold at most one entry per matching ({self.M}), got shape {f.shape}")
-        row = np.zeros(self.M, np.uint8)
-        row[:f.shape[0]] = f != 0
-        return row
+        return flags_row(active_flags, self.M)
 
     def round_index(self, it):
         """`it` checked against the plan table: a schedule row, or T after adhoc()."""

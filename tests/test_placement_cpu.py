@@ -145,3 +145,18 @@ def test_placement_argument_validation(pkg):
         pkg.placement.resolve(topo, 2, "random")
     assert pkg.placement.block_workers([3, 1, 0, 2], 1, 2) == [1, 0]
     assert pkg.placement.block_workers(None, 4, 2) == [4, 5]
+
+
+def test_flags_row_reference_walk(pkg):
+    """engine.flags_row: the row averaging(active_flags) walks (communicator.py:99-110) as one entry
+    per matching -- a shorter row (FixedProcessor's [0, 1] / [1, 0], graph_manager.py:208-225) names
+    the first matchings, non-zero entries count as active, a longer row is refused like the
+    reference's neighbors_info[graph_id] lookup would fail."""
+    fr = pkg.engine.flags_row
+    assert fr([0, 1], 5).tolist() == [0, 1, 0, 0, 0]
+    assert fr(np.array([2, 0, -1], np.int64), 3).tolist() == [1, 0, 1]
+    assert fr([], 4).tolist() == [0, 0, 0, 0]
+    with pytest.raises(IndexError):
+        fr([1] * 6, 5)
+    with pytest.raises(IndexError):
+        fr([[1, 0]], 5)
