@@ -248,7 +248,7 @@ def pmc_traffic(kernel_prefix="mix_kernel"):
     """HBM bytes per launch of the mixing kernel from the newest committed rocprofv3 PMC summary
     (tools/profile_round.sh -> profiles/rocprof_<round>.json; FETCH_SIZE x2 + WRITE_SIZE)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "rocprof_*.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "rocprof_r[0-9]*.json")))   # headline summaries only
     if not files:
         return None, None
     with open(files[-1]) as f:
