@@ -63,6 +63,11 @@ SIGNATURES = {
     "mx_allgather": (c_int, [c_p, c_p, c_i64, c_p, c_p]),
     "mx_mean_rows": (c_int, [c_p, c_int, c_i64, c_i64, c_int, c_p, c_p]),
     "mx_mean_rows_to": (c_int, [c_p, c_int, c_i64, c_i64, c_int, c_p, c_int, c_i64, c_p]),
+    "mx_mean_kernel_name": (ctypes.c_char_p, [c_int, c_i64, c_int]),
+    "mx_pull_gate": (c_int, [c_p, c_p, c_int, c_p, c_int, c_p, c_p, c_int, c_int, c_int, c_int, c_i64, c_int, c_u64,
+                             c_p, c_int, c_f64, c_p, c_p]),
+    "mx_host_words": (c_int, [c_int, c_p, c_p]),
+    "mx_host_words_free": (c_int, [c_p]),
     "mx_synth_fill": (c_int, [c_p, c_i64, c_u64, c_p]),
     "mx_max_weight_matching": (c_int, [c_int, c_p, c_p, c_p, c_int, c_p, c_p, c_p]),
     "mx_snapshot_publish": (c_int, [c_p, c_p, c_i64, c_p]),
@@ -73,6 +78,9 @@ SIGNATURES = {
     "mx_ipc_close": (c_int, [c_p]),
     "mx_ipc_free": (c_int, [c_p]),
 }
+
+
+MX_OK, MX_ERR_INVALID, MX_ERR_HIP, MX_ERR_RCCL, MX_ERR_RNG, MX_ERR_UNSUPPORTED = 0, -1, -2, -3, -4, -5
 
 
 class MXError(RuntimeError):

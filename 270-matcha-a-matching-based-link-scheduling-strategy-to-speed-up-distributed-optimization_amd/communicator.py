@@ -300,7 +300,7 @@ class decenCommunicator(Communicator):
         torch.cuda.synchronize()
         tic = time.time()
         self._group.step(it)
-        wait_round(self._group.engine.comm)
+        self._group.wait_round()
         toc = time.time()
         self._stage.store()
         return toc - tic
@@ -346,7 +346,7 @@ class decenCommunicator(Communicator):
         torch.cuda.synchronize()
         tic = time.time()
         self._group.step(it)
-        wait_round(self._group.engine.comm)
+        self._group.wait_round()
         toc = time.time()
         self.recv_buffer = self.send_buffer
         return toc - tic
@@ -414,7 +414,7 @@ class ChocoCommunicator(Communicator):
         torch.cuda.synchronize()
         tic = time.time()
         self._group.step(it)
-        wait_round(self._group.engine.comm)
+        self._group.wait_round()
         toc = time.time()
         self._group.check_topk()
         self._stage.store()

@@ -150,6 +150,8 @@ extern "C" int mx_rccl_count(void* comm, int* nranks_out) {
 // (hipEventQuery) until it completes or timeout_ms passes; on expiry the communicator is aborted
 // (ncclCommAbort: its kernels see the abort flag and exit, the stream drains) and MX_ERR_RCCL
 // "timed out" is returned -- the caller must not use the communicator again.
+static constexpr int64_t kDrainMs = 2000;       // after an abort: how long the stream may take to drain
+
 extern "C" int mx_rccl_wait(void* comm, void* stream, int64_t timeout_ms) {
     MX_CHECK(comm, "mx_rccl_wait: null communicator");
     if (timeout_ms <= 0) timeout_ms = g_op_timeout_ms.load();
@@ -168,10 +170,23 @@ extern "C" int mx_rccl_wait(void* comm, void* stream, int64_t timeout_ms) {
         const auto ms = std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t0).count();
         if (ms >= timeout_ms) {
             (void)ncclCommAbort(reinterpret_cast<ncclComm_t>(comm));
-            (void)hipEventSynchronize(ev);      // the aborted kernels have left the stream
-            (void)hipEventDestroy(ev);
+            // the aborted kernels should leave the stream; wait for that against a second, short
+            // deadline (never an unbounded hipEventSynchronize: a kernel that misses the abort flag,
+            // or another long kernel behind it, would hang here)
+            const auto t1 = std::chrono::steady_clock::now();
+            bool drained = false;
+            for (;;) {
+                const hipError_t q = hipEventQuery(ev);
+                if (q != hipErrorNotReady) { drained = true; break; }
+                if (std::chrono::duration_cast<std::chrono::milliseconds>(std::chrono::steady_clock::now() - t1)
+                        .count() >= kDrainMs)
+                    break;
+                std::this_thread::sleep_for(std::chrono::microseconds(500));
+            }
+            if (drained) (void)hipEventDestroy(ev);   // else the event stays: destroying it could block
             mx::set_error("mx_rccl_wait: the stream did not drain within %lld ms (a peer rank died or skipped an "
-                          "exchange); the communicator was aborted", (long long)timeout_ms);
+                          "exchange); the communicator was aborted%s", (long long)timeout_ms,
+                          drained ? "" : " and the stream was still busy 2 s later");
             return MX_ERR_RCCL;
         }
         if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(spin > 4096 ? 1000 : 20));
@@ -517,6 +532,17 @@ extern "C" int mx_mean_rows_to(const float* rows, int nrows, int64_t ld, int64_t
     MX_CHECK(order == 0 || order == 1, "mx_mean_rows_to: order %d (0 tree, 1 rank order)", order);
     MX_CHECK(dst == rows ? (dst_ld == ld || ndst <= 1) : true, "mx_mean_rows_to: in place needs dst_ld == ld");
     if (count == 0 || ndst == 0) return MX_OK;
+    {
+        // every kernel reads a column of every row before writing that column: a destination that
+        // overlaps the rows is safe only when each destination element sits in the same column of
+        // the rows' frame (offset and stride whole multiples of ld); anything else is refused
+        const uintptr_t r0 = (uintptr_t)rows, r1 = (uintptr_t)(rows + (int64_t)(nrows - 1) * ld + count);
+        const uintptr_t d0 = (uintptr_t)dst, d1 = (uintptr_t)(dst + (int64_t)(ndst - 1) * (ndst > 1 ? dst_ld : 0) + count);
+        const bool overlap = d0 < r1 && r0 < d1;
+        const int64_t off = (int64_t)(dst - rows);
+        MX_CHECK(!overlap || (off % ld == 0 && (ndst <= 1 || dst_ld % ld == 0)),
+                 "mx_mean_rows_to: dst overlaps rows at a column offset (only whole-row aliasing is supported)");
+    }
     hipStream_t st = mx::as_stream(stream);
     const float d = (float)nrows;
     const bool vec = count >= 4 && ld % 4 == 0 && (ndst <= 1 || dst_ld % 4 == 0) &&
@@ -582,6 +608,21 @@ extern "C" int mx_mean_rows_to(const float* rows, int nrows, int64_t ld, int64_t
     return MX_OK;
 }
 
+// The kernel that moves the bulk of an mx_mean_rows_to call on 16-byte aligned rows (ld, dst_ld
+// multiples of 4) -- the same dispatch as above, for reports (bench.py's centralized figure).
+extern "C" const char* mx_mean_kernel_name(int nrows, int64_t count, int order) {
+    if (nrows < 1 || count < 0 || (order != 0 && order != 1)) return "invalid";
+    const bool vec = count >= 4 && (order == 1 || nrows <= 8);
+    if (vec) {
+        if (nrows <= 8 && count / 4 >= 128) return order == 1 ? "mean_tile_kernel<0>" : "mean_tile_kernel<1>";
+        return order == 1 ? "mean4_kernel<0, 4>" : "mean4_kernel<1, 4>";
+    }
+    if (order == 1) return "mean_to_kernel<float, 0, 1>";
+    if (nrows <= 8) return "mean_to_kernel<float, 1, 8>";
+    if (nrows <= 64) return "mean_to_kernel<float, 1, 64>";
+    return "mean_to_kernel<float, 2, 1>";
+}
+
 extern "C" int mx_allgather(void* comm_v, const float* send, int64_t count, float* gather, void* stream) {
     MX_CHECK(comm_v && count >= 0 && (count == 0 || (send && gather)), "mx_allgather: bad arguments");
     if (count == 0) return MX_OK;
@@ -615,8 +656,16 @@ extern "C" int mx_ipc_alloc(int64_t bytes, void** ptr_out, void* handle_out) {
     MX_CHECK(bytes > 0 && ptr_out && handle_out, "mx_ipc_alloc: bad arguments");
     void* p = nullptr;
     MX_HIP(hipMalloc(&p, (size_t)bytes));
+    // zero-filled (the pull header's epoch starts at 0) and complete before the handle is shared
+    hipError_t e = hipMemset(p, 0, (size_t)bytes);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+        (void)hipFree(p);
+        mx::set_error("mx_ipc_alloc: hipMemset -> %s", hipGetErrorString(e));
+        return MX_ERR_HIP;
+    }
     hipIpcMemHandle_t h;
-    const hipError_t e = hipIpcGetMemHandle(&h, p);
+    e = hipIpcGetMemHandle(&h, p);
     if (e != hipSuccess) {
         (void)hipFree(p);
         mx::set_error("mx_ipc_alloc: hipIpcGetMemHandle -> %s", hipGetErrorString(e));

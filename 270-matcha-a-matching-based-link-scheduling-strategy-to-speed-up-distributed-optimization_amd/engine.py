@@ -18,7 +18,7 @@ import time
 import numpy as np
 import torch
 
-from ._lib import MXError, check, lib, require_device, stream_ptr
+from ._lib import MX_ERR_RCCL, MXError, check, lib, require_device, stream_ptr
 
 ROW_ALIGN = 64  # arena rows padded to 256 B
 
@@ -141,7 +141,8 @@ class RcclComm:
         ms = int(1000 * (self.timeout_s if timeout_s is None else float(timeout_s)))
         rc = lib.mx_rccl_wait(self.handle, stream_ptr(stream), max(1, ms))
         if rc:
-            self.handle = None                  # aborted by mx_rccl_wait
+            if rc == MX_ERR_RCCL:
+                self.handle = None              # only the timeout path aborts the communicator
             check(rc, "mx_rccl_wait")
 
     def abort(self):
@@ -161,30 +162,42 @@ class PullTransport:
     """Cross-GPU partner rows without RCCL: every rank publishes a snapshot of its rows in an
     IPC-shared device buffer (mx_ipc_alloc); its peers map it (mx_ipc_open) and their mixing
     kernel reads the partner rows straight from this GPU's HBM over xGMI (communicator.py:110's
-    sendrecv becomes a remote load inside the FMA chain).  Round protocol (VirtualWorkerGroup):
-        1. copy the local rows into snapshot buffer `round % 2` (mx_snapshot_publish: a local HBM
-           copy whose workgroups end with a system-scope release, so the bytes are in HBM, not
-           only in this GPU's write-back L2, when the kernel completes);
-        2. synchronize + barrier: every rank's snapshot of this round is complete;
-        3. point the receive slots of this round's plan at the peers' snapshot rows and mix; the
-           plan records carry the peer-reads bit (mx_plan_set_peer_reads), so every workgroup of
-           the mixing kernel first acquires at system scope (buffer_inv sc0 sc1): lines of the
-           same snapshot buffer cached on THIS GPU in round r - 2 are not served.
-    Snapshots alternate between two buffers, so round r+1's copy never overwrites what a slower
-    peer still reads in round r; round r+2's copy comes after round r+1's barrier, which every
-    rank passes only once its round-r mix has finished.  Needs one process per GPU of ONE node
+    sendrecv becomes a remote load inside the FMA chain).  A round is three launches on one
+    stream and nothing on the host (VirtualWorkerGroup._step_pull):
+        1. mx_snapshot_publish: the local rows into snapshot `round % 2` of the buffer, every
+           workgroup ending with a system-scope release (the bytes reach HBM, not only this
+           GPU's write-back L2);
+        2. mx_pull_gate (one wave): this rank's epoch = round + 1 (system-scope release), then a
+           bounded wait for the epochs of the ranks owning this round's and the previous round's
+           remote partners, then the receive slots pointed at their snapshot rows (csrc/pull.hip);
+        3. the mixing kernel; the plan records carry the peer-reads bit
+           (mx_plan_set_peer_reads), so every workgroup first acquires at system scope: lines of
+           the same snapshot buffer cached on THIS GPU in round r - 2 are not served.
+    Snapshots alternate between two buffers; a rank overwrites snapshot r % 2 in round r + 2 only
+    after its gate of round r + 1 saw every reader of round r past its mix.  A
+    peer that stops publishing makes the gate expire after `timeout_s` (default
+    $MX_PULL_TIMEOUT_S or 300 s): sticky error words, MXError at the end of the round
+    (VirtualWorkerGroup.wait_round) or at the next step.  Needs one process per GPU of ONE node
     (the peers' HBM must be mappable) -- or, for tests, several processes sharing a GPU.
-    Bootstrap and barrier use torch.distributed (any backend).  VirtualWorkerGroup.close() is
-    collective under this transport (a barrier before the buffers are freed)."""
+    Bootstrap uses torch.distributed (any backend).  VirtualWorkerGroup.close() is collective
+    under this transport (a barrier before the buffers are freed)."""
 
     handle = None
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, timeout_s=None):
+        import os
         import torch.distributed as dist
         require_device()
         self.group = group
         self.rank = dist.get_rank(group)
         self.nranks = dist.get_world_size(group)
+        if self.nranks > 64:
+            raise ValueError("PullTransport: at most 64 ranks")
+        if timeout_s is None:
+            timeout_s = float(os.environ.get("MX_PULL_TIMEOUT_S") or 300.0)
+        if not timeout_s > 0:
+            raise ValueError("PullTransport: timeout_s must be > 0")
+        self.timeout_s = float(timeout_s)
 
     def bind(self, vwg):
         """Collective: allocate vwg's snapshot buffer, exchange handles, map the peers'.  Every
@@ -197,7 +210,8 @@ class PullTransport:
         handle = (ctypes.c_char * hb)()
         err = None
         try:
-            check(lib.mx_ipc_alloc(2 * half, ctypes.byref(own), ctypes.cast(handle, ctypes.c_void_p)), "mx_ipc_alloc")
+            check(lib.mx_ipc_alloc(PULL_HEADER + 2 * half, ctypes.byref(own), ctypes.cast(handle, ctypes.c_void_p)),
+                  "mx_ipc_alloc")
         except MXError as e:
             err = str(e)
         objs = [None] * self.nranks
@@ -228,13 +242,40 @@ class PullTransport:
             if own.value:
                 lib.mx_ipc_free(own.value)
             raise MXError(f"pull transport unavailable: rank {bad[0][0]}: {bad[0][1]}")
-        return _PullState(self, own.value, peers, opened, half)
+        return _PullState(self, vwg, own.value, peers, opened, half)
+
+
+PULL_HEADER = 256          # MX_PULL_HEADER_BYTES: the epoch word ahead of the two snapshots
 
 
 class _PullState:
-    def __init__(self, transport, own, peers, opened, half):
+    """One group's bound pull buffers: the device table of every rank's snapshot buffer
+    (mx_pull_rank), the previous round's flags row, and the gate's sticky error words."""
+
+    def __init__(self, transport, vwg, own, peers, opened, half):
         self.transport, self.own, self.peers, self.opened, self.half = transport, own, peers, opened, half
         self.round = 0
+        blocks = partition(int(vwg.topology.size), transport.nranks)
+        tab = np.zeros((transport.nranks, 2), np.int64)
+        for r, (b, c) in enumerate(blocks):
+            tab[r, 0] = peers[r]
+            tab[r, 1] = (int(b) & 0xFFFFFFFF) | (int(c) << 32)      # int32 row_base, int32 n_local
+        self.ranks_dev = torch.from_numpy(tab).to("cuda")
+        self.owner_dev = torch.from_numpy(np.ascontiguousarray(vwg.engine.owner)).to("cuda")
+        self.prev_row = torch.zeros(vwg.engine.M, dtype=torch.uint8, device="cuda")
+        host, dev = ctypes.POINTER(ctypes.c_int32)(), ctypes.c_void_p()
+        check(lib.mx_host_words(4, ctypes.byref(host), ctypes.byref(dev)), "mx_host_words")
+        self.err_host, self.err_dev = host, dev.value
+
+    def error(self):
+        """None, or the gate's message once one of its waits expired (sticky)."""
+        if not self.err_host or self.err_host[0] == 0:
+            return None
+        e = [int(self.err_host[i]) for i in range(4)]
+        if e[0] == 2:
+            return "pull gate: more distinct remote partners than receive slots"
+        return (f"pull gate: rank {e[1]} did not publish round epoch {e[2]} within "
+                f"{self.transport.timeout_s:g} s (last seen {e[3]}); the round's result is undefined")
 
     def close(self):
         for p in self.opened:
@@ -243,13 +284,19 @@ class _PullState:
         if self.own:
             lib.mx_ipc_free(self.own)
             self.own = 0
+        if self.err_host:
+            lib.mx_host_words_free(ctypes.cast(self.err_host, ctypes.c_void_p))
+            self.err_host = None
 
 
 def wait_round(comm, stream=None):
     """The end-of-round synchronisation of communicate(): with the library's RCCL communicator a
     deadline-bounded wait (RcclComm.wait -- a peer gone mid-exchange raises instead of hanging),
-    otherwise torch.cuda.synchronize()."""
-    if isinstance(comm, RcclComm) and comm.handle:
+    otherwise torch.cuda.synchronize().  An RcclComm that was aborted raises: its kernels may
+    still be queued, and an unbounded synchronize could hang on them."""
+    if isinstance(comm, RcclComm):
+        if not comm.handle:
+            raise MXError("the RCCL communicator was aborted or closed (an earlier exchange timed out)")
         comm.wait(stream)
     else:
         torch.cuda.synchronize()
@@ -595,11 +642,11 @@ class VirtualWorkerGroup:
             check(lib.mx_plan_set_peer_reads(self.engine.plan.data_ptr(), self.engine.T + 1, self.n_local,
                                              self.engine.M, 1, stream_ptr()), "mx_plan_set_peer_reads")
             self.engine.peer_reads = True
-            self._pull_table = np.zeros((1, self.engine.n_slots), np.int64)
-            self._pull_table[0, :self.n_local] = self._row_ptrs
-            self._pull_table[0, self.n_local:] = self._pull.own
-            self.layout = Layout([self.numel], [[int(p)] for p in self._pull_table[0]], self.engine.n_slots)
-            self._blocks = partition(n, nranks)
+            # receive slots start at this rank's own snapshot 0 (valid memory); every round's gate
+            # points them at the partners' snapshot rows on the device (mx_pull_gate)
+            slot_ptrs = [[p] for p in self._row_ptrs]
+            slot_ptrs += [[self._pull.own + PULL_HEADER]] * self.engine.max_remote
+            self.layout = Layout([self.numel], slot_ptrs, self.engine.n_slots)
         else:
             slot_ptrs = [[p] for p in self._row_ptrs]
             if self.slab is not None:
@@ -627,30 +674,38 @@ class VirtualWorkerGroup:
         return True
 
     def _step_pull(self, it, stream=None):
-        """PullTransport round: snapshot, barrier, receive slots -> peers' snapshots, mix."""
-        import torch.distributed as dist
+        """PullTransport round, three launches on one stream and no host wait: snapshot publish,
+        the gate (epoch out, bounded epoch waits, receive slots -> the partners' snapshot rows),
+        mix.  A gate that expired in an earlier round raises here (sticky)."""
         st = self._pull
+        msg = st.error()
+        if msg:
+            raise MXError(msg)
+        eng = self.engine
+        it = eng.round_index(it)
         par = st.round & 1
         st.round += 1
-        total = self.n_local * self.ld
+        s = stream_ptr(stream)
         # the copy ends with a system-scope release per workgroup (visible to the peers' loads)
-        check(lib.mx_snapshot_publish(self.arena.data_ptr(), st.own + par * st.half, total, stream_ptr(stream)),
-              "mx_snapshot_publish")
-        torch.cuda.synchronize()
-        dist.barrier(group=st.transport.group)
-        eng = self.engine
-        table = self._pull_table
-        for kind, peer, idx, who in eng.exchange_plan(it):
-            if kind == 1:
-                owner = int(eng.owner[who])
-                base, n_loc = self._blocks[owner]
-                table[0, self.n_local + int(idx)] = (st.peers[owner] + par * n_loc * self.ld * 4 +
-                                                     (int(who) - base) * self.ld * 4)
-        self.layout.seg_ptrs.copy_(torch.from_numpy(table), non_blocking=False)
-        if stream is not None:
-            stream.wait_stream(torch.cuda.current_stream())
+        check(lib.mx_snapshot_publish(self.arena.data_ptr(), st.own + PULL_HEADER + par * st.half,
+                                      self.n_local * self.ld, s), "mx_snapshot_publish")
+        frow = (eng._adhoc_flags.data_ptr() if it == eng.T else eng.flags_dev.data_ptr() + it * eng.M)
+        tr = st.transport
+        check(lib.mx_pull_gate(frow, st.prev_row.data_ptr(), eng.M, eng.partner_dev.data_ptr(), eng.n,
+                               st.owner_dev.data_ptr(), st.ranks_dev.data_ptr(), tr.nranks, tr.rank, self.row_base,
+                               self.n_local, self.ld * 4, par, st.round, self.layout.seg_ptrs.data_ptr(),
+                               eng.n_slots, tr.timeout_s, st.err_dev, s), "mx_pull_gate")
         eng.mix(it, self.layout, stream)
         return True
+
+    def wait_round(self, stream=None):
+        """The end of a round for communicate(): the transport's wait (engine.wait_round), then
+        the pull gate's sticky error, if any, as MXError."""
+        wait_round(self.engine.comm, stream)
+        if self._pull is not None:
+            msg = self._pull.error()
+            if msg:
+                raise MXError(msg)
 
     @property
     def pulls(self):
@@ -741,5 +796,5 @@ class VirtualWorkerGroup:
         torch.cuda.synchronize()
         tic = time.time()
         self.step(it)
-        wait_round(self.engine.comm)
+        self.wait_round()
         return time.time() - tic

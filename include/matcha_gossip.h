@@ -351,6 +351,33 @@ int mx_snapshot_publish(const float* src, float* dst, int64_t n, void* stream);
  * the mixing kernels then start with a system-scope acquire per workgroup (buffer_inv sc0 sc1: no
  * line of a peer's buffer cached on this GPU from an earlier round is served).  on = 1 / 0. */
 int mx_plan_set_peer_reads(int32_t* plan_dev, int64_t T, int n_local, int M, int on, void* stream);
+/* A rank's snapshot buffer (mx_ipc_alloc, zero-filled): MX_PULL_HEADER_BYTES of header -- its
+ * uint64 epoch at offset 0 -- then snapshot 0 and snapshot 1, each n_local rows of ld_bytes. */
+#define MX_PULL_HEADER_BYTES 256
+typedef struct mx_pull_rank {
+    int64_t base;      /* the rank's snapshot buffer as mapped in THIS process (own: the allocation) */
+    int32_t row_base;  /* its block of workers [row_base, row_base + n_local) */
+    int32_t n_local;
+} mx_pull_rank;
+/* The pull round's handshake, one single-wave kernel on `stream` between mx_snapshot_publish (into
+ * snapshot `parity`) and the mixing launch -- replaces the host synchronize + barrier + pointer-table
+ * copy per round (and the reference's sendrecv pairing, communicator.py:99-112):
+ *   1. epoch[my_rank] = epoch (system-scope release; the snapshot is complete by stream order);
+ *   2. bounded wait for epoch[r] >= epoch of every rank r owning an active remote partner of a
+ *      local worker under flags_row_dev (this round) or prev_row_dev (the previous pull round);
+ *   3. slot_ptrs_dev[n_local + j] = the j-th distinct remote partner's row in its owner's snapshot
+ *      `parity` (plan_kernel's slot numbering); prev_row_dev = flags_row_dev afterwards.
+ * ranks_dev: mx_pull_rank[nranks] (device).  On expiry after timeout_s: err_dev[0] = 1, [1] = the
+ * rank that did not publish, [2] = the epoch awaited, [3] = the last one seen (err_dev: mx_host_words,
+ * read by the host once the stream has passed the gate); err_dev[0] = 2: more remote partners than
+ * slots.  1 <= n_global <= 4096, nranks <= 64, epochs start at 1 and rise by one per pull round. */
+int mx_pull_gate(const uint8_t* flags_row_dev, uint8_t* prev_row_dev, int M, const int32_t* partner_dev,
+                 int n_global, const int32_t* owner_dev, const mx_pull_rank* ranks_dev, int nranks, int my_rank,
+                 int row_base, int n_local, int64_t ld_bytes, int parity, uint64_t epoch, int64_t* slot_ptrs_dev,
+                 int n_slots, double timeout_s, int32_t* err_dev, void* stream);
+/* n zeroed int32 words of coherent mapped host memory: *host_out for the host, *dev_out for kernels. */
+int mx_host_words(int n, int32_t** host_out, int32_t** dev_out);
+int mx_host_words_free(int32_t* host);
 int mx_ipc_handle_bytes(void);
 int mx_ipc_alloc(int64_t bytes, void** ptr_out, void* handle_out);
 int mx_ipc_open(const void* handle, void** ptr_out);
@@ -383,6 +410,10 @@ int mx_mean_rows(const float* rows, int nrows, int64_t ld, int64_t count, int or
  * staged in LDS. */
 int mx_mean_rows_to(const float* rows, int nrows, int64_t ld, int64_t count, int order, float* dst, int ndst,
                     int64_t dst_ld, void* stream);
+/* The kernel that carries the bulk of mx_mean_rows_to(nrows, count, order) on 16-byte aligned rows
+ * (static string, e.g. "mean_tile_kernel<1>"), for reports.  A dst that overlaps the rows other
+ * than at whole-row offsets (offset and dst_ld multiples of ld) is refused (MX_ERR_INVALID). */
+const char* mx_mean_kernel_name(int nrows, int64_t count, int order);
 
 /* ---------------------------------------------------------------- host: matching decomposition
  * nx.max_weight_matching (graph_manager.py:64, inside GraphProcessor.getSubGraphs 57-83) without

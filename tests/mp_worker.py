@@ -33,7 +33,9 @@ def by_worker(grp, rows):
     return out
 
 
-def decen_case(pkg, T, gid, P, rounds, chunk_cols=None, seed=5, placement=None):
+def decen_case(pkg, T, gid, P, rounds, chunk_cols=None, seed=5, placement=None, back_to_back=False):
+    """rounds through communicate() (a wait per round), or with back_to_back all rounds enqueued
+    by step() with no host wait between them (one synchronize at the end)"""
     rank, world = dist.get_rank(), dist.get_world_size()
     n = pkg.GRAPH_SIZES[gid]
     gp = pkg.GraphProcessor(pkg.select_graph(gid), 1.0, 0, n, 4, True)
@@ -47,9 +49,14 @@ def decen_case(pkg, T, gid, P, rounds, chunk_cols=None, seed=5, placement=None):
     X = np.stack([O.synth(77 + i, P) for i in range(n)])
     grp.rows.copy_(torch.from_numpy(X[grp.workers]))
     for it in range(rounds):
-        grp.communicate()
+        if back_to_back:
+            grp.step(it)
+        else:
+            grp.communicate()
         if flags[it].any():
             X = O.decen_round(X, topo.neighbors_info, flags[it], 0.21)
+    if back_to_back:
+        grp.wait_round()
     got = by_worker(grp, gather_rows(grp.rows, grp.row_base, n))
     grp.close()
     return bool(np.array_equal(got.view(np.uint32), X.view(np.uint32)))
@@ -126,6 +133,8 @@ def main():
         # kernel reads partner rows from it (processes share GPU 0 here; xGMI on a real node)
         "decen_g0_pull": decen_case(pkg, pkg.PullTransport(), 0, 30_011, 6),
         "decen_g2_pull_placed": decen_case(pkg, pkg.PullTransport(), 2, 9_001, 5, placement="auto"),
+        # 40 device-gated rounds (no host barrier per round): each snapshot buffer reused 20 times
+        "decen_g0_pull_long": decen_case(pkg, pkg.PullTransport(), 0, 30_011, 40, seed=11, back_to_back=True),
     }
     torch.cuda.synchronize()
     if dist.get_rank() == 0:

@@ -125,6 +125,19 @@ def test_bench_multiprocess_overlap_forms(nproc, overlap, pull):
         assert set(out["overlap"]["calib_ms"]) == {"rccl", "rccl_chunked", "pull"}
 
 
+def test_pull_gate_stalled_peer_raises():
+    """PullTransport without a host barrier: a rank whose peer stops publishing is held by the
+    device gate's BOUNDED wait (mx_pull_gate, 2 s deadline here) and communicate() raises MXError
+    naming the peer -- no hang; the error is sticky (the next step raises at once); the stalled
+    peer's own round completes once it resumes."""
+    r = _torchrun(2, [os.path.join(HERE, "mp_pull_stall.py")], timeout=150)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["first_rounds_ok"] and out["raised"] and out["sticky"] and out["peer_round_ok"], out
+    assert "rank 1 did not publish" in out["message"], out
+    assert 1.5 <= out["seconds"] < 30, out
+
+
 def test_bench_self_launch_gloo():
     """`python bench.py --gpus 2` WITHOUT torchrun: the parent starts the ranks
     as a child torch.distributed.run and relays rank 0's line -- n_gpus 2, the oracle self-check
