@@ -11,7 +11,7 @@ from .engine import GossipEngine, VirtualWorkerGroup, RcclComm, PullTransport, L
 from .choco import ChocoWorkerGroup, topk_count
 from .communicator import Communicator, decenCommunicator, ChocoCommunicator, centralizedCommunicator
 from .comm_helpers import flatten_tensors, unflatten_tensors, scatter_tensors
-from .compressors import get_top_k
+from .compressors import get_top_k, check_top_k
 from .topologies import select_graph, erdos_renyi, GRAPH_SIZES
 from . import solver
 from . import harness
@@ -22,6 +22,6 @@ __all__ = [
     "MXError", "lib", "GraphProcessor", "FixedProcessor", "MatchaProcessor", "GossipEngine",
     "VirtualWorkerGroup", "RcclComm", "PullTransport", "Layout", "partition", "ChocoWorkerGroup", "topk_count",
     "Communicator", "decenCommunicator", "ChocoCommunicator", "centralizedCommunicator",
-    "flatten_tensors", "unflatten_tensors", "scatter_tensors", "get_top_k", "select_graph",
+    "flatten_tensors", "unflatten_tensors", "scatter_tensors", "get_top_k", "check_top_k", "select_graph",
     "erdos_renyi", "GRAPH_SIZES", "solver", "harness", "placement", "best_placement", "placement_cost",
 ]

@@ -38,6 +38,7 @@ SIGNATURES = {
     "mx_topk_set": (c_int, [ctypes.c_char_p, c_i64]),
     "mx_topk_get": (c_i64, [ctypes.c_char_p]),
     "mx_topk_check": (c_int, [c_p, c_i64, c_int, c_i64, c_p]),
+    "mx_topk_err_forward": (c_int, [c_p, c_i64, c_int, c_i64, c_p, c_p]),
     "mx_topk_stats": (c_int, [c_p, c_i64, c_int, c_i64, c_p, c_p]),
     "mx_topk_abs_diff": (c_int, [c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p]),
     "mx_topk_abs_diff_rows": (c_int, [c_p, c_p, c_i64, c_int, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_p]),

@@ -319,13 +319,14 @@ class decenCommunicator(Communicator):
 
     def _round_of(self, active_flags):
         """The plan record of `active_flags`: the schedule's row of the current iteration when they
-        are that row (the reference's communicate() passes exactly it), else a scratch record."""
+        are that row (the reference's communicate() passes exactly it), else any record already
+        built for the same row (engine.record_for), else a scratch record."""
         eng = self._group.engine
         f = eng.flags_row(active_flags)
         i = self.iter - 1
         if 0 <= i < eng.T and np.array_equal(f, eng.flags_host[i]):
             return i
-        return eng.adhoc(f)
+        return eng.record_for(f)
 
     def prepare_comm_buffer(self):
         """communicator.py:87-90.  `self.tensor_list` (set by the caller, as the reference's

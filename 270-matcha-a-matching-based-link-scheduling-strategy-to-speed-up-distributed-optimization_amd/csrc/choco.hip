@@ -72,6 +72,7 @@ struct SelState {
     uint32_t last_cand;   // the last call's candidate count (keys kept by its first compaction)
     uint32_t win_digit;   // the last call's floor digit (fine_floor's window; b0 itself is rewritten
                           // by the compaction while its other blocks still read the window)
+    int32_t scan;         // row 0 only: mx_topk_check's result (first row with `err` set, or -1)
 };
 static_assert(sizeof(SelState) <= 64, "SelState must fit its 64-byte slot");
 
@@ -330,6 +331,9 @@ __device__ __forceinline__ uint32_t ld_sc1(const uint32_t* p) {
 }
 
 constexpr uint64_t kSpinTicks = 1ull << 28;    // ~2.7 s of the 100 MHz constant clock
+// the bounded waits' deadline (mx_topk_set "spin_ticks": a test knob -- 0 makes every wait that has
+// to wait at all expire, so the error path can be exercised on purpose)
+__device__ uint64_t g_spin_ticks_dev = kSpinTicks;
 
 // block-uniform values the compiler cannot prove uniform (they come through LDS): into SGPRs
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -344,7 +348,7 @@ __device__ __forceinline__ bool wait_count(const uint32_t* ctr, uint32_t target)
     const uint64_t t0 = wall_clock64();
     while (ld_sc1(ctr) < target) {
         __builtin_amdgcn_s_sleep(2);
-        if ((uint64_t)wall_clock64() - t0 > kSpinTicks) return false;
+        if ((uint64_t)wall_clock64() - t0 > g_spin_ticks_dev) return false;
     }
     return true;
 }
@@ -1833,6 +1837,7 @@ unsigned clamp_grid(int64_t n, int64_t per, int64_t cap) {
 }  // namespace
 
 int g_sample_stride = 0;   // 0 = auto (about kSampleTarget sampled elements per row)
+uint64_t g_spin_ticks_host = kSpinTicks;   // host copy of g_spin_ticks_dev (mx_topk_get)
 int g_compact_blocks = 0;     // persistent compaction blocks over all rows; 0 = auto: ~720 for one
                               // row (an even chunk count each), 2560 for several (same-box sweeps: one row 256 / 384 / 512 / 640 /
                               // 1024 / 2048 blocks 131 / 121 / 116.4 / 116.2 / 119 / 134 us per round,
@@ -1987,6 +1992,13 @@ extern "C" int mx_topk_set(const char* key, int64_t value) {
         g_select_blocks = (int)value;
         return MX_OK;
     }
+    if (!strcmp(key, "spin_ticks")) {
+        MX_CHECK(value >= 0, "mx_topk_set: spin_ticks %lld", (long long)value);
+        const uint64_t v = (uint64_t)value;
+        MX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_spin_ticks_dev), &v, sizeof(v)));
+        g_spin_ticks_host = v;
+        return MX_OK;
+    }
     if (!strcmp(key, "sample_pieces")) {
         MX_CHECK(value >= 1 && value <= 1024, "mx_topk_set: sample_pieces %lld", (long long)value);
         g_sample_pieces = (int)value;
@@ -1996,6 +2008,7 @@ extern "C" int mx_topk_set(const char* key, int64_t value) {
 }
 
 extern "C" int64_t mx_topk_get(const char* key) {
+    if (key && !strcmp(key, "spin_ticks")) return (int64_t)g_spin_ticks_host;
     if (key && !strcmp(key, "sample_stride")) return g_sample_stride;
     if (key && !strcmp(key, "compact_blocks")) return g_compact_blocks;
     if (key && !strcmp(key, "sample_pieces")) return g_sample_pieces;
@@ -2116,10 +2129,14 @@ extern "C" int mx_topk_abs_diff_rows(const float* x, const float* x_hat, int64_t
 }
 
 // The rows' sticky error words (a bounded row-barrier wait that expired: the sampled-floor fallback
-// in cand_hist<10>, or select_kernel): synchronises `stream`, reads and clears them.
+// in cand_hist<10>, or select_kernel).
 namespace {
-// one lane: the first row whose error word is set (or -1), and every set word cleared
-__global__ void err_scan_kernel(char* work, int64_t work_ld, int nrows, int64_t off, int32_t* out) {
+// one lane: the first row whose error word is set (or -1), every set word cleared; the result goes
+// to row 0's SelState.scan (the caller's own scratch: no word shared between calls or streams) and,
+// when `flag` is given and a row was set, row + 1 to *flag with a system-scope release (a host-mapped
+// word the host reads without synchronising: mx_topk_err_forward)
+__global__ void err_scan_kernel(char* work, int64_t work_ld, int nrows, int64_t off, int64_t scan_off,
+                                int32_t* flag) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     int32_t bad = -1;
     for (int r = 0; r < nrows; ++r) {
@@ -2129,29 +2146,32 @@ __global__ void err_scan_kernel(char* work, int64_t work_ld, int nrows, int64_t 
             *e = 0u;
         }
     }
-    *out = bad;
+    *reinterpret_cast<int32_t*>(work + scan_off) = bad;
+    if (flag && bad >= 0)
+        __hip_atomic_store((__attribute__((address_space(1))) int32_t*)flag, bad + 1, __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+int launch_err_scan(void* work, int64_t work_ld_bytes, int nrows, int64_t P, int32_t* flag, hipStream_t st) {
+    const int64_t off = (int64_t)(layout(P).state + offsetof(SelState, err));
+    const int64_t scan_off = (int64_t)(layout(P).state + offsetof(SelState, scan));
+    hipLaunchKernelGGL(err_scan_kernel, dim3(1), dim3(64), 0, st, static_cast<char*>(work), work_ld_bytes, nrows, off,
+                       scan_off, flag);
+    MX_LAUNCH_CHECK();
+    return MX_OK;
 }
 }  // namespace
 
+// Synchronises `stream`, reads and clears the words; MX_ERR_HIP naming the first row if any was set.
 extern "C" int mx_topk_check(void* work, int64_t work_ld_bytes, int nrows, int64_t P, void* stream) {
     MX_CHECK(work && nrows >= 1 && P >= 1 && (nrows == 1 || work_ld_bytes >= (int64_t)layout(P).total),
              "mx_topk_check: bad arguments");
-    static int32_t* dev_out[64] = {nullptr};     // one word per device, allocated once
-    static std::mutex mu;
-    int dev = 0;
-    MX_HIP(hipGetDevice(&dev));
-    MX_CHECK(dev >= 0 && dev < 64, "mx_topk_check: device %d", dev);
-    {
-        std::lock_guard<std::mutex> lock(mu);
-        if (!dev_out[dev]) MX_HIP(hipMalloc(&dev_out[dev], sizeof(int32_t)));
-    }
     hipStream_t st = mx::as_stream(stream);
-    const int64_t off = (int64_t)(layout(P).state + offsetof(SelState, err));
-    hipLaunchKernelGGL(err_scan_kernel, dim3(1), dim3(64), 0, st, static_cast<char*>(work), work_ld_bytes, nrows, off,
-                       dev_out[dev]);
-    MX_LAUNCH_CHECK();
+    const int rc = launch_err_scan(work, work_ld_bytes, nrows, P, nullptr, st);
+    if (rc != MX_OK) return rc;
     int32_t bad = -1;
-    MX_HIP(hipMemcpyAsync(&bad, dev_out[dev], sizeof(bad), hipMemcpyDeviceToHost, st));
+    MX_HIP(hipMemcpyAsync(&bad, static_cast<char*>(work) + layout(P).state + offsetof(SelState, scan), sizeof(bad),
+                          hipMemcpyDeviceToHost, st));
     MX_HIP(hipStreamSynchronize(st));
     if (bad >= 0) {
         mx::set_error("mx_topk: a row barrier's bounded wait expired (row %d): not every block of the row was "
@@ -2159,6 +2179,17 @@ extern "C" int mx_topk_check(void* work, int64_t work_ld_bytes, int nrows, int64
         return MX_ERR_HIP;
     }
     return MX_OK;
+}
+
+// Stream-ordered and non-blocking: the words are scanned and cleared on `stream` behind the call
+// they belong to, and an expired one is forwarded as row + 1 to *flag_dev (mx_host_words: the host
+// polls it without a synchronisation, e.g. at the start of its next call).
+extern "C" int mx_topk_err_forward(void* work, int64_t work_ld_bytes, int nrows, int64_t P, int32_t* flag_dev,
+                                   void* stream) {
+    MX_CHECK(work && flag_dev && nrows >= 1 && P >= 1 &&
+                 (nrows == 1 || work_ld_bytes >= (int64_t)layout(P).total),
+             "mx_topk_err_forward: bad arguments");
+    return launch_err_scan(work, work_ld_bytes, nrows, P, flag_dev, mx::as_stream(stream));
 }
 
 // Per row: {calls, fallback compactions, current floor-hint margin, the last call's threshold key T,

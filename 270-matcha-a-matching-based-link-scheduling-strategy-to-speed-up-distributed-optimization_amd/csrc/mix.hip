@@ -1093,6 +1093,7 @@ extern "C" int mx_mix_set(const char* key, int value) {
     } else if (!strcmp(key, "mid_tiles")) {
         MX_CHECK(value >= 0 && value <= 1024, "mx_mix_set: mid_tiles %d", value);
         slot = &g_tune.mid_tiles;
+
     } else if (!strcmp(key, "flat_small")) {
         MX_CHECK(value >= 0 && value <= 4096, "mx_mix_set: flat_small %d", value);
         slot = &g_tune.flat_small;

@@ -434,6 +434,7 @@ class GossipEngine:
         self.peer_reads = False                  # set by a pull-transport group: applied to adhoc records too
         self._adhoc_ready = False
         self._adhoc_flags = None
+        self._row_index = None                   # flags bytes -> first schedule iteration (record_for)
 
     def adhoc(self, active_flags):
         """A round for an arbitrary flags row -- the reference's averaging(active_flags) takes any
@@ -456,6 +457,25 @@ class GossipEngine:
             check(lib.mx_plan_set_peer_reads(rec, 1, self.n_local, self.M, 1, stream_ptr()), "mx_plan_set_peer_reads")
         self._adhoc_ready = True
         return self.T
+
+    def record_for(self, active_flags):
+        """The plan record of an arbitrary flags row without rebuilding when one exists: a record
+        depends only on the row (partners and alpha are fixed), so any schedule iteration with the
+        same row -- or the scratch record when it already holds this row -- serves it; otherwise
+        adhoc() builds it.  (The reference's averaging(active_flags) sub-step, communicator.py:92-122,
+        driven directly: at most 2^M distinct rows, so rebuilds stop after the first of each.)"""
+        f = self.flags_row(active_flags)
+        key = f.tobytes()
+        if self._row_index is None:
+            self._row_index = {}
+            for t in range(self.T - 1, -1, -1):          # the first iteration holding each row
+                self._row_index[self.flags_host[t].tobytes()] = t
+        t = self._row_index.get(key)
+        if t is not None:
+            return t
+        if self._adhoc_ready and self.flags_host[self.T].tobytes() == key:
+            return self.T
+        return self.adhoc(f)
 
     def flags_row(self, active_flags):
         return flags_row(active_flags, self.M)

@@ -38,6 +38,14 @@ PKG_NAME = "270-matcha-a-matching-based-link-scheduling-strategy-to-speed-up-dis
 HBM_PEAK = 8.0e12          # bytes/s, MI355X spec (MI355X_MICROARCH.md)
 XGMI_LINK_PEAK = 153e9     # bytes/s per direction per link
 METRIC = "gossip rounds/sec (8 workers x 25.6M fp32 params, graph 0, full MATCHA round)"
+# Fixed per-round cost of each N > 1 exchange form (seconds), for the `predicted` object.  pull:
+# measured with tools/form_overhead.py at P = 100k, N processes sharing one GPU (profiles/
+# r05b_pull_overhead_after_n*.log: snapshot publish + gate + mix launches, device gate).  RCCL
+# forms: not measurable on a one-GPU box (RCCL refuses two ranks on one device) -- ASSUMED one
+# grouped send/recv launch (~25 us) per exchange, one per chunk for the pipelined form.
+PULL_FIXED_S = {2: 26e-6, 4: 31e-6, 8: 62e-6}
+RCCL_FIXED_S = 25e-6
+HEADLINE_HBM_FRAC = 0.75   # the mixing kernel's measured fraction of 8 TB/s (BENCH_r04, profiles/)
 
 
 def parse():
@@ -381,6 +389,30 @@ def round_bytes(partner, owner, flags_rows, rank, row_base, n_local, P):
     return hbm, link, pair_b, total
 
 
+def predict_round(form, world, link_bytes, mix_s, publish_bytes, chunks=4, mix_source="measured"):
+    """What a round of `form` should cost at N = world, from its parts: the busiest
+    xGMI link's bytes at 153 GB/s, the mixing kernel on this GPU (mix_s), the form's fixed cost
+    (PULL_FIXED_S measured / RCCL_FIXED_S assumed) and, for pull, the snapshot copy at the headline's
+    HBM fraction.  plain RCCL: exchange, then mix (one stream); pipelined: the longer of the two
+    plus one chunk of the shorter; pull: publish, then the mix reading partners over xGMI."""
+    t_link = link_bytes / XGMI_LINK_PEAK
+    if form == "pull":
+        fixed = PULL_FIXED_S.get(world, max(PULL_FIXED_S.values()))
+        src = "measured (tools/form_overhead.py, N processes sharing one GPU)"
+        t_pub = publish_bytes / (HEADLINE_HBM_FRAC * HBM_PEAK)
+        t = t_pub + max(t_link, mix_s) + fixed
+    elif form == "rccl_chunked":
+        fixed, src, t_pub = chunks * RCCL_FIXED_S, "assumed (no two-GPU RCCL run yet)", 0.0
+        t = max(t_link, mix_s) + min(t_link, mix_s) / chunks + fixed
+    else:
+        fixed, src, t_pub = RCCL_FIXED_S, "assumed (no two-GPU RCCL run yet)", 0.0
+        t = t_link + mix_s + fixed
+    return {"busiest_link_bytes": float(link_bytes), "link_bound_ms": 1e3 * t_link, "mix_ms": 1e3 * mix_s,
+            "mix_source": mix_source, "publish_ms": 1e3 * t_pub, "fixed_ms": 1e3 * fixed, "fixed_source": src,
+            "round_ms": 1e3 * t, "rounds_per_s": 1.0 / t if t > 0 else None,
+            "xgmi_frac": (link_bytes / t / XGMI_LINK_PEAK) if t > 0 else None}
+
+
 def p2p_probe(rank, world, nbytes, dev, reps=5):
     """N > 1: one xGMI link through RCCL (torch.distributed send/recv on the nccl group), ranks 0
     and 1 only: unidirectional 0 -> 1 and bidirectional 0 <-> 1, seconds per transfer (max over
@@ -507,7 +539,8 @@ def allreduce_figure(pkg, args, rank, world, n, P, K, W, comm, dev, arena=None):
     if world == 1:
         alg = 2 * n * P * 4
         kern_ms = ev[0].elapsed_time(ev[1]) / K
-        out["roofline"] = {"bound": "hbm", "kernel": "mean4_kernel<1, 4> (mx_mean_rows_to: 16-byte path, tree order)", "bytes_per_launch": alg,
+        kname = L.mx_mean_kernel_name(n, P, 0).decode()          # the dispatch mx_mean_rows_to launches
+        out["roofline"] = {"bound": "hbm", "kernel": f"{kname} (mx_mean_rows_to, tree order)", "bytes_per_launch": alg,
                            "avg_launch_ms": kern_ms, "achieved": alg / (kern_ms * 1e-3) / 1e9,
                            "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": alg / (kern_ms * 1e-3) / HBM_PEAK,
                            "note": "algorithmic bytes 2 x n x P x 4 (every row read once, the mean written to "
@@ -814,7 +847,13 @@ def er_figure(pkg, args, rank, world, comm, dev):
         g.close()
         del g
         torch.cuda.empty_cache()
-        row = {"budget": b, "rounds_per_s": Ker / el, "ms_per_round": 1e3 * el / Ker,
+        pred = None
+        if world > 1:
+            mix_est = float(np.mean(hbm)) / (HEADLINE_HBM_FRAC * HBM_PEAK)
+            pred = predict_round(chosen, world, float(np.mean(link)), mix_est, 2 * n_local * P * 4,
+                                 mix_source="this GPU's algorithmic HBM bytes at the headline kernel's 0.75 of 8 TB/s")
+            pred["achieved_over_predicted"] = pred["round_ms"] / (1e3 * el / Ker)
+        row = {"budget": b, "rounds_per_s": Ker / el, "ms_per_round": 1e3 * el / Ker, "predicted": pred,
                "mean_active_matchings": float(flags.sum(1).mean()), "skipped_rounds": int((flags.sum(1) == 0).sum()),
                "alpha": GPb.neighbor_weight, "slots_per_rank": slots,
                "hbm_TBps_rank0": (float(np.sum(hbm)) / el / 1e12) if world == 1 else None,
@@ -1246,6 +1285,18 @@ def run(args, world, rank, line, wd):
                        "note": "busiest GPU pair: bytes that cross it per round (one direction, and "
                                "both directions summed) / whole-job round time (exchange + mix), "
                                "against the 153 GB/s per-link figure of SURVEY.md §8d"}
+        # the expected round of every form, from its parts (achieved / predicted names the term that is off)
+        mix_s = float(np.median(mix_ms)) * 1e-3
+        mix_s = max_over_ranks(mix_s, world, dev)
+        pub = 2 * group.n_local * P * 4
+        chunks = overlap.get("chunks") if overlap and overlap.get("chunks") else 4
+        out["predicted"] = {f: predict_round(f, world, lb, mix_s, pub, chunks,
+                                             "mixing-alone launches of this run (max over ranks)")
+                            for f in ("rccl", "rccl_chunked", "pull")}
+        chosen_form = overlap.get("chosen_form") if overlap else "rccl"
+        pr = out["predicted"].get(chosen_form or "rccl")
+        out["predicted"]["timed_form"] = chosen_form or "rccl"
+        out["predicted"]["achieved_over_predicted"] = (pr["round_ms"] / (1e3 * round_s)) if pr else None
     wd.disarm()
     # self-check: every worker's sampled columns after every round the timed group ran vs the
     # oracle's rounds on the same columns from the synthetic initial values (checker, untimed)

@@ -227,7 +227,9 @@ size_t mx_topk_work_bytes(int64_t P);
  * "select_blocks" = select_kernel workgroups per row (0 = auto: the fewest whose LDS caches every
  * candidate region, at most 32); "select_trace" = 1: select_kernel stores stage clocks in the
  * scratch (diagnostic, tools/select_trace.py).
- * Knobs tune speed only, never results.
+ * Knobs tune speed only, never results -- except the test knob "spin_ticks": the bounded row-barrier
+ * waits' deadline in 100 MHz ticks (default 2^28, ~2.7 s); 0 makes every wait that has to wait
+ * expire, so tests can drive the error path below on purpose.
  * mx_topk_get also reads "hist_grid" (the last call's first-candidate-pass grid per row) and
  * "hist_capacity" (the co-resident block cap that grid was held to with sampling on, 0 without). */
 int mx_topk_set(const char* key, int64_t value);
@@ -237,6 +239,11 @@ int64_t mx_topk_get(const char* key);
  * that call's output undefined instead of hanging the GPU.  Synchronises `stream`, reads and clears
  * the words; MX_ERR_HIP if any was set.  (work, work_ld_bytes, nrows, P) as in the call checked. */
 int mx_topk_check(void* work, int64_t work_ld_bytes, int nrows, int64_t P, void* stream);
+/* The same scan, stream-ordered and NON-blocking: the words are read and cleared on `stream` behind
+ * the call they belong to, and an expired one sets *flag_dev = first row + 1 with a system-scope
+ * release (flag_dev: mx_host_words -- the host polls it without synchronising).  compressors.get_top_k
+ * on GPU tensors enqueues it after every call and raises at the next call, or at check_top_k(). */
+int mx_topk_err_forward(void* work, int64_t work_ld_bytes, int nrows, int64_t P, int32_t* flag_dev, void* stream);
 /* Diagnostics of the candidate floor, per row r: out[5r] = calls made on this scratch, out[5r+1] =
  * how many of them ran the fallback compaction (floor above the k-th key), out[5r+2] = the row's
  * current floor_hint margin (bins), out[5r+3] = the last call's threshold key (bits of |k-th value|),

@@ -82,6 +82,13 @@ def test_bench_multiprocess_path(nproc):
     assert (full["exchange_only_ms"] or 0) > 0 or er["form"] != "rccl"
     assert set(er["calib_ms"]) == {"rccl", "rccl_chunked", "pull"}
     assert len(out["xgmi"]["exchange_only_ms_per_rank"]) == nproc
+    # the expected round of every form from its parts: present and positive
+    pr = out["predicted"]
+    for f in ("rccl", "rccl_chunked", "pull"):
+        assert pr[f]["busiest_link_bytes"] > 0 and pr[f]["link_bound_ms"] > 0 and pr[f]["mix_ms"] > 0, pr[f]
+        assert pr[f]["fixed_ms"] > 0 and pr[f]["rounds_per_s"] > 0 and 0 < pr[f]["xgmi_frac"] < 1, pr[f]
+    assert pr["achieved_over_predicted"] > 0
+    assert all(b["predicted"]["rounds_per_s"] > 0 for b in er["sweep"] if b["predicted"]), er["sweep"]
 
 
 def test_bench_watchdog_line_on_hang():
@@ -246,4 +253,5 @@ def test_bench_single_gpu_line():
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["pickle"]["value"] > 0 and cb["pickle"]["cores"] >= 1
     ar = out["allreduce_baseline"]
     assert ar["parity_ok"] is True and 0 < ar["roofline"]["frac"] < 1 and out["rccl_ranks"] is None
+    assert ar["roofline"]["kernel"].startswith("mean_tile"), ar["roofline"]    # named from the dispatch
     assert out["choco"]["topk"]["fallback_compactions"] >= 0 and out["choco"]["topk"]["floor"] == "fine sampled"

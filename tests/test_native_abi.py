@@ -118,3 +118,21 @@ def test_mix_kernel_dispatch_names(pkg):
         assert pkg.lib.mx_mix_set(b"rows", 3) != 0
     finally:
         E.set_mix_tuning(**saved)
+
+
+def test_mean_rows_to_refuses_partial_overlap_and_names_kernels(pkg):
+    """a destination overlapping the rows at a column offset is refused before any
+    launch (host-side validation, fake device addresses); whole-row aliasing passes validation.
+    mx_mean_kernel_name follows the launch dispatch (the bench's centralized figure)."""
+    L = pkg.lib
+    base, ld, count = 1 << 40, 1024, 1000
+    rc = L.mx_mean_rows_to(base, 8, ld, count, 0, base + 4 * 16, 8, ld, None)   # 16 columns in
+    assert rc == -1 and b"column offset" in L.mx_last_error()
+    rc = L.mx_mean_rows_to(base, 8, ld, count, 0, base + 4 * (3 * ld + 5), 1, count, None)
+    assert rc == -1 and b"column offset" in L.mx_last_error()
+    assert L.mx_mean_kernel_name(8, 25_600_000, 0) == b"mean_tile_kernel<1>"
+    assert L.mx_mean_kernel_name(8, 25_600_000, 1) == b"mean_tile_kernel<0>"
+    assert L.mx_mean_kernel_name(8, 400, 0) == b"mean4_kernel<1, 4>"
+    assert L.mx_mean_kernel_name(16, 4096, 1) == b"mean4_kernel<0, 4>"
+    assert L.mx_mean_kernel_name(16, 4096, 0) == b"mean_to_kernel<float, 1, 64>"
+    assert L.mx_mean_kernel_name(65, 4096, 0) == b"mean_to_kernel<float, 2, 1>"
