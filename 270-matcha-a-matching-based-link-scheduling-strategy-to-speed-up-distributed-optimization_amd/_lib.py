@@ -40,6 +40,7 @@ SIGNATURES = {
     "mx_topk_check": (c_int, [c_p, c_i64, c_int, c_i64, c_p]),
     "mx_topk_err_forward": (c_int, [c_p, c_i64, c_int, c_i64, c_p, c_p]),
     "mx_topk_stats": (c_int, [c_p, c_i64, c_int, c_i64, c_p, c_p]),
+    "mx_topk_trace": (c_int, [c_p, c_i64]),
     "mx_topk_abs_diff": (c_int, [c_p, c_p, c_i64, c_i64, c_p, c_p, c_p, c_p]),
     "mx_topk_abs_diff_rows": (c_int, [c_p, c_p, c_i64, c_int, c_i64, c_i64, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_p]),
     "mx_choco_msg_bytes": (c_i64, [c_i64, c_i64]),

@@ -334,6 +334,16 @@ constexpr uint64_t kSpinTicks = 1ull << 28;    // ~2.7 s of the 100 MHz constant
 // the bounded waits' deadline (mx_topk_set "spin_ticks": a test knob -- 0 makes every wait that has
 // to wait at all expire, so the error path can be exercised on purpose)
 __device__ uint64_t g_spin_ticks_dev = kSpinTicks;
+// compaction trace (mx_topk_set "compact_trace" 1, diagnostic): per workgroup of the last one-row
+// compaction launch, the constant clock at its start, after its floor is resolved, and at its end
+constexpr int kTraceBlocks = 8192;
+__device__ uint64_t g_ctrace[kTraceBlocks * 3];
+__device__ int g_ctrace_on = 0;
+__device__ __forceinline__ void ctrace(int slot) {
+    const int b = blockIdx.x;
+    if (g_ctrace_on && threadIdx.x == 0 && blockIdx.y == 0 && b < kTraceBlocks)
+        g_ctrace[3 * b + slot] = (uint64_t)wall_clock64();
+}
 
 // block-uniform values the compiler cannot prove uniform (they come through LDS): into SGPRs
 __device__ __forceinline__ int uni(int x) { return __builtin_amdgcn_readfirstlane(x); }
@@ -526,6 +536,53 @@ __device__ uint32_t floor_key(const Rows& R, const RowView& v, int64_t S, double
     return (uint32_t)b << kTopShift;
 }
 
+// The same floor with its inputs loaded ahead (compact_run): the sampled histogram and every window
+// sub-bin are loaded BEFORE the first chunk's x / x_hat loads are issued.  Loads return in issue
+// order, so histogram loads issued after the chunk's (the old order) waited for its HBM latency, and
+// the window's sub-bins were a second dependent round trip after that: the block's floor was ready
+// ~4 us after its start, ~2 us after its first chunk (profiles/r05h_compact_trace.log).  Thread
+// (wave w, lane l) holds window slot w's sub-bin 63 - l (kTPB / 64 == kWinBins waves), so the
+// sub-bin is found by one wave scan instead of a second block-wide load and scan.
+static_assert(kTPB / 64 == kWinBins && kFineSub == 64, "one wave per window slot, one lane per sub-bin");
+#ifndef MX_FLOOR_EARLY
+#define MX_FLOOR_EARLY 1      // 0: the round-4 order (floor resolved after the first chunk's loads), for A/B builds
+#endif
+struct FloorIn {
+    Bins<kTopBins> hs;
+    uint32_t sub;
+};
+
+// (unconditional -- a branch here would join with register moves that wait for the loads; with the
+// floor hint (S = 0) the loaded bins are simply unused)
+__device__ __forceinline__ void floor_load(const RowView& v, FloorIn& fi) {
+    load_bins<kTopBins>(v.hs, fi.hs);
+    fi.sub = v.hsf[(threadIdx.x >> 6) * kFineSub + kFineSub - 1 - (threadIdx.x & 63)];
+}
+
+__device__ uint32_t floor_key_loaded(const Rows& R, const RowView& v, int64_t S, double frac, const FloorIn& fi) {
+    if (S == 0) return floor_key(R, v, S, frac);
+    const double e = (double)R.k * frac;
+    const int64_t want = S > 1 ? (int64_t)ceil(1.25 * e + 4.0 * sqrt(e) + 16.0) : R.k;
+    int b;
+    int64_t rem, tot;
+    scan_bins<kTopBins>(fi.hs, want, &b, &rem, &tot);
+    if (tot < want) return 0u;                              // too few sampled keys: keep everything
+    const int w0 = fine_window(R, v);                       // block-uniform
+    if (w0 >= 0 && b >= w0 && b < w0 + kWinBins) {
+        __shared__ int s_sb;
+        if (threadIdx.x == 0) s_sb = -1;
+        __syncthreads();
+        if ((int)(threadIdx.x >> 6) == b - w0) {             // wave-uniform
+            const int64_t incl = wave_incl_scan64((int64_t)fi.sub);
+            if (incl - (int64_t)fi.sub < rem && incl >= rem) s_sb = kFineSub - 1 - (int)(threadIdx.x & 63);
+        }
+        __syncthreads();
+        const int sb = s_sb;
+        if (sb >= 0) return ((uint32_t)b << kTopShift) | ((uint32_t)sb << kFineShift);
+    }
+    return (uint32_t)b << kTopShift;
+}
+
 // After the threshold pass resolved T (one thread per row): the next call's floor hint, the margin
 // adapted (a fallback widens it by 4 bins, a candidate set above 4 k narrows it by one), counts.
 // cn = this call's candidate count (keys kept by the first compaction).
@@ -565,6 +622,9 @@ __device__ void compact_run(const Rows& R, const RowView& v, int64_t S, double f
         }
     };
     auto issue = [&](int64_t c) { issue_to(ax, ah, c); };
+    if (!fallback) ctrace(0);
+    FloorIn fi;
+    if (MX_FLOOR_EARLY && !fallback) floor_load(v, fi);   // ahead of the chunk loads (floor_key_loaded)
     int64_t c = bx;
     if (c < nc && whole(c)) issue(c);              // the first chunk flies while b_lo is resolved
     if constexpr (PF2) {
@@ -573,13 +633,14 @@ __device__ void compact_run(const Rows& R, const RowView& v, int64_t S, double f
 
     uint32_t b_lo = 0, fkey = 0;                   // floor: keys >= fkey (digit b_lo) are kept
     if (!fallback) {
-        fkey = floor_key(R, v, S, frac);
+        fkey = MX_FLOOR_EARLY ? floor_key_loaded(R, v, S, frac, fi) : floor_key(R, v, S, frac);
         b_lo = fkey >> kTopShift;
         if (bx == 0 && threadIdx.x == 0) {
             v.st->b0 = b_lo;
             v.st->bar = 0;                                  // the selection's row barriers start here
         }
     }
+    if (!fallback) ctrace(1);
     // only digits >= b_lo are ever counted: zero and flush just those bins (b_lo is near the top)
     const int h0 = (int)(b_lo & ~(uint32_t)(kTPB - 1));
     for (int i = h0 + threadIdx.x; i < kTopBins; i += kTPB) h[i] = 0;
@@ -721,6 +782,7 @@ __device__ void compact_run(const Rows& R, const RowView& v, int64_t S, double f
     for (int i = h0 + threadIdx.x; i < kTopBins; i += kTPB)
         if (h[i]) atomicAdd(&out[i], h[i]);
     if (!fallback && threadIdx.x == 0 && kept) atomicAdd(&v.st->cand_n, (unsigned long long)kept);
+    if (!fallback) ctrace(2);
 }
 
 template <bool BAL, bool LOOP, bool PF2 = false>
@@ -1838,6 +1900,7 @@ unsigned clamp_grid(int64_t n, int64_t per, int64_t cap) {
 
 int g_sample_stride = 0;   // 0 = auto (about kSampleTarget sampled elements per row)
 uint64_t g_spin_ticks_host = kSpinTicks;   // host copy of g_spin_ticks_dev (mx_topk_get)
+int g_compact_trace = 0;                   // host copy of g_ctrace_on
 int g_compact_blocks = 0;     // persistent compaction blocks over all rows; 0 = auto: ~720 for one
                               // row (an even chunk count each), 2560 for several (same-box sweeps: one row 256 / 384 / 512 / 640 /
                               // 1024 / 2048 blocks 131 / 121 / 116.4 / 116.2 / 119 / 134 us per round,
@@ -1992,6 +2055,12 @@ extern "C" int mx_topk_set(const char* key, int64_t value) {
         g_select_blocks = (int)value;
         return MX_OK;
     }
+    if (!strcmp(key, "compact_trace")) {
+        const int on = value != 0;
+        MX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_ctrace_on), &on, sizeof(on)));
+        g_compact_trace = on;
+        return MX_OK;
+    }
     if (!strcmp(key, "spin_ticks")) {
         MX_CHECK(value >= 0, "mx_topk_set: spin_ticks %lld", (long long)value);
         const uint64_t v = (uint64_t)value;
@@ -2009,6 +2078,7 @@ extern "C" int mx_topk_set(const char* key, int64_t value) {
 
 extern "C" int64_t mx_topk_get(const char* key) {
     if (key && !strcmp(key, "spin_ticks")) return (int64_t)g_spin_ticks_host;
+    if (key && !strcmp(key, "compact_trace")) return g_compact_trace;
     if (key && !strcmp(key, "sample_stride")) return g_sample_stride;
     if (key && !strcmp(key, "compact_blocks")) return g_compact_blocks;
     if (key && !strcmp(key, "sample_pieces")) return g_sample_pieces;
@@ -2190,6 +2260,15 @@ extern "C" int mx_topk_err_forward(void* work, int64_t work_ld_bytes, int nrows,
                  (nrows == 1 || work_ld_bytes >= (int64_t)layout(P).total),
              "mx_topk_err_forward: bad arguments");
     return launch_err_scan(work, work_ld_bytes, nrows, P, flag_dev, mx::as_stream(stream));
+}
+
+// The compaction trace (mx_topk_set "compact_trace" 1): n <= 8192 workgroups x {start, floor
+// resolved, end} constant-clock stamps of the last traced launch (row 0's blocks).  Synchronises.
+extern "C" int mx_topk_trace(uint64_t* out, int64_t nblocks) {
+    MX_CHECK(out && nblocks >= 1 && nblocks <= kTraceBlocks, "mx_topk_trace: nblocks %lld", (long long)nblocks);
+    MX_HIP(hipDeviceSynchronize());
+    MX_HIP(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ctrace), (size_t)nblocks * 3 * sizeof(uint64_t)));
+    return MX_OK;
 }
 
 // Per row: {calls, fallback compactions, current floor-hint margin, the last call's threshold key T,

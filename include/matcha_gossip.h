@@ -249,6 +249,11 @@ int mx_topk_err_forward(void* work, int64_t work_ld_bytes, int nrows, int64_t P,
  * current floor_hint margin (bins), out[5r+3] = the last call's threshold key (bits of |k-th value|),
  * out[5r+4] = its candidate count.  Synchronises `stream`. */
 int mx_topk_stats(const void* work, int64_t work_ld_bytes, int nrows, int64_t P, int64_t* out, void* stream);
+/* Diagnostic: with mx_topk_set("compact_trace", 1), every workgroup of row 0's candidate compaction
+ * stamps the 100 MHz constant clock at its start, once its floor is resolved, and at its end;
+ * out[3b .. 3b+2] = workgroup b's stamps of the last launch (nblocks <= 8192).  Synchronises the
+ * device.  tools/compact_trace.py reads it (ramp vs tail of the one-row compaction). */
+int mx_topk_trace(uint64_t* out, int64_t nblocks);
 int mx_topk_abs_diff(const float* x, const float* x_hat, int64_t P, int64_t k, float* vals,
                      int64_t* idx, void* work, void* stream);
 /* Batched form (one set of launches for every local worker): row r reads x + r*ld (and

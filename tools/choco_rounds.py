@@ -1,5 +1,7 @@
 """K Choco rounds of one group (CHOCO_GROUP = rows8: 8 rows on one GPU; row1: one row, a rank's
-share at N = 8 with a null transport) -- a short fixed workload for rocprofv3 kernel traces."""
+share at N = 8 with a null transport) -- a short fixed workload for rocprofv3 kernel traces; prints
+the per-round HIP-event median / min (us) of the last K - 5 rounds as one JSON line (same-box A/B
+of library builds through MX_GOSSIP_LIB)."""
 import importlib
 import os
 import sys
@@ -32,7 +34,17 @@ else:
 for kv in filter(None, os.environ.get("TOPK_SET", "").split(":")):     # e.g. TOPK_SET=select=1:select_blocks=32
     k_, v_ = kv.split("=")
     pkg._lib.check(pkg.lib.mx_topk_set(k_.encode(), int(v_)))
+import json  # noqa: E402
+ev = []
 for it in range(K):
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
     c.step(it)
+    b.record()
+    ev.append((a, b))
 torch.cuda.synchronize()
-print("done", K)
+us = sorted(1e3 * a.elapsed_time(b) for a, b in ev[5:])
+print(json.dumps({"group": os.environ.get("CHOCO_GROUP", "row1"), "lib": os.environ.get("MX_GOSSIP_LIB") or "tree",
+                  "topk_set": os.environ.get("TOPK_SET", ""),
+                  "rounds": len(us), "round_us_median": round(us[len(us) // 2], 2), "round_us_min": round(us[0], 2)}),
+      flush=True)
