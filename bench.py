@@ -1142,7 +1142,7 @@ def run(args, world, rank, line, wd):
         overlap = {"pull_unavailable": pull_err}
     # per-round HIP events of the whole round (diagnostic): real rounds run BEFORE the timed region,
     # in blocks of K, for at least --settle-ms (an idle MI355X takes ~10 ms of streaming to reach
-    # its steady clocks: tools/ramp.py), so the timed rounds measure the steady state of the loop
+    # its steady clocks: profiles/r02_clock_ramp.log), so the timed rounds measure the steady state of the loop
     step_ms = []
     it = W
     t_settle = time.perf_counter()
