@@ -98,6 +98,10 @@ class ChocoWorkerGroup:
                                         self.bnd_off, self.work.data_ptr(), self.work_ld, stream_ptr(stream)),
               "mx_topk_abs_diff_rows")
 
+    def wait_round(self, stream=None):
+        """The end of a round for communicate(): the transport's wait (engine.wait_round)."""
+        wait_round(self.engine.comm, stream)
+
     def check_topk(self, stream=None):
         """Synchronise and raise MXError if a top-k row barrier's bounded wait expired since the
         last check (mx_topk_check: that round's messages are undefined; never a GPU hang)."""
