@@ -40,11 +40,13 @@ XGMI_LINK_PEAK = 153e9     # bytes/s per direction per link
 METRIC = "gossip rounds/sec (8 workers x 25.6M fp32 params, graph 0, full MATCHA round)"
 # Fixed per-round cost of each N > 1 exchange form (seconds), for the `predicted` object.  pull:
 # measured with tools/form_overhead.py at P = 100k, N processes sharing one GPU (profiles/
-# r05b_pull_overhead_after_n*.log: snapshot publish + gate + mix launches, device gate).  RCCL
-# forms: not measurable on a one-GPU box (RCCL refuses two ranks on one device) -- ASSUMED one
-# grouped send/recv launch (~25 us) per exchange, one per chunk for the pipelined form.
+# r05b_pull_overhead_after_n*.log: snapshot publish + gate + mix launches, device gate).  RCCL:
+# a cross-GPU group cannot run on a one-GPU box (RCCL refuses two ranks on one device); its floor
+# is measured with a one-rank self send + receive in one group, back to back (tools/
+# rccl_overhead.py, profiles/r05m_rccl_overhead.log: 7.3 us for 4 KB - 1.8 MB) -- a LOWER bound of a
+# cross-GPU group's cost, one per exchange (one per chunk for the pipelined form).
 PULL_FIXED_S = {2: 26e-6, 4: 31e-6, 8: 62e-6}
-RCCL_FIXED_S = 25e-6
+RCCL_FIXED_S = 7.3e-6
 HEADLINE_HBM_FRAC = 0.75   # the mixing kernel's measured fraction of 8 TB/s (BENCH_r04, profiles/)
 
 
@@ -392,7 +394,7 @@ def round_bytes(partner, owner, flags_rows, rank, row_base, n_local, P):
 def predict_round(form, world, link_bytes, mix_s, publish_bytes, chunks=4, mix_source="measured"):
     """What a round of `form` should cost at N = world, from its parts: the busiest
     xGMI link's bytes at 153 GB/s, the mixing kernel on this GPU (mix_s), the form's fixed cost
-    (PULL_FIXED_S measured / RCCL_FIXED_S assumed) and, for pull, the snapshot copy at the headline's
+    (PULL_FIXED_S measured / RCCL_FIXED_S a measured lower bound) and, for pull, the snapshot copy at the headline's
     HBM fraction.  plain RCCL: exchange, then mix (one stream); pipelined: the longer of the two
     plus one chunk of the shorter; pull: publish, then the mix reading partners over xGMI."""
     t_link = link_bytes / XGMI_LINK_PEAK
@@ -402,10 +404,10 @@ def predict_round(form, world, link_bytes, mix_s, publish_bytes, chunks=4, mix_s
         t_pub = publish_bytes / (HEADLINE_HBM_FRAC * HBM_PEAK)
         t = t_pub + max(t_link, mix_s) + fixed
     elif form == "rccl_chunked":
-        fixed, src, t_pub = chunks * RCCL_FIXED_S, "assumed (no two-GPU RCCL run yet)", 0.0
+        fixed, src, t_pub = chunks * RCCL_FIXED_S, "lower bound: one-rank RCCL self-exchange (tools/rccl_overhead.py)", 0.0
         t = max(t_link, mix_s) + min(t_link, mix_s) / chunks + fixed
     else:
-        fixed, src, t_pub = RCCL_FIXED_S, "assumed (no two-GPU RCCL run yet)", 0.0
+        fixed, src, t_pub = RCCL_FIXED_S, "lower bound: one-rank RCCL self-exchange (tools/rccl_overhead.py)", 0.0
         t = t_link + mix_s + fixed
     return {"busiest_link_bytes": float(link_bytes), "link_bound_ms": 1e3 * t_link, "mix_ms": 1e3 * mix_s,
             "mix_source": mix_source, "publish_ms": 1e3 * t_pub, "fixed_ms": 1e3 * fixed, "fixed_source": src,
