@@ -62,6 +62,40 @@ def decen_case(pkg, T, gid, P, rounds, chunk_cols=None, seed=5, placement=None, 
     return bool(np.array_equal(got.view(np.uint32), X.view(np.uint32)))
 
 
+def pull_rows_case(pkg, gid, P, rounds, seed=21, placement=None):
+    """The reference's averaging(active_flags) with arbitrary rows under the pull transport: each
+    round's row is drawn at random (the same on every rank), its plan record found or built by
+    engine.record_for (a schedule iteration with the same row, else the scratch record -- then the
+    gate reads the scratch row), and the rounds enqueued back to back with no host wait; every
+    worker's row vs the oracle at the end."""
+    rank, world = dist.get_rank(), dist.get_world_size()
+    n = pkg.GRAPH_SIZES[gid]
+    gp = pkg.GraphProcessor(pkg.select_graph(gid), 1.0, 0, n, 4, True)
+    M = len(gp.neighbors_info)
+    sched = np.zeros((3, M), np.uint8)
+    sched[0] = 1
+    sched[1, ::2] = 1
+    topo = Topo(gp.neighbors_info, 0.19, sched)
+    grp = pkg.VirtualWorkerGroup(topo, numel=P, rank=rank, nranks=world, comm=pkg.PullTransport(), placement=placement)
+    X = np.stack([O.synth(500 + i, P) for i in range(n)])
+    grp.rows.copy_(torch.from_numpy(X[grp.workers]))
+    rng = np.random.RandomState(seed)
+    adhoc = 0
+    for _ in range(rounds):
+        f = (rng.uniform(size=M) < 0.5).astype(np.uint8)
+        if rng.uniform() < 0.3:
+            f = sched[rng.randint(2)].copy()
+        it = grp.engine.record_for(f)
+        adhoc += it == grp.engine.T
+        if f.any():
+            grp.step(it)
+            X = O.decen_round(X, topo.neighbors_info, f, 0.19)
+    grp.wait_round()
+    got = by_worker(grp, gather_rows(grp.rows, grp.row_base, n))
+    grp.close()
+    return bool(np.array_equal(got.view(np.uint32), X.view(np.uint32))) and adhoc > 0
+
+
 def choco_case(pkg, T, P, ratio, rounds, seed=9, placement=None):
     rank, world = dist.get_rank(), dist.get_world_size()
     n = 8
@@ -135,6 +169,7 @@ def main():
         "decen_g2_pull_placed": decen_case(pkg, pkg.PullTransport(), 2, 9_001, 5, placement="auto"),
         # 40 device-gated rounds (no host barrier per round): each snapshot buffer reused 20 times
         "decen_g0_pull_long": decen_case(pkg, pkg.PullTransport(), 0, 30_011, 40, seed=11, back_to_back=True),
+        "decen_g2_pull_rows_placed": pull_rows_case(pkg, 2, 12_007, 24, placement="auto"),
     }
     torch.cuda.synchronize()
     if dist.get_rank() == 0:
