@@ -46,6 +46,7 @@ METRIC = "gossip rounds/sec (8 workers x 25.6M fp32 params, graph 0, full MATCHA
 # rccl_overhead.py, profiles/r05m_rccl_overhead.log: 7.3 us for 4 KB - 1.8 MB) -- a LOWER bound of a
 # cross-GPU group's cost, one per exchange (one per chunk for the pipelined form).
 PULL_FIXED_S = {2: 26e-6, 4: 31e-6, 8: 62e-6}
+PULL_TIMEOUT_S = 20.0      # the pull gate's deadline in the bench (lockstep rounds of at most a few ms)
 RCCL_FIXED_S = 7.3e-6
 HEADLINE_HBM_FRAC = 0.75   # the mixing kernel's measured fraction of 8 TB/s (BENCH_r04, profiles/)
 
@@ -801,7 +802,7 @@ def er_figure(pkg, args, rank, world, comm, dev):
         elif form == "rccl_chunked":
             g = pkg.VirtualWorkerGroup(GPb, comm=comm, chunk_cols=((P + 3) // 4 + 63) // 64 * 64, **kw)
         elif form == "pull":
-            g = pkg.VirtualWorkerGroup(GPb, comm=pkg.PullTransport(), **kw)
+            g = pkg.VirtualWorkerGroup(GPb, comm=pkg.PullTransport(timeout_s=PULL_TIMEOUT_S), **kw)
         else:
             g = pkg.VirtualWorkerGroup(GPb, **kw)
         fill_synth(pkg, g)
@@ -1108,15 +1109,24 @@ def run(args, world, rank, line, wd):
     if any_remote and args.pull != "off":
         # the pull transport: partner rows read straight from the peers' HBM (IPC-mapped
         # snapshots) by the mixing kernel -- no RCCL copies; collective setup, all ranks agree
+        # (bench rounds run in lockstep: a device gate that waits PULL_TIMEOUT_S has met a fault,
+        # not a slow peer -- the form is then dropped on EVERY rank, so the forms stay in step)
+        gpull = None
         try:
-            gpull = pkg.VirtualWorkerGroup(GP, numel=P, rank=rank, nranks=world, comm=pkg.PullTransport(),
-                                           placement=args.placement)
+            gpull = pkg.VirtualWorkerGroup(GP, numel=P, rank=rank, nranks=world,
+                                           comm=pkg.PullTransport(timeout_s=PULL_TIMEOUT_S), placement=args.placement)
             fill_synth(pkg, gpull)
             for it in range(W):
                 run(gpull, it)
-            forms["pull"] = gpull
+            gpull.wait_round()                   # a gate that expired in the warmup raises here
         except pkg.MXError as e:
             pull_err = str(e)
+        if gpull is not None:                    # bound on every rank (bind is all-or-nothing)
+            if max_over_ranks(float(pull_err is not None), world, dev) > 0:
+                pull_err = pull_err or "a peer's pull warmup failed"
+                gpull.close()
+            else:
+                forms["pull"] = gpull
     if len(forms) > 1:
         # every form runs R untimed rounds; the fastest (max over ranks, so every rank picks the
         # same) is the one timed -- unless one is forced (--overlap on / --pull on)
@@ -1179,6 +1189,7 @@ def run(args, world, rank, line, wd):
         # rounds the pull group ran on its two alternating snapshot buffers (each reused >= 3 times
         # when this is >= 6); parity_ok below covers every one of them
         overlap["pull_rounds"] = int(timed._pull.round)
+        overlap["pull_gate_error"] = timed._pull.error()   # an expired device wait (None: every gate passed)
     final_cols = gather_columns(timed, cols_dev, world, dev)
     # mixing kernel alone (N > 1: without the RCCL exchange, so rows go stale) -> its HBM roofline
     stream = torch.cuda.current_stream()

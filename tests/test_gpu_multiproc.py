@@ -126,6 +126,7 @@ def test_bench_multiprocess_overlap_forms(nproc, overlap, pull):
         # (a stale line of round r - 2 would break parity_ok)
         assert out["overlap"]["chosen_form"] == "pull" and out["overlap"]["pull_unavailable"] is None
         assert out["overlap"]["pull_rounds"] >= 6, out["overlap"]
+        assert out["overlap"]["pull_gate_error"] is None, out["overlap"]
     elif overlap == "off" and pull == "off":
         assert out["overlap"] is None
     else:
