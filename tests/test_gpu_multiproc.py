@@ -230,6 +230,18 @@ def test_rccl_peer_skips_exchange():
     assert 2.5 <= out["seconds"] < 30, out
 
 
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs (one RCCL rank each)")
+def test_cross_gpu_transports_match_oracle():
+    """One rank per GPU (2-4 GPUs): RCCL plain / pipelined exchange, Choco messages, the ordered
+    all-reduce, and the pull transport's device gate with snapshots on other GPUs (the cross-L2
+    coherence protocol), every worker's row bit-exact vs the oracle.  Skipped on a one-GPU box."""
+    n = min(4, torch.cuda.device_count())
+    r = _torchrun(n, [os.path.join(HERE, "mp_gpus.py")], timeout=280)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert res["world"] == n and all(v for k, v in res.items() if k != "world"), res
+
+
 def test_bench_single_gpu_line():
     """bench.py at N = 1 (headline shape, few rounds): the line's contract fields, the self-check,
     the per-round event statistics, the config and host-model figures and the CPU baseline legs."""
