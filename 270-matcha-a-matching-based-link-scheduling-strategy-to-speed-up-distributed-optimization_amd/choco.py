@@ -5,6 +5,12 @@ persistent Choco state x_hat and s (all [n_local, P] in HBM).  Per round:
     q_r = top-k(|x_r - x_hat_r|)            mx_topk_abs_diff   (prepare_comm_buffer, 175-196)
     [N > 1] RCCL exchange of the messages   mx_exchange_round  (12 k bytes per edge direction)
     s / x_hat updates + dense x update      mx_choco_apply     (averaging, 200-230; one fused pass)
+Under PullTransport (N > 1, one process per GPU of a node) the messages are not sent: every rank
+publishes its rows' messages into its IPC-shared snapshot buffer (mx_snapshot_publish), the device
+gate (mx_pull_gate) waits for the partners' epochs and points the receive slots of a device slot
+table at their snapshots, and the apply pass reads the partners' messages from the owners' HBM
+(mx_choco_apply_slots) -- four launches per round and no host step, as VirtualWorkerGroup's pull
+round (engine.PullTransport).
 """
 import time
 
@@ -12,7 +18,9 @@ import numpy as np
 import torch
 
 from ._lib import check, lib, require_device, stream_ptr
-from .engine import GossipEngine, PullTransport, ROW_ALIGN, default_comm, owner_table, partition, wait_round
+from ._lib import MXError
+from .engine import (PULL_HEADER, GossipEngine, PullTransport, ROW_ALIGN, default_comm, owner_table, partition,
+                     wait_round)
 
 
 def topk_count(P, ratio):
@@ -33,9 +41,6 @@ class ChocoWorkerGroup:
         self.workers = block_workers(self.placement, self.row_base, self.n_local)
         if nranks > 1 and comm is None:
             comm = default_comm()
-        if isinstance(comm, PullTransport):
-            raise TypeError("ChocoWorkerGroup: PullTransport carries whole-row rounds only "
-                            "(VirtualWorkerGroup); Choco messages need the RCCL transport")
         self.engine = GossipEngine(topology, self.row_base, self.n_local, comm=comm,
                                    owner=owner_table(n, nranks))
         self.topology = topology
@@ -78,6 +83,18 @@ class ChocoWorkerGroup:
                                       dtype=torch.uint8, device="cuda")
         self.gamma32 = float(np.float32(consensus_lr))
         self.iter_dev = torch.zeros(1, dtype=torch.int64, device="cuda")   # device_round's counter
+        self._pull = None
+        if isinstance(comm, PullTransport):
+            # each rank's snapshot buffer holds two generations of its rows' messages; the apply
+            # reads message `slot` at slot_ptrs[slot]: local slots here, remote ones set per round
+            # by the gate to the partners' snapshots (placeholder: this rank's own snapshot 0)
+            self._pull = comm.bind(self, row_bytes=self.msg_ld)
+            ptrs = [self.msgs.data_ptr() + r * self.msg_ld for r in range(self.n_local)]
+            ptrs += [self._pull.own + PULL_HEADER] * (self.engine.n_slots - self.n_local)
+            self.slot_ptrs = torch.tensor(ptrs, dtype=torch.int64, device="cuda")
+            check(lib.mx_plan_set_peer_reads(self.engine.plan.data_ptr(), self.engine.T + 1, self.n_local,
+                                             self.engine.M, 1, stream_ptr()), "mx_plan_set_peer_reads")
+            self.engine.peer_reads = True
 
     @property
     def rows(self):
@@ -99,8 +116,28 @@ class ChocoWorkerGroup:
               "mx_topk_abs_diff_rows")
 
     def wait_round(self, stream=None):
-        """The end of a round for communicate(): the transport's wait (engine.wait_round)."""
+        """The end of a round for communicate(): the transport's wait (engine.wait_round), then
+        the pull gate's sticky error, if any, as MXError."""
         wait_round(self.engine.comm, stream)
+        if self._pull is not None:
+            msg = self._pull.error()
+            if msg:
+                raise MXError(msg)
+
+    @property
+    def pulls(self):
+        """True when partner messages are read from the peers' IPC-mapped snapshots (PullTransport)."""
+        return self._pull is not None
+
+    def close(self):
+        """Release the pull transport's shared buffers; COLLECTIVE under PullTransport (as
+        VirtualWorkerGroup.close: a barrier after this rank's last apply, then unmap and free)."""
+        if self._pull is not None:
+            import torch.distributed as dist
+            torch.cuda.synchronize()
+            dist.barrier(group=self._pull.transport.group)
+            self._pull.close()
+            self._pull = None
 
     def check_topk(self, stream=None):
         """Synchronise and raise MXError if a top-k row barrier's bounded wait expired since the
@@ -113,6 +150,8 @@ class ChocoWorkerGroup:
         transport into the message slots after the local ones), then the s / x_hat scatters and
         the dense x update."""
         it = self.engine.round_index(it)         # mx_choco_apply indexes the plan table by `it`
+        if self._pull is not None:
+            return self._average_pull(it, stream)
         mbase = self.msgs.data_ptr()
         if self.engine.comm is not None:
             self.engine.exchange(it, [mbase + r * self.msg_ld for r in range(self.n_local)],
@@ -122,6 +161,32 @@ class ChocoWorkerGroup:
                                  self.engine.plan.data_ptr(), int(it), self.n_local, self.engine.M,
                                  self.engine.alpha32, self.gamma32, self.apply_work.data_ptr(),
                                  stream_ptr(stream)), "mx_choco_apply")
+
+    def _average_pull(self, it, stream=None):
+        """PullTransport averaging, three launches and no host wait: the local messages into
+        snapshot `round % 2` (system-scope release per workgroup), the gate (this rank's epoch out,
+        bounded waits for the partners', remote slots -> their snapshots), the apply reading the
+        partners' messages from their owners' HBM.  A gate that expired earlier raises here."""
+        st = self._pull
+        msg = st.error()
+        if msg:
+            raise MXError(msg)
+        eng = self.engine
+        par = st.round & 1
+        st.round += 1
+        s = stream_ptr(stream)
+        check(lib.mx_snapshot_publish(self.msgs.data_ptr(), st.own + PULL_HEADER + par * st.half,
+                                      self.n_local * self.msg_ld // 4, s), "mx_snapshot_publish")
+        frow = (eng._adhoc_flags.data_ptr() if it == eng.T else eng.flags_dev.data_ptr() + it * eng.M)
+        tr = st.transport
+        check(lib.mx_pull_gate(frow, st.prev_row.data_ptr(), eng.M, eng.partner_dev.data_ptr(), eng.n,
+                               st.owner_dev.data_ptr(), st.ranks_dev.data_ptr(), tr.nranks, tr.rank, self.row_base,
+                               self.n_local, self.msg_ld, par, st.round, self.slot_ptrs.data_ptr(), eng.n_slots,
+                               tr.timeout_s, st.err_dev, s), "mx_pull_gate")
+        check(lib.mx_choco_apply_slots(self.x.data_ptr(), self.x_hat.data_ptr(), self.s.data_ptr(), self.ld,
+                                       self.numel, self.k, self.slot_ptrs.data_ptr(), eng.n_slots,
+                                       eng.plan.data_ptr(), int(it), self.n_local, eng.M, eng.alpha32, self.gamma32,
+                                       s), "mx_choco_apply_slots")
 
     def device_round(self, stream=None):
         """Graph-replayable round at the device counter `self.iter_dev` (then advanced): top-k of
@@ -176,7 +241,7 @@ class ChocoWorkerGroup:
         torch.cuda.synchronize()
         tic = time.time()
         self.step(it)
-        wait_round(self.engine.comm)
+        self.wait_round()
         toc = time.time()
         self.check_topk()
         return toc - tic

@@ -203,12 +203,12 @@ class _Staging:
 
 
 def _refuse_pull(transport, who):
-    """The pull transport serves whole-row gossip only (VirtualWorkerGroup): Choco messages and
-    the centralized all-gather need a transport that moves buffers."""
+    """The pull transport serves gossip rounds (decenCommunicator / ChocoCommunicator): the
+    centralized all-gather needs a transport that moves buffers."""
     from .engine import PullTransport
     if isinstance(transport, PullTransport):
-        raise TypeError(f"{who}: PullTransport carries decentralized whole-row rounds only "
-                        "(decenCommunicator / VirtualWorkerGroup); use the RCCL transport (transport=None)")
+        raise TypeError(f"{who}: PullTransport carries gossip rounds only (decenCommunicator / "
+                        "ChocoCommunicator); use the RCCL transport (transport=None)")
 
 
 class Communicator(object):
@@ -362,7 +362,6 @@ class ChocoCommunicator(Communicator):
     """communicator.py:161-268 -- top-k compressed gossip with persistent x_hat / s."""
 
     def __init__(self, rank, size, topology, ratio, consensus_lr, *, transport=None):
-        _refuse_pull(transport, "ChocoCommunicator")
         super(ChocoCommunicator, self).__init__(rank, size, transport=transport)
         self.topology = topology
         self.neighbor_weight = topology.neighbor_weight
@@ -454,7 +453,7 @@ class ChocoCommunicator(Communicator):
         torch.cuda.synchronize()
         tic = time.time()
         self._group.average(it)
-        wait_round(self._group.engine.comm)
+        self._group.wait_round()
         toc = time.time()
         return toc - tic
 
@@ -463,9 +462,19 @@ class ChocoCommunicator(Communicator):
         self._list_stage.store()
 
     def close(self):
+        """Release the worker group (collective under PullTransport, as decenCommunicator.close)."""
+        if self._group is not None:
+            self._group.close()
         self._group = None
         self._stage = None
         self._model_params = None
+
+    def __del__(self):
+        try:
+            if self._group is not None and not self._group.pulls:
+                self.close()
+        except Exception:                        # interpreter teardown: nothing left to release
+            pass
 
 
 ORDERS = {"tree": 0, "sequential": 1}

@@ -1635,10 +1635,29 @@ struct Msg {
 };
 
 // message layout (mx_choco_msg_bytes): vals f32[kpad] | idx int64[k] | bnd int32[ntiles + 1]
+// SP = false: message `slot` at msgs + slot * msg_ld (one buffer); SP = true (mx_choco_apply_slots,
+// the pull transport): `msgs` is a device table of int64 message addresses, one per slot -- the
+// local rows' messages here, the partners' in their owners' IPC-mapped snapshot buffers
+template <bool SP>
 __device__ __forceinline__ Msg msg_at(const char* msgs, int64_t msg_ld, int64_t kpad, int64_t k, int slot) {
-    const char* b = msgs + (int64_t)slot * msg_ld;
+    const char* b = SP ? reinterpret_cast<const char*>(reinterpret_cast<const int64_t*>(msgs)[slot])
+                       : msgs + (int64_t)slot * msg_ld;
     return Msg{reinterpret_cast<const float*>(b), reinterpret_cast<const int64_t*>(b + 4 * kpad),
                reinterpret_cast<const int32_t*>(b + 4 * kpad + 8 * k)};
+}
+
+// Pull transport (plan word [2] bit 1, mx_plan_set_peer_reads): the partner messages are read from
+// peers' IPC-mapped snapshot buffers, which this GPU's L2 may hold as non-local lines from two rounds
+// ago.  One system-scope acquire per workgroup before its first message load -- the same protocol
+// as the mixing kernels' peer_acquire (mix.hip); block-uniform, nothing for rounds without it.
+__device__ __forceinline__ void peer_acquire(int32_t mode_word) {
+    if (mode_word & 2) {
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");       // system scope: buffer_inv sc0 sc1
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+    }
 }
 
 // The plan record of this round: `rec` itself, or with iter_dev (graph-replayable launches) the
@@ -1661,7 +1680,7 @@ __device__ __forceinline__ const int32_t* round_rec(const int32_t* rec, const in
 // GRAN: floats per dirty granule of s / x_hat written back.  16 (64 B) is the one instantiated: 32-B
 // granules measured 8 rows 639 -> 715 us per round (same-box A/B; partial non-temporal line writes),
 // one row unchanged
-template <bool NT, int GRAN>
+template <bool NT, int GRAN, bool SP>
 __device__ __forceinline__ void apply_tile(float* __restrict__ x, float* __restrict__ xh, float* __restrict__ s,
                                            int64_t ld, int64_t P, const char* __restrict__ msgs, int64_t msg_ld,
                                            int64_t kpad, int64_t k, const int32_t* __restrict__ rec, int n_local,
@@ -1699,7 +1718,7 @@ __device__ __forceinline__ void apply_tile(float* __restrict__ x, float* __restr
     const int d = deg[r];
     const int32_t* src = deg + 2 * n_local + r * M;
     for (int e = 0; e < d; ++e) {              // partners, ascending matching order
-        const Msg m = msg_at(msgs, msg_ld, kpad, k, src[e]);
+        const Msg m = msg_at<SP>(msgs, msg_ld, kpad, k, src[e]);
         const int lo = max(m.bnd[t], 0), hi = min(m.bnd[t + 1], (int)k);   // clamped: a received
         for (int q = lo + tid; q < hi; q += kTPB) {                        // message is not trusted
             const int c = (int)(m.ix[q] - t0);                             // to stay in range
@@ -1711,7 +1730,7 @@ __device__ __forceinline__ void apply_tile(float* __restrict__ x, float* __restr
     }
     {                                          // own message
         const float sw = __int_as_float(deg[n_local + r]);
-        const Msg m = msg_at(msgs, msg_ld, kpad, k, r);
+        const Msg m = msg_at<SP>(msgs, msg_ld, kpad, k, r);
         const int lo = max(m.bnd[t], 0), hi = min(m.bnd[t + 1], (int)k);
         for (int q = lo + tid; q < hi; q += kTPB) {
             const int c = (int)(m.ix[q] - t0);
@@ -1746,7 +1765,7 @@ __device__ __forceinline__ void apply_tile(float* __restrict__ x, float* __restr
     }
 }
 
-template <bool NT, int GRAN>
+template <bool NT, int GRAN, bool SP>
 __global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, float* __restrict__ xh,
                                                      float* __restrict__ s, int64_t ld, int64_t P,
                                                      const char* __restrict__ msgs, int64_t msg_ld,
@@ -1757,9 +1776,10 @@ __global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, floa
                                                      float alpha, float g) {
     const int32_t* rec = round_rec(rec_in, iter_dev, n_iters, words);
     if (!rec) return;
+    peer_acquire(rec[2]);
     __shared__ float ls[kTile], lh[kTile];
     __shared__ uint8_t ds[kTile / GRAN], dh[kTile / GRAN];
-    apply_tile<NT, GRAN>(x, xh, s, ld, P, msgs, msg_ld, kpad, k, rec, n_local, M, alpha, g, ls, lh, ds, dh);
+    apply_tile<NT, GRAN, SP>(x, xh, s, ld, P, msgs, msg_ld, kpad, k, rec, n_local, M, alpha, g, ls, lh, ds, dh);
 }
 
 // The same pass with the message phase's global reads moved under the tile's stream: the plan
@@ -1771,7 +1791,7 @@ __global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, floa
 // are loaded as in the plain kernel.  Same order of updates, same results.
 constexpr int kPfMsgs = 8;
 
-template <bool NT>
+template <bool NT, bool SP>
 __global__ __launch_bounds__(kTPB) void apply_kernel_pf(float* __restrict__ x, float* __restrict__ xh,
                                                         float* __restrict__ s, int64_t ld, int64_t P,
                                                         const char* __restrict__ msgs, int64_t msg_ld,
@@ -1782,6 +1802,7 @@ __global__ __launch_bounds__(kTPB) void apply_kernel_pf(float* __restrict__ x, f
                                                         float alpha, float g) {
     const int32_t* rec = round_rec(rec_in, iter_dev, n_iters, words);
     if (!rec) return;
+    peer_acquire(rec[2]);
     constexpr int kGran = 16;
     const int r = blockIdx.y;
     const int64_t t = blockIdx.x;
@@ -1793,7 +1814,7 @@ __global__ __launch_bounds__(kTPB) void apply_kernel_pf(float* __restrict__ x, f
     __shared__ float ls[kTile], lh[kTile];
     __shared__ uint8_t ds[kTile / kGran], dh[kTile / kGran];
     if (!(len == kTile && (((uintptr_t)xr | (uintptr_t)sr | (uintptr_t)hr) & 15) == 0)) {   // partial /
-        apply_tile<NT, 16>(x, xh, s, ld, P, msgs, msg_ld, kpad, k, rec, n_local, M, alpha, g, ls, lh, ds, dh);
+        apply_tile<NT, 16, SP>(x, xh, s, ld, P, msgs, msg_ld, kpad, k, rec, n_local, M, alpha, g, ls, lh, ds, dh);
         return;                                                                         // unaligned tile
     }
     // from here on the whole-tile path is branch-free up to the message phase, so the waitcnt pass
@@ -1814,7 +1835,7 @@ __global__ __launch_bounds__(kTPB) void apply_kernel_pf(float* __restrict__ x, f
         const int e = lane < kPfMsgs ? lane : 0;
         const int sl = lane < kPfMsgs && e < d ? src[e] : r;
         my_sl = sl;
-        const Msg m = msg_at(msgs, msg_ld, kpad, k, sl);
+        const Msg m = msg_at<SP>(msgs, msg_ld, kpad, k, sl);
         if (lane < kPfMsgs && e < nm) {
             my_lo = max(m.bnd[t], 0);              // clamped: a received message is not trusted
             my_hi = min(m.bnd[t + 1], (int)k);     // to stay in range
@@ -1836,7 +1857,7 @@ __global__ __launch_bounds__(kTPB) void apply_kernel_pf(float* __restrict__ x, f
         plo[e] = __builtin_amdgcn_readlane(my_lo, e);
         phi[e] = __builtin_amdgcn_readlane(my_hi, e);
         const int q = plo[e] + tid < phi[e] ? plo[e] + tid : 0;     // clamped: loads stay unconditional
-        const Msg m = msg_at(msgs, msg_ld, kpad, k, __builtin_amdgcn_readlane(my_sl, e));
+        const Msg m = msg_at<SP>(msgs, msg_ld, kpad, k, __builtin_amdgcn_readlane(my_sl, e));
         pix[e] = m.ix[q];
         pv[e] = m.v[q];
     }
@@ -1864,14 +1885,14 @@ __global__ __launch_bounds__(kTPB) void apply_kernel_pf(float* __restrict__ x, f
         const bool own = e == d;
         if (plo[e] + tid < phi[e]) upd(own, pix[e], pv[e]);
         if (phi[e] - plo[e] > kTPB) {
-            const Msg m = msg_at(msgs, msg_ld, kpad, k, __builtin_amdgcn_readlane(my_sl, e));
+            const Msg m = msg_at<SP>(msgs, msg_ld, kpad, k, __builtin_amdgcn_readlane(my_sl, e));
             for (int q = plo[e] + kTPB + tid; q < phi[e]; q += kTPB) upd(own, m.ix[q], m.v[q]);
         }
         __syncthreads();                       // a later message may touch the same element
     }
     for (int e = kPfMsgs; e < nm; ++e) {
         const bool own = e == d;
-        const Msg m = msg_at(msgs, msg_ld, kpad, k, own ? r : src[e]);
+        const Msg m = msg_at<SP>(msgs, msg_ld, kpad, k, own ? r : src[e]);
         const int lo = max(m.bnd[t], 0), hi = min(m.bnd[t + 1], (int)k);
         for (int q = lo + tid; q < hi; q += kTPB) upd(own, m.ix[q], m.v[q]);
         __syncthreads();
@@ -2304,7 +2325,20 @@ extern "C" size_t mx_choco_apply_work_bytes(int64_t, int) { return 0; }
 namespace {
 int choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t k, const void* msgs,
                 int64_t msg_ld_bytes, int n_slots, const int32_t* plan_dev, int64_t iter, const int64_t* iter_dev,
-                int n_local, int M, float alpha, float gamma, void* work, void* stream);
+                int n_local, int M, float alpha, float gamma, void* work, void* stream, bool slot_table = false);
+}
+
+// The pull transport's apply (ChocoWorkerGroup under PullTransport): message `slot` is read from the
+// address slot_ptrs_dev[slot] -- the local rows' messages in this GPU's message buffer, the partners'
+// in their owners' IPC-mapped snapshot buffers (pointed there by mx_pull_gate on the device).  Same
+// pass, same order of updates, same bits as mx_choco_apply.
+extern "C" int mx_choco_apply_slots(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t k,
+                                    const int64_t* slot_ptrs_dev, int n_slots, const int32_t* plan_dev,
+                                    int64_t iter, int n_local, int M, float alpha, float gamma, void* stream) {
+    MX_CHECK(iter >= 0, "mx_choco_apply_slots: iter < 0");
+    MX_CHECK(slot_ptrs_dev, "mx_choco_apply_slots: null slot table");
+    return choco_apply(x, xhat, s, ld, P, k, slot_ptrs_dev, 0, n_slots, plan_dev, iter, nullptr, n_local, M,
+                       alpha, gamma, nullptr, stream, true);
 }
 
 extern "C" int mx_choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t k,
@@ -2328,7 +2362,7 @@ extern "C" int mx_choco_apply_at(float* x, float* xhat, float* s, int64_t ld, in
 namespace {
 int choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t k, const void* msgs,
                 int64_t msg_ld_bytes, int n_slots, const int32_t* plan_dev, int64_t iter, const int64_t* iter_dev,
-                int n_local, int M, float alpha, float gamma, void* work, void* stream) {
+                int n_local, int M, float alpha, float gamma, void* work, void* stream, bool slot_table) {
     (void)work;
     MX_CHECK(x && xhat && s && msgs && plan_dev, "mx_choco_apply: null pointer");
     MX_CHECK(P >= 1 && k >= 1 && k <= P && ld >= P && k < (int64_t)1 << 31, "mx_choco_apply: P=%lld k=%lld ld=%lld",
@@ -2336,8 +2370,8 @@ int choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t 
     MX_CHECK(n_local >= 1 && n_local <= 65535 && n_slots >= n_local && n_slots <= 65535 && M >= 1,
              "mx_choco_apply: n_local=%d n_slots=%d M=%d", n_local, n_slots, M);
     const int64_t kpad = (k + 1) / 2 * 2;
-    MX_CHECK(msg_ld_bytes >= mx_choco_msg_bytes(P, k) && msg_ld_bytes % 8 == 0, "mx_choco_apply: msg_ld %lld",
-             (long long)msg_ld_bytes);
+    MX_CHECK(slot_table || (msg_ld_bytes >= mx_choco_msg_bytes(P, k) && msg_ld_bytes % 8 == 0),
+             "mx_choco_apply: msg_ld %lld", (long long)msg_ld_bytes);
     hipStream_t st = mx::as_stream(stream);
     const int64_t words = mx::plan_words(n_local, M);
     const int32_t* rec = iter_dev ? plan_dev : plan_dev + iter * words;   // with iter_dev: iter = n_iters
@@ -2345,8 +2379,10 @@ int choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t 
     const char* m = static_cast<const char*>(msgs);
     MX_CHECK(nt <= 0x7fffffff, "mx_choco_apply: P too large");
     const bool nt_hint = g_apply_nt < 0 ? n_local > 1 : g_apply_nt > 0;
-    auto kern = g_apply_pf ? (nt_hint ? apply_kernel_pf<true> : apply_kernel_pf<false>)
-                           : (nt_hint ? apply_kernel<true, 16> : apply_kernel<false, 16>);
+    auto kern = slot_table ? (g_apply_pf ? (nt_hint ? apply_kernel_pf<true, true> : apply_kernel_pf<false, true>)
+                                         : (nt_hint ? apply_kernel<true, 16, true> : apply_kernel<false, 16, true>))
+                           : (g_apply_pf ? (nt_hint ? apply_kernel_pf<true, false> : apply_kernel_pf<false, false>)
+                                         : (nt_hint ? apply_kernel<true, 16, false> : apply_kernel<false, 16, false>));
     hipLaunchKernelGGL(kern, dim3((unsigned)nt, n_local), dim3(kTPB),
                        0, st, x, xhat, s, ld, P, m,
                        msg_ld_bytes, kpad, k, rec, iter_dev, iter, words, n_local, M, alpha, gamma);

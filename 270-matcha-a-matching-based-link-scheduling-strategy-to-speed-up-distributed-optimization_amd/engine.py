@@ -199,13 +199,15 @@ class PullTransport:
             raise ValueError("PullTransport: timeout_s must be > 0")
         self.timeout_s = float(timeout_s)
 
-    def bind(self, vwg):
+    def bind(self, vwg, row_bytes=None):
         """Collective: allocate vwg's snapshot buffer, exchange handles, map the peers'.  Every
         rank takes part in every exchange even when its own step failed, and all ranks raise
-        together (MXError) if any failed, so a refusal on one GPU cannot leave the others waiting."""
+        together (MXError) if any failed, so a refusal on one GPU cannot leave the others waiting.
+        row_bytes: the stride of one worker's snapshot (default: a whole row, vwg.ld floats; a
+        ChocoWorkerGroup passes its message stride)."""
         import torch.distributed as dist
         hb = int(lib.mx_ipc_handle_bytes())
-        half = vwg.n_local * vwg.ld * 4
+        half = vwg.n_local * (int(row_bytes) if row_bytes is not None else vwg.ld * 4)
         own = ctypes.c_void_p()
         handle = (ctypes.c_char * hb)()
         err = None

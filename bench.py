@@ -604,16 +604,50 @@ def choco_oracle_round(pkg, grp, GP, it, ratio, gamma, rank, world):
     return ok
 
 
-def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99, gamma=0.1, placement=None):
+def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99, gamma=0.1, placement=None,
+                 pull="auto"):
     """Secondary figure: ChocoSGD rounds (BASELINE config 4: VGG-16 size, top-1 %, graph 0, every
     matching active) on the same GPUs -- top-k compress + [N > 1] message exchange + fused apply.
-    Parity: one more round after the timed ones, x / x_hat / s of every worker vs the oracle's
-    round from the same state (choco_oracle_round)."""
+    N > 1: the messages travel over RCCL (mx_exchange_round) or, under the pull transport, are read
+    by the apply pass from the owners' IPC-mapped snapshot buffers (mx_choco_apply_slots behind the
+    device gate); both forms run R untimed rounds and the faster (max over ranks) is timed, unless
+    --pull on / off forces it.  Parity: one more round after the timed ones, x / x_hat / s of every
+    worker vs the oracle's round from the same state (choco_oracle_round)."""
+    R = 4
     grp = pkg.ChocoWorkerGroup(GP, numel=P, ratio=ratio, consensus_lr=gamma, rank=rank, nranks=world,
                                comm=comm, placement=placement)
     fill_synth(pkg, grp)
     for it in range(W):
         grp.step(it)
+    forms, calib, pull_err = {"rccl": grp}, None, None
+    any_remote = world > 1 and max_over_ranks(float(grp.engine.max_remote), world, dev) > 0   # collective
+    if any_remote and pull != "off":
+        gp = None
+        try:
+            gp = pkg.ChocoWorkerGroup(GP, numel=P, ratio=ratio, consensus_lr=gamma, rank=rank, nranks=world,
+                                      comm=pkg.PullTransport(timeout_s=PULL_TIMEOUT_S), placement=placement)
+            fill_synth(pkg, gp)
+            for it in range(W):
+                gp.step(it)
+            gp.wait_round()                      # a gate that expired in the warmup raises here
+        except pkg.MXError as e:
+            pull_err = str(e)
+        if gp is not None:
+            if max_over_ranks(float(pull_err is not None), world, dev) > 0:
+                pull_err = pull_err or "a peer's pull warmup failed"
+                gp.close()
+            else:
+                forms["pull"] = gp
+    if len(forms) > 1:
+        calib = {name: 1e3 * timed_loop(g.step, W, R, world, dev) / R for name, g in forms.items()}
+        chosen = "pull" if pull == "on" else min(calib, key=calib.get)
+        for name in list(forms):
+            if name != chosen:
+                forms.pop(name).close()
+        grp = forms[chosen]
+        W += R
+    else:
+        chosen = "rccl" if world > 1 else None
     el = timed_loop(grp.step, W, K, world, dev)
     st = np.zeros(5 * grp.n_local, np.int64)
     pkg._lib.check(pkg.lib.mx_topk_stats(grp.work.data_ptr(), grp.work_ld, grp.n_local, grp.numel, st.ctypes.data,
@@ -625,9 +659,16 @@ def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99
            "topk": {"calls_per_row": int(st[:, 0].max()), "fallback_compactions": int(st[:, 1].sum()),
                     "candidates_per_k_last": [round(int(c) / grp.k, 2) for c in st[:, 4]],
                     "floor": "fine sampled" if pkg.lib.mx_topk_get(b"fine_floor") == 1 else "sampled digit"}}
+    if world > 1:
+        out["form"] = chosen
+        out["calib_ms"] = calib
+        out["pull_unavailable"] = pull_err
+        if grp.pulls:
+            out["pull_rounds"] = int(grp._pull.round)
+            out["pull_gate_error"] = grp._pull.error()
     out["parity_ok"] = choco_oracle_round(pkg, grp, GP, W + K, ratio, gamma, rank, world)
-    out["parity"] = (f"round {W + K} (after the {W} warmup + {K} timed rounds) of every worker: x, x_hat, s vs the "
-                     f"oracle's Choco round from the same state, uint32")
+    out["parity"] = (f"round {W + K} (after the {W} warmup / calibration + {K} timed rounds) of every worker: x, "
+                     f"x_hat, s vs the oracle's Choco round from the same state, uint32")
     if world == 1:
         # ~6 P 4 B per worker (top-k reads x, x_hat; apply reads x, s, x_hat, writes x)
         alg = 24 * P * grp.n_local
@@ -635,7 +676,8 @@ def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99
                            "frac_of_8TBps": alg / (el / K) / HBM_PEAK,
                            "note": "algorithmic bytes; the passes also move the dirty 64-B granules of s / x_hat "
                                    "and the candidate / message bytes (~3.2 GB per 8-row round by PMC, r02)"}
-    del grp
+    grp.close()
+    del grp, forms
     torch.cuda.empty_cache()
     if world == 1:
         out["one_row_share_n8"] = choco_row_share(pkg, GP, P, ratio, gamma, K, W)
@@ -1384,7 +1426,8 @@ def run(args, world, rank, line, wd):
     del timed, group
     torch.cuda.empty_cache()
     out["choco"] = figure("choco", lambda: choco_figure(pkg, GP, rank, world, max(20, K), 3, comm, dev,
-                                                        P=args.choco_params, placement=args.placement),
+                                                        P=args.choco_params, placement=args.placement,
+                                                        pull=args.pull),
                           bool(args.choco))
     out["cpu_resident_models"] = figure("staged", lambda: staged_figure(pkg, GP, n, P, 3, W),
                                         world == 1 and bool(args.staged))

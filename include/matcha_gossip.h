@@ -294,6 +294,16 @@ int mx_choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64
 int mx_choco_apply_at(float* x, float* x_hat, float* s, int64_t ld, int64_t P, int64_t k, const void* msgs,
                       int64_t msg_ld_bytes, int n_slots, const int32_t* plan_dev, const int64_t* iter_dev,
                       int64_t n_iters, int n_local, int M, float alpha, float gamma, void* work, void* stream);
+/* The pull transport's form (ChocoWorkerGroup under PullTransport; replaces the sendrecv of the
+ * compressed messages, communicator.py:214, with loads from the owners' HBM): message `slot` is
+ * read at the device address slot_ptrs_dev[slot] (int64 [n_slots]) -- the local rows' messages in
+ * this GPU's buffer, the partners' in their owners' IPC-mapped snapshot buffers (mx_snapshot_publish
+ * of the message slots, then mx_pull_gate with ld_bytes = the message stride points the remote
+ * slots there).  A plan record with the peer-reads bit (mx_plan_set_peer_reads) makes every
+ * workgroup acquire at system scope before its first message load.  Same bits as mx_choco_apply. */
+int mx_choco_apply_slots(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t k,
+                         const int64_t* slot_ptrs_dev, int n_slots, const int32_t* plan_dev, int64_t iter,
+                         int n_local, int M, float alpha, float gamma, void* stream);
 
 /* ---------------------------------------------------------------- cross-GPU exchange (RCCL)
  * One process per GPU; workers partitioned by owner[].  mx_exchange_round posts, inside one

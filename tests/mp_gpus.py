@@ -1,7 +1,8 @@
 """One rank per GPU (tests/test_gpu_multiproc.py::test_cross_gpu_transports_match_oracle launches 2-4
 via torchrun when that many GPUs are visible): the REAL cross-GPU transports -- the library's RCCL
 communicator (plain and column-pipelined exchange, Choco messages, the ordered all-reduce) and the
-pull transport over xGMI with its device gate (back to back, arbitrary rows, snapshot buffers on
+pull transport over xGMI with its device gate (whole rows and Choco messages, back to back,
+arbitrary rows, snapshot buffers on
 different GPUs, so the cross-L2 release / acquire protocol is exercised) -- every worker's row vs
 the single-process oracle, bit-exact.  Skipped on a one-GPU box (RCCL refuses two ranks on one
 device).  Rank 0 prints one JSON line; exit status 0 = every case matched."""
@@ -37,6 +38,8 @@ def main():
         "pull_decen_g0_long": W.decen_case(pkg, pkg.PullTransport(timeout_s=60), 0, 30_011, 30, seed=11,
                                            back_to_back=True),
         "pull_rows_g2_placed": W.pull_rows_case(pkg, 2, 12_007, 20, placement="auto"),
+        "pull_choco_g0_placed_long": W.choco_case(pkg, pkg.PullTransport(timeout_s=60), 20_011, 0.9, 12, seed=13,
+                                                  placement="auto", back_to_back=True),
     }
     torch.cuda.synchronize()
     flags = [None] * dist.get_world_size()

@@ -96,7 +96,10 @@ def pull_rows_case(pkg, gid, P, rounds, seed=21, placement=None):
     return bool(np.array_equal(got.view(np.uint32), X.view(np.uint32))) and adhoc > 0
 
 
-def choco_case(pkg, T, P, ratio, rounds, seed=9, placement=None):
+def choco_case(pkg, T, P, ratio, rounds, seed=9, placement=None, back_to_back=False):
+    """x and x_hat of every worker vs the oracle's Choco rounds; with back_to_back all rounds are
+    enqueued by step() with no host wait between them (the pull transport's device gate alone
+    orders them across ranks)"""
     rank, world = dist.get_rank(), dist.get_world_size()
     n = 8
     gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, n, 4, True)
@@ -112,12 +115,22 @@ def choco_case(pkg, T, P, ratio, rounds, seed=9, placement=None):
     S = np.zeros_like(X)
     grp.rows.copy_(torch.from_numpy(X[grp.workers]))
     for it in range(rounds):
-        grp.communicate()
+        if back_to_back:
+            grp.step(it)
+        else:
+            grp.communicate()
         if flags[it].any():
             O.choco_round(X, XH, S, np.asarray(topo.neighbors_info, np.int32), flags[it], 2 / 7, grp.k, 0.1)
+    if back_to_back:
+        grp.wait_round()
+        grp.check_topk()
     got = by_worker(grp, gather_rows(grp.rows, grp.row_base, n))
     gxh = by_worker(grp, gather_rows(grp.x_hat[:, :P], grp.row_base, n))
-    return bool(np.array_equal(got.view(np.uint32), X.view(np.uint32)) and np.array_equal(gxh, XH))
+    gs = by_worker(grp, gather_rows(grp.s[:, :P], grp.row_base, n))
+    grp.close()
+    return bool(np.array_equal(got.view(np.uint32), X.view(np.uint32)) and
+                np.array_equal(gxh.view(np.uint32), XH.view(np.uint32)) and
+                np.array_equal(gs.view(np.uint32), S.view(np.uint32)))
 
 
 def centralized_case(pkg, T):
@@ -170,6 +183,11 @@ def main():
         # 40 device-gated rounds (no host barrier per round): each snapshot buffer reused 20 times
         "decen_g0_pull_long": decen_case(pkg, pkg.PullTransport(), 0, 30_011, 40, seed=11, back_to_back=True),
         "decen_g2_pull_rows_placed": pull_rows_case(pkg, 2, 12_007, 24, placement="auto"),
+        # Choco under the pull transport: the partners' top-k messages read by the apply pass from
+        # the owners' snapshot buffers (each reused 3 / 7 times), communicate() and back to back
+        "choco_g0_pull": choco_case(pkg, pkg.PullTransport(), 40_003, 0.9, 6),
+        "choco_g0_pull_long_placed": choco_case(pkg, pkg.PullTransport(), 20_011, 0.9, 14, seed=13,
+                                                placement="auto", back_to_back=True),
     }
     torch.cuda.synchronize()
     if dist.get_rank() == 0:

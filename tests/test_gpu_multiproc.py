@@ -69,6 +69,9 @@ def test_bench_multiprocess_path(nproc):
     assert out["allreduce_baseline"]["rounds_per_s"] > 0
     assert out["allreduce_baseline"]["parity_ok"] is True          # all-gather + mx_mean_rows_to, tree order
     assert out["choco"]["topk"]["calls_per_row"] > 0
+    # Choco at N > 1: the RCCL-form (gloo here) and pull forms calibrated, the faster timed
+    assert set(out["choco"]["calib_ms"]) == {"rccl", "pull"} and out["choco"]["form"] in ("rccl", "pull")
+    assert out["choco"]["pull_unavailable"] is None
     # every self-check is the oracle's (checker) on the same inputs
     assert out["parity_ok"] is True and "oracle" in out["parity"]
     assert out["choco"]["parity_ok"] is True
@@ -114,10 +117,12 @@ def test_bench_watchdog_line_on_hang():
                                                (4, "auto", "auto")])
 def test_bench_multiprocess_overlap_forms(nproc, overlap, pull):
     """bench.py's N > 1 branch with the exchange form forced (column-pipelined / plain / pull) or
-    calibrated among all three; the timed form passes the self-check."""
+    calibrated among all three; the timed form passes the self-check.  With --pull on the Choco
+    figure runs too, forced onto the pull form (messages read from the owners' snapshots)."""
+    choco = ["--choco", "1", "--choco-params", "100000"] if pull == "on" else ["--choco", "0"]
     r = _torchrun(nproc, ["bench.py", "--gpus", str(nproc), "--transport", "gloo", "--steps", "3", "--warmup", "1",
-                          "--params", "100000", "--choco", "0", "--cpu-seconds", "0", "--overlap", overlap,
-                          "--pull", pull, "--configs", "0", "--er", "0", "--allreduce", "0"])
+                          "--params", "100000", "--cpu-seconds", "0", "--overlap", overlap,
+                          "--pull", pull, "--configs", "0", "--er", "0", "--allreduce", "0"] + choco)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["value"] > 0 and out["parity_ok"] is True
@@ -129,6 +134,9 @@ def test_bench_multiprocess_overlap_forms(nproc, overlap, pull):
         assert out["overlap"]["chosen_form"] == "pull" and out["overlap"]["pull_unavailable"] is None
         assert out["overlap"]["pull_rounds"] >= 6, out["overlap"]
         assert out["overlap"]["pull_gate_error"] is None, out["overlap"]
+        ch = out["choco"]
+        assert ch["form"] == "pull" and ch["pull_rounds"] >= 6 and ch["pull_gate_error"] is None, ch
+        assert ch["parity_ok"] is True, ch
     elif overlap == "off" and pull == "off":
         assert out["overlap"] is None
     else:

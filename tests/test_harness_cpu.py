@@ -86,17 +86,14 @@ def test_rendezvous_port_from_job_id(pkg):
 
 
 def test_pull_transport_refused_where_it_cannot_carry(pkg):
-    """The pull transport serves whole-row gossip only (VirtualWorkerGroup): the Choco and the
-    centralized communicators refuse it at construction with a clear TypeError, not
-    with a null-handle error at the first round.  No GPU: the refusal comes first."""
+    """The pull transport serves gossip rounds (whole rows and, from round 5, Choco messages): the
+    centralized communicator refuses it at construction with a clear TypeError, not
+    with a null-handle error at the first round (the Choco communicator takes it: -m gpu tests).
+    No GPU: the refusal comes first."""
     import pytest as _pytest
-    from conftest import Topo
     t = pkg.PullTransport.__new__(pkg.PullTransport)
-    topo = Topo([[1, 0]], 0.5, [[1]])
     with _pytest.raises(TypeError, match="PullTransport"):
         pkg.centralizedCommunicator(0, 2, transport=t)
-    with _pytest.raises(TypeError, match="PullTransport"):
-        pkg.ChocoCommunicator(0, 2, topo, 0.9, 0.1, transport=t)
 
 
 def test_rccl_deadline_api_declared(pkg):

@@ -11,6 +11,9 @@ both sides, max over ranks.  Forms:
   chunked  -- the same, column-pipelined in 4 chunks on a side stream
   pull     -- PullTransport (IPC-mapped snapshots read by the mixing kernel)
   mix_only -- the pull group's mixing launches alone (no publish, gate or exchange)
+and the same for ChocoSGD rounds (top-1 %, same P): choco_plain (messages over the gloo stand-in),
+choco_pull (the apply reads them from the owners' snapshots behind the device gate) and choco_null
+(a transport that moves nothing: compress + apply alone).
 Prints one JSON line (rank 0)."""
 import json
 import os
@@ -65,9 +68,31 @@ def main():
             st = g._pull
             res["pull_rounds"] = int(st.round)
         g.close()
+    class NullComm:
+        handle = None
+
+        def __init__(self):
+            self.rank, self.nranks = rank, world
+
+        def exchange_round(self, *a):
+            return 0
+
+    cforms = {"choco_plain": GlooTransport(pkg), "choco_pull": pkg.PullTransport(), "choco_null": NullComm()}
+    for name, comm in cforms.items():
+        g = pkg.ChocoWorkerGroup(topo, numel=P, ratio=0.99, consensus_lr=0.1, rank=rank, nranks=world, comm=comm)
+        for r in range(g.n_local):
+            pkg._lib.check(pkg.lib.mx_synth_fill(g.rows[r].data_ptr(), P, 1234 + g.workers[r], None))
+        for it in range(5):
+            g.step(it)
+        res[name + "_ms"] = timed(world, g.step, 5, K)
+        if name == "choco_pull":
+            res["choco_pull_rounds"] = int(g._pull.round)
+        g.close()
     if rank == 0:
         for name in forms:
             res[name + "_overhead_ms"] = res[name + "_ms"] - res["mix_only_ms"]
+        for name in ("choco_plain", "choco_pull"):
+            res[name + "_overhead_ms"] = res[name + "_ms"] - res["choco_null_ms"]
         print(json.dumps(res), flush=True)
     dist.barrier()
     dist.destroy_process_group()
