@@ -46,6 +46,10 @@ METRIC = "gossip rounds/sec (8 workers x 25.6M fp32 params, graph 0, full MATCHA
 # rccl_overhead.py, profiles/r05m_rccl_overhead.log: 7.3 us for 4 KB - 1.8 MB) -- a LOWER bound of a
 # cross-GPU group's cost, one per exchange (one per chunk for the pipelined form).
 PULL_FIXED_S = {2: 26e-6, 4: 31e-6, 8: 62e-6}
+# the same for a ChocoSGD round under the pull transport (message publish + gate + the apply's
+# remote reads, minus compress + apply with a transport that moves nothing; P = 100k, top-1 %:
+# profiles/r05p_overhead_n*.log)
+PULL_CHOCO_FIXED_S = {2: 10.6e-6, 4: 12.0e-6, 8: 41.8e-6}
 PULL_TIMEOUT_S = 20.0      # the pull gate's deadline in the bench (lockstep rounds of at most a few ms)
 RCCL_FIXED_S = 7.3e-6
 HEADLINE_HBM_FRAC = 0.75   # the mixing kernel's measured fraction of 8 TB/s (BENCH_r04, profiles/)
@@ -416,6 +420,25 @@ def predict_round(form, world, link_bytes, mix_s, publish_bytes, chunks=4, mix_s
             "xgmi_frac": (link_bytes / t / XGMI_LINK_PEAK) if t > 0 else None}
 
 
+def predict_choco(form, world, link_bytes, local_s, publish_bytes):
+    """What a ChocoSGD round of `form` should cost at N = world: this rank's compress
+    + apply with a transport that moves nothing (local_s, measured in the same run, max over ranks),
+    plus the busiest link's message bytes at 153 GB/s, plus the form's fixed cost (RCCL: the
+    one-rank self-exchange floor, a lower bound; pull: PULL_CHOCO_FIXED_S measured, and the message
+    snapshot copy at the headline's HBM fraction).  Serial sum: the messages cross before the apply."""
+    t_link = link_bytes / XGMI_LINK_PEAK
+    if form == "pull":
+        fixed = PULL_CHOCO_FIXED_S.get(world, max(PULL_CHOCO_FIXED_S.values()))
+        src = "measured (tools/form_overhead.py, N processes sharing one GPU)"
+        t_pub = publish_bytes / (HEADLINE_HBM_FRAC * HBM_PEAK)
+    else:
+        fixed, src, t_pub = RCCL_FIXED_S, "lower bound: one-rank RCCL self-exchange (tools/rccl_overhead.py)", 0.0
+    t = local_s + t_pub + t_link + fixed
+    return {"busiest_link_bytes": float(link_bytes), "link_bound_ms": 1e3 * t_link, "local_ms": 1e3 * local_s,
+            "publish_ms": 1e3 * t_pub, "fixed_ms": 1e3 * fixed, "fixed_source": src, "round_ms": 1e3 * t,
+            "rounds_per_s": 1.0 / t if t > 0 else None}
+
+
 def p2p_probe(rank, world, nbytes, dev, reps=5):
     """N > 1: one xGMI link through RCCL (torch.distributed send/recv on the nccl group), ranks 0
     and 1 only: unidirectional 0 -> 1 and bidirectional 0 <-> 1, seconds per transfer (max over
@@ -666,6 +689,25 @@ def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99
         if grp.pulls:
             out["pull_rounds"] = int(grp._pull.round)
             out["pull_gate_error"] = grp._pull.error()
+        # the expected round of each form from its parts: this rank's compress + apply alone (a
+        # transport that moves nothing, K rounds, max over ranks) + the busiest link's messages
+        eng = grp.engine
+        flags = np.asarray(GP.active_flags[W:W + K], np.uint8)
+        _, link_b, _, _ = round_bytes(eng.partner, eng.owner, flags, rank, grp.row_base, grp.n_local,
+                                      grp.msg_bytes / 4)
+        loc = pkg.ChocoWorkerGroup(GP, numel=P, ratio=ratio, consensus_lr=gamma, rank=rank, nranks=world,
+                                   comm=_NullComm(rank, world), placement=placement)
+        fill_synth(pkg, loc)
+        for it in range(W):
+            loc.step(it)
+        local_s = timed_loop(loc.step, W, K, world, dev) / K
+        del loc
+        lb = float(np.mean(link_b))
+        out["predicted"] = {f: predict_choco(f, world, lb, local_s, grp.n_local * grp.msg_ld) for f in ("rccl", "pull")}
+        pr = out["predicted"][chosen]
+        out["predicted"]["timed_form"] = chosen
+        out["predicted"]["achieved_over_predicted"] = pr["round_ms"] / (1e3 * el / K)
+        out["message_bytes"] = int(grp.msg_bytes)
     out["parity_ok"] = choco_oracle_round(pkg, grp, GP, W + K, ratio, gamma, rank, world)
     out["parity"] = (f"round {W + K} (after the {W} warmup / calibration + {K} timed rounds) of every worker: x, "
                      f"x_hat, s vs the oracle's Choco round from the same state, uint32")

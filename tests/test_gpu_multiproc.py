@@ -72,6 +72,10 @@ def test_bench_multiprocess_path(nproc):
     # Choco at N > 1: the RCCL-form (gloo here) and pull forms calibrated, the faster timed
     assert set(out["choco"]["calib_ms"]) == {"rccl", "pull"} and out["choco"]["form"] in ("rccl", "pull")
     assert out["choco"]["pull_unavailable"] is None
+    cp = out["choco"]["predicted"]
+    for f in ("rccl", "pull"):
+        assert cp[f]["busiest_link_bytes"] > 0 and cp[f]["local_ms"] > 0 and cp[f]["round_ms"] > 0, cp[f]
+    assert cp["timed_form"] == out["choco"]["form"] and cp["achieved_over_predicted"] > 0
     # every self-check is the oracle's (checker) on the same inputs
     assert out["parity_ok"] is True and "oracle" in out["parity"]
     assert out["choco"]["parity_ok"] is True

@@ -7,7 +7,9 @@ built with a null transport (tools/nullcomm.py: no transfer; received rows hold 
 mixing kernel alone is timed (HIP events, median of K launches) -- the "mixing share" term.  The
 busiest directed link's bytes per round come from bench.round_bytes; bench.predict_round adds the
 form's fixed cost (pull measured, RCCL assumed) and, for pull, the snapshot copy.  The slowest
-rank's mixing time is used (the round ends with it).  Prints one JSON line."""
+rank's mixing time is used (the round ends with it).  Then the same for ChocoSGD rounds (config 4:
+compress + apply per rank, the busiest link's messages, bench.predict_choco).  Prints two JSON
+lines."""
 import importlib
 import json
 import os
@@ -57,3 +59,43 @@ for N in (2, 4, 8):
         row[form] = bench.predict_round(form, N, lb, mix_s, pub, 4, "one-GPU mixing share of the slowest rank")
     out["rows"].append(row)
 print(json.dumps(out), flush=True)
+
+# ChocoSGD (config 4: VGG-16 size, top-1 %): every rank's compress + apply with the null transport
+# (received message slots hold stand-ins: the top-k messages of other synthetic rows, as the bench's
+# one-row share), per-round HIP events, median; link bytes = the busiest link's messages
+CP = int(float(os.environ.get("PRED_CHOCO_P", 14_774_436)))
+cout = {"graph": 0, "workers": n, "P": CP, "ratio": 0.99, "placement": "auto", "rows": []}
+for N in (2, 4, 8):
+    loc, links, pubs = [], [], []
+    for r in range(N):
+        c = pkg.ChocoWorkerGroup(GP, numel=CP, ratio=0.99, consensus_lr=0.1, rank=r, nranks=N, comm=NullComm(r, N),
+                                 placement="auto")
+        for s in range(c.n_local, c.engine.n_slots):
+            pkg._lib.check(pkg.lib.mx_synth_fill(c.rows[0].data_ptr(), CP, 7000 + s, None))
+            c.compress(0)
+            torch.cuda.synchronize()
+            c.msgs[s * c.msg_ld:(s + 1) * c.msg_ld].copy_(c.msgs[:c.msg_ld])
+        for i in range(c.n_local):
+            pkg._lib.check(pkg.lib.mx_synth_fill(c.rows[i].data_ptr(), CP, 1234 + c.workers[i], None))
+        c.work.zero_()
+        for j in range(3):
+            c.step(j)
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+        for j, (a, b) in enumerate(ev):
+            a.record()
+            c.step(3 + j)
+            b.record()
+        torch.cuda.synchronize()
+        loc.append(float(np.median([a.elapsed_time(b) for a, b in ev])) * 1e-3)
+        flags = np.asarray(GP.active_flags[3:3 + K], np.uint8)
+        _, link, _, _ = bench.round_bytes(c.engine.partner, c.engine.owner, flags, r, c.row_base, c.n_local,
+                                          c.msg_bytes / 4)
+        links.append(float(np.mean(link)))
+        pubs.append(c.n_local * c.msg_ld)
+        del c
+        torch.cuda.empty_cache()
+    row = {"N": N, "local_ms_per_rank": [round(1e3 * v, 4) for v in loc], "busiest_link_bytes": max(links)}
+    for form in ("rccl", "pull"):
+        row[form] = bench.predict_choco(form, N, max(links), max(loc), max(pubs))
+    cout["rows"].append(row)
+print(json.dumps(cout), flush=True)
