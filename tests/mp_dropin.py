@@ -4,7 +4,8 @@ The reference's deployment: one process per worker, each holding one model and c
 decenCommunicator / ChocoCommunicator(rank, size, GP, ...).communicate(model) after its
 optimizer step (train_mpi.py:79-81, 142).  Here the 8 processes share GPU 0 and exchange rows /
 messages through the gloo test transport; each round every rank's parameters are gathered and
-compared bit-exactly with the single-process oracle.  Exit status 0 = all matched."""
+compared bit-exactly with the single-process oracle -- and the same over the pull transport.
+Exit status 0 = all matched."""
 import importlib
 import json
 import os
@@ -66,6 +67,7 @@ def decen_case(pkg, T, dev, rounds=8):
         ok &= bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))
         ok &= (t == 0) == (not f.any())
     ok &= ids == [id(p) for p in model.parameters()] and comm.iter == rounds
+    comm.close()                         # collective under PullTransport (every rank, same call)
     return ok
 
 
@@ -94,6 +96,7 @@ def choco_case(pkg, T, dev, rounds=6, ratio=0.9, gamma=0.2):
         xh = [None] * n
         dist.all_gather_object(xh, comm.x_hat.cpu().numpy())
         ok &= bool(np.array_equal(np.stack(xh), XH))
+    comm.close()
     return ok
 
 
@@ -105,7 +108,12 @@ def main():
     res = {"decen_gpu_models": decen_case(pkg, T, "cuda"),
            "decen_cpu_models": decen_case(pkg, T, "cpu"),
            "choco_gpu_models": choco_case(pkg, T, "cuda"),
-           "choco_cpu_models": choco_case(pkg, T, "cpu")}
+           "choco_cpu_models": choco_case(pkg, T, "cpu"),
+           # train_mpi.py's deployment over the pull transport: rows / Choco messages read from the
+           # peers' IPC-mapped snapshot buffers behind the device gate (8 processes share GPU 0 here)
+           "decen_gpu_models_pull": decen_case(pkg, pkg.PullTransport(), "cuda"),
+           "choco_gpu_models_pull": choco_case(pkg, pkg.PullTransport(), "cuda"),
+           "choco_cpu_models_pull": choco_case(pkg, pkg.PullTransport(), "cpu")}
     torch.cuda.synchronize()
     flags = [None] * dist.get_world_size()
     dist.all_gather_object(flags, all(res.values()))

@@ -133,6 +133,45 @@ def choco_case(pkg, T, P, ratio, rounds, seed=9, placement=None, back_to_back=Fa
                 np.array_equal(gs.view(np.uint32), S.view(np.uint32)))
 
 
+def choco_pull_rows_case(pkg, P, rounds, seed=23, placement=None):
+    """ChocoCommunicator.averaging(active_flags) with arbitrary rows under the pull transport: a
+    random row per round (the same on every rank), its plan record found or built by
+    engine.record_for, rounds enqueued back to back (compress + publish + gate + apply) with no
+    host wait; x / x_hat / s of every worker vs the oracle at the end."""
+    rank, world = dist.get_rank(), dist.get_world_size()
+    n = 8
+    gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, n, 4, True)
+    M = len(gp.neighbors_info)
+    sched = np.zeros((3, M), np.uint8)
+    sched[0] = 1
+    sched[1, ::2] = 1
+    topo = Topo(gp.neighbors_info, 2 / 7, sched)
+    grp = pkg.ChocoWorkerGroup(topo, numel=P, ratio=0.95, consensus_lr=0.15, rank=rank, nranks=world,
+                               comm=pkg.PullTransport(), placement=placement)
+    X = np.stack([O.synth(700 + i, P) for i in range(n)])
+    XH = np.zeros_like(X)
+    S = np.zeros_like(X)
+    grp.rows.copy_(torch.from_numpy(X[grp.workers]))
+    rng = np.random.RandomState(seed)
+    partner = np.asarray(topo.neighbors_info, np.int32)
+    adhoc = 0
+    for _ in range(rounds):
+        f = (rng.uniform(size=M) < 0.5).astype(np.uint8)
+        if rng.uniform() < 0.3:
+            f = sched[rng.randint(2)].copy()
+        it = grp.engine.record_for(f)
+        adhoc += it == grp.engine.T
+        if f.any():
+            grp.step(it)
+            O.choco_round(X, XH, S, partner, f, 2 / 7, grp.k, 0.15)
+    grp.wait_round()
+    grp.check_topk()
+    got = [by_worker(grp, gather_rows(t[:, :P], grp.row_base, n)) for t in (grp.x, grp.x_hat, grp.s)]
+    grp.close()
+    return all(bool(np.array_equal(a.view(np.uint32), b.view(np.uint32))) for a, b in zip(got, (X, XH, S))) \
+        and adhoc > 0
+
+
 def centralized_case(pkg, T):
     """centralizedCommunicator through the product path (gather over the transport, then the
     native mx_mean_rows in the reference's order + the div_ of communicator.py:62) on random rows:
@@ -188,6 +227,7 @@ def main():
         "choco_g0_pull": choco_case(pkg, pkg.PullTransport(), 40_003, 0.9, 6),
         "choco_g0_pull_long_placed": choco_case(pkg, pkg.PullTransport(), 20_011, 0.9, 14, seed=13,
                                                 placement="auto", back_to_back=True),
+        "choco_g0_pull_rows_placed": choco_pull_rows_case(pkg, 15_013, 16, placement="auto"),
     }
     torch.cuda.synchronize()
     if dist.get_rank() == 0:
