@@ -228,6 +228,10 @@ def main():
         "choco_g0_pull_long_placed": choco_case(pkg, pkg.PullTransport(), 20_011, 0.9, 14, seed=13,
                                                 placement="auto", back_to_back=True),
         "choco_g0_pull_rows_placed": choco_pull_rows_case(pkg, 15_013, 16, placement="auto"),
+        # edge shapes under pull: one entry per message (k = 1, the reference's argmax branch) on a
+        # row shorter than one 4096-element tile, and an odd k on a ragged last tile
+        "choco_g0_pull_k1": choco_case(pkg, pkg.PullTransport(), 1_000, 0.9995, 5, seed=3, back_to_back=True),
+        "choco_g0_pull_odd_k": choco_case(pkg, pkg.PullTransport(), 12_389, 0.99, 5, seed=4),
     }
     torch.cuda.synchronize()
     if dist.get_rank() == 0:
