@@ -451,8 +451,21 @@ class RankTrainer:
     """One worker per process (torchrun): train_mpi.py's run(rank, size) with the drop-in
     communicators -- sync through RCCL all-reduce, then per batch step + communicate(model)."""
 
-    def __init__(self, args, model_fn, n_batches, rank, size, transport=None, device="cuda"):
-        from .communicator import ChocoCommunicator, centralizedCommunicator, decenCommunicator
+    def __init__(self, args, model_fn, n_batches, rank, size, transport=None, device="cuda",
+                 sync_transport="same"):
+        """transport: the communicators' (None = RCCL; "pull" = a PullTransport over the default
+        process group, which the gossip rounds use while the initial sync_allreduce stays on RCCL,
+        as the pull transport carries gossip rounds only).  sync_transport: the sync_allreduce's
+        ("same": `transport`, or RCCL when that is the pull transport)."""
+        from .communicator import ChocoCommunicator, _ensure_process_group, centralizedCommunicator, decenCommunicator
+        from .engine import PullTransport
+        if isinstance(transport, str):
+            if transport != "pull":
+                raise ValueError(f"transport {transport!r}: None, 'pull' or a transport object")
+            _ensure_process_group(rank, size)
+            transport = PullTransport()
+        if isinstance(sync_transport, str) and sync_transport == "same":
+            sync_transport = None if isinstance(transport, PullTransport) else transport
         self.args = args
         self.rank, self.size = rank, size
         torch.manual_seed(args.randomSeed + rank)                # train_mpi.py:61
@@ -467,7 +480,7 @@ class RankTrainer:
         self.optimizer = torch.optim.SGD(self.model.parameters(), lr=args.lr, momentum=args.momentum,
                                          weight_decay=5e-4, nesterov=args.nesterov, dampening=0)
         self.criterion = nn.CrossEntropyLoss()
-        centralizedCommunicator(rank, size, transport=transport).communicate(self.model)   # sync_allreduce
+        centralizedCommunicator(rank, size, transport=sync_transport).communicate(self.model)   # sync_allreduce
         self.data = synthetic_batches(rank, n_batches, args.bs, args.shape, args.num_classes, args.randomSeed,
                                       device)
         self.n_batches = n_batches
@@ -503,8 +516,11 @@ class RankTrainer:
                  "comm_time": comm_time}]
 
     def finish(self):
+        """Save the logs and release the communicator's group (collective under the pull
+        transport: every rank calls finish)."""
         if self.recorder is not None:
             self.recorder.save_to_file()
+        self.communicator.close()
 
 
 class HarnessArgs:

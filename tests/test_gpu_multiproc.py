@@ -188,6 +188,17 @@ def test_dropin_communicators_one_process_per_worker():
     assert res["world"] == 8 and all(v for k, v in res.items() if k != "world"), res
 
 
+def test_rank_trainer_matches_virtual_trainer():
+    """train_mpi.py's per-rank loop (harness.RankTrainer: sync_allreduce, then per batch SGD step +
+    communicate(model)) over 8 processes -- gossip through the gloo test transport and through the
+    pull transport (decen and Choco) -- ends with every worker's parameters bit-identical to the
+    single-process VirtualTrainer's (2 epochs, MATCHA 0.5, momentum 0.9)."""
+    r = _torchrun(8, [os.path.join(HERE, "mp_trainer.py")], timeout=280)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert res["world"] == 8 and all(v for k, v in res.items() if k != "world"), res
+
+
 def test_rccl_single_rank_linkage():
     """The library's own RCCL communicator (unique id over torch.distributed, ncclCommInitRank,
     all-reduce mean, an exchange round with nothing to move, destroy) under torchrun with the nccl

@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--batched", action="store_true", help="one vmap'd step for all virtual workers")
     ap.add_argument("--graph", action="store_true", help="with --batched: replay each iteration (step + "
                     "gossip round) as one captured HIP graph once the learning rate is constant")
+    ap.add_argument("--pull", action="store_true", help="one process per GPU: gossip rounds over the pull "
+                    "transport (partner rows / Choco messages read from the peers' HBM) instead of RCCL")
     a = ap.parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -55,7 +57,8 @@ def main():
     import torch
     if world > 1:
         torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
-        tr = H.RankTrainer(args, H.model_factory(args), a.batches, rank, world)
+        tr = H.RankTrainer(args, H.model_factory(args), a.batches, rank, world,
+                           transport="pull" if a.pull else None)
     else:
         tr = H.VirtualTrainer(args, H.model_factory(args), a.batches, batched=a.batched or a.graph, graph=a.graph)
         if a.resume:
