@@ -49,6 +49,7 @@ SIGNATURES = {
                                c_int, c_f32, c_f32, c_p, c_p]),
     "mx_choco_apply_at": (c_int, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_int, c_p, c_p, c_i64, c_int,
                                   c_int, c_f32, c_f32, c_p, c_p]),
+    "mx_pull_fetch": (c_int, [c_p, c_int, c_int, c_p, c_p, c_i64, c_i64, c_p]),
     "mx_choco_apply_slots": (c_int, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_int, c_p, c_i64, c_int, c_int,
                                      c_f32, c_f32, c_p]),
     "mx_rccl_unique_id": (c_int, [c_p]),

@@ -7,10 +7,11 @@ persistent Choco state x_hat and s (all [n_local, P] in HBM).  Per round:
     s / x_hat updates + dense x update      mx_choco_apply     (averaging, 200-230; one fused pass)
 Under PullTransport (N > 1, one process per GPU of a node) the messages are not sent: every rank
 publishes its rows' messages into its IPC-shared snapshot buffer (mx_snapshot_publish), the device
-gate (mx_pull_gate) waits for the partners' epochs and points the receive slots of a device slot
-table at their snapshots, and the apply pass reads the partners' messages from the owners' HBM
-(mx_choco_apply_slots) -- four launches per round and no host step, as VirtualWorkerGroup's pull
-round (engine.PullTransport).
+gate (mx_pull_gate) waits for the partners' epochs and points a device slot table at their
+snapshots, mx_pull_fetch copies the round's partner messages from the owners' HBM into the receive
+slots, and the apply pass runs as under RCCL (pull_read="fetch"; "direct": the apply reads them in
+place, mx_choco_apply_slots) -- no host step per round, as VirtualWorkerGroup's pull round
+(engine.PullTransport).
 """
 import time
 
@@ -30,9 +31,16 @@ def topk_count(P, ratio):
 
 class ChocoWorkerGroup:
     def __init__(self, topology, models=None, numel=None, *, ratio, consensus_lr, rank=0, nranks=1,
-                 comm=None, adopt=True, placement=None):
+                 comm=None, adopt=True, placement=None, pull_read="fetch"):
         """placement: as VirtualWorkerGroup (None / "contiguous", "auto" or a worker order);
-        `workers` lists the worker id of each local row."""
+        `workers` lists the worker id of each local row.  pull_read (PullTransport only): "fetch"
+        (default) copies the round's partner messages from their owners' snapshots into the receive
+        slots (mx_pull_fetch) before the apply; "direct" lets the apply read them in place
+        (mx_choco_apply_slots: no copy, but a system-scope acquire per apply workgroup and a table
+        load per message).  Same bits; which is faster across GPUs is measured by bench.py."""
+        if pull_read not in ("fetch", "direct"):
+            raise ValueError("pull_read must be 'fetch' or 'direct'")
+        self.pull_read = pull_read
         require_device()
         from .placement import block_workers, place
         n = int(topology.size)
@@ -85,16 +93,19 @@ class ChocoWorkerGroup:
         self.iter_dev = torch.zeros(1, dtype=torch.int64, device="cuda")   # device_round's counter
         self._pull = None
         if isinstance(comm, PullTransport):
-            # each rank's snapshot buffer holds two generations of its rows' messages; the apply
-            # reads message `slot` at slot_ptrs[slot]: local slots here, remote ones set per round
-            # by the gate to the partners' snapshots (placeholder: this rank's own snapshot 0)
+            # each rank's snapshot buffer holds two generations of its rows' messages; the gate
+            # points the remote entries of the slot table at the round's partners' snapshots
+            # (placeholder: this rank's own snapshot 0).  "fetch": mx_pull_fetch copies them into
+            # the receive slots and the apply reads local memory only; "direct": the apply reads
+            # every slot through the table, acquiring at system scope first (peer-reads bit)
             self._pull = comm.bind(self, row_bytes=self.msg_ld)
             ptrs = [self.msgs.data_ptr() + r * self.msg_ld for r in range(self.n_local)]
             ptrs += [self._pull.own + PULL_HEADER] * (self.engine.n_slots - self.n_local)
             self.slot_ptrs = torch.tensor(ptrs, dtype=torch.int64, device="cuda")
-            check(lib.mx_plan_set_peer_reads(self.engine.plan.data_ptr(), self.engine.T + 1, self.n_local,
-                                             self.engine.M, 1, stream_ptr()), "mx_plan_set_peer_reads")
-            self.engine.peer_reads = True
+            if pull_read == "direct":
+                check(lib.mx_plan_set_peer_reads(self.engine.plan.data_ptr(), self.engine.T + 1, self.n_local,
+                                                 self.engine.M, 1, stream_ptr()), "mx_plan_set_peer_reads")
+                self.engine.peer_reads = True
 
     @property
     def rows(self):
@@ -163,10 +174,11 @@ class ChocoWorkerGroup:
                                  stream_ptr(stream)), "mx_choco_apply")
 
     def _average_pull(self, it, stream=None):
-        """PullTransport averaging, three launches and no host wait: the local messages into
+        """PullTransport averaging, four launches and no host wait: the local messages into
         snapshot `round % 2` (system-scope release per workgroup), the gate (this rank's epoch out,
-        bounded waits for the partners', remote slots -> their snapshots), the apply reading the
-        partners' messages from their owners' HBM.  A gate that expired earlier raises here."""
+        bounded waits for the partners', remote slot table -> their snapshots), the fetch of the
+        round's partner messages from their owners' HBM into the receive slots, the apply.  A gate
+        that expired earlier raises here."""
         st = self._pull
         msg = st.error()
         if msg:
@@ -183,10 +195,19 @@ class ChocoWorkerGroup:
                                st.owner_dev.data_ptr(), st.ranks_dev.data_ptr(), tr.nranks, tr.rank, self.row_base,
                                self.n_local, self.msg_ld, par, st.round, self.slot_ptrs.data_ptr(), eng.n_slots,
                                tr.timeout_s, st.err_dev, s), "mx_pull_gate")
-        check(lib.mx_choco_apply_slots(self.x.data_ptr(), self.x_hat.data_ptr(), self.s.data_ptr(), self.ld,
-                                       self.numel, self.k, self.slot_ptrs.data_ptr(), eng.n_slots,
-                                       eng.plan.data_ptr(), int(it), self.n_local, eng.M, eng.alpha32, self.gamma32,
-                                       s), "mx_choco_apply_slots")
+        if self.pull_read == "direct":
+            check(lib.mx_choco_apply_slots(self.x.data_ptr(), self.x_hat.data_ptr(), self.s.data_ptr(), self.ld,
+                                           self.numel, self.k, self.slot_ptrs.data_ptr(), eng.n_slots,
+                                           eng.plan.data_ptr(), int(it), self.n_local, eng.M, eng.alpha32,
+                                           self.gamma32, s), "mx_choco_apply_slots")
+            return
+        mbase = self.msgs.data_ptr()
+        rec = eng.plan.data_ptr() + 4 * int(it) * eng.plan_words
+        check(lib.mx_pull_fetch(self.slot_ptrs.data_ptr(), self.n_local, eng.max_remote, rec,
+                                mbase + self.n_local * self.msg_ld, self.msg_ld, self.msg_bytes, s), "mx_pull_fetch")
+        check(lib.mx_choco_apply(self.x.data_ptr(), self.x_hat.data_ptr(), self.s.data_ptr(), self.ld, self.numel,
+                                 self.k, mbase, self.msg_ld, eng.n_slots, eng.plan.data_ptr(), int(it), self.n_local,
+                                 eng.M, eng.alpha32, self.gamma32, self.apply_work.data_ptr(), s), "mx_choco_apply")
 
     def device_round(self, stream=None):
         """Graph-replayable round at the device counter `self.iter_dev` (then advanced): top-k of

@@ -114,7 +114,65 @@ __global__ __launch_bounds__(64) void pull_gate_kernel(const uint8_t* __restrict
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");            // system scope
 }
+// The fetch of small remote payloads behind the gate (ChocoWorkerGroup under PullTransport: the
+// partners' top-k messages, 1.79 MB each at VGG-16 size).  Workgroup (b, j) copies part b of remote
+// slot j -- slot_ptrs[n_local + j], a peer's snapshot row pointed there by mx_pull_gate -- into
+// dst + j * dst_ld, for j below the round's remote count (plan record word [1]: plan_kernel numbers
+// the remote slots in the gate's order).  The bulk copy streams each message over its xGMI link
+// with 16-byte loads, 4 in flight per lane, so the apply pass that follows reads only local memory
+// (reading the messages in place inside the apply -- mx_choco_apply_slots -- costs every one of its
+// thousands of workgroups a system-scope acquire and a dependent table load: one row 45 -> 66 us,
+// profiles/r05y_slots_ab2.log).  Each workgroup acquires at system scope before its first load:
+// the gate, earlier on this stream, saw the owners' epochs, which they stored after a system-scope
+// release of the snapshot (the mixing kernels' protocol, mix.hip peer_acquire).
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const f4 g_cf4;
+typedef __attribute__((address_space(1))) f4 g_f4;
+
+__global__ __launch_bounds__(256) void pull_fetch_kernel(const int64_t* __restrict__ slots, int n_local,
+                                                         const int32_t* __restrict__ rec, char* __restrict__ dst,
+                                                         int64_t dst_ld, int64_t n16) {
+    const int j = blockIdx.y;
+    if (j >= rec[1]) return;                                   // block-uniform
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");          // system scope: buffer_inv sc0 sc1
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    g_cf4* src = (g_cf4*)slots[n_local + j];
+    g_f4* out = (g_f4*)(dst + (int64_t)j * dst_ld);
+    constexpr int U = 4;
+    const int64_t step = (int64_t)gridDim.x * 256;
+    int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    for (; i + (U - 1) * step < n16; i += U * step) {
+        f4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[u] = src[i + u * step];
+#pragma unroll
+        for (int u = 0; u < U; ++u) out[i + u * step] = v[u];
+    }
+    for (; i < n16; i += step) out[i] = src[i];
+}
 }  // namespace
+
+extern "C" int mx_pull_fetch(const int64_t* slot_ptrs_dev, int n_local, int max_remote, const int32_t* plan_rec_dev,
+                             void* dst, int64_t dst_ld, int64_t nbytes, void* stream) {
+    MX_CHECK(slot_ptrs_dev && plan_rec_dev && dst, "mx_pull_fetch: null pointer");
+    MX_CHECK(n_local >= 1 && max_remote >= 0 && max_remote <= 65535 && nbytes >= 0,
+             "mx_pull_fetch: n_local %d max_remote %d nbytes %lld", n_local, max_remote, (long long)nbytes);
+    const int64_t n16 = (nbytes + 15) / 16;
+    MX_CHECK(dst_ld >= 16 * n16 && dst_ld % 16 == 0 && (uintptr_t)dst % 16 == 0,
+             "mx_pull_fetch: dst_ld %lld must hold %lld bytes, 16-byte aligned", (long long)dst_ld,
+             (long long)(16 * n16));
+    if (max_remote == 0 || n16 == 0) return MX_OK;
+    int64_t nb = (n16 + 4 * 256 - 1) / (4 * 256);
+    if (nb > 64) nb = 64;
+    hipLaunchKernelGGL(pull_fetch_kernel, dim3((unsigned)nb, (unsigned)max_remote), dim3(256), 0,
+                       mx::as_stream(stream), slot_ptrs_dev, n_local, plan_rec_dev, static_cast<char*>(dst), dst_ld,
+                       n16);
+    MX_LAUNCH_CHECK();
+    return MX_OK;
+}
 
 extern "C" int mx_pull_gate(const uint8_t* flags_row_dev, uint8_t* prev_row_dev, int M, const int32_t* partner_dev,
                             int n_global, const int32_t* owner_dev, const mx_pull_rank* ranks_dev, int nranks,

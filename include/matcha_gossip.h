@@ -397,6 +397,14 @@ int mx_pull_gate(const uint8_t* flags_row_dev, uint8_t* prev_row_dev, int M, con
                  int n_global, const int32_t* owner_dev, const mx_pull_rank* ranks_dev, int nranks, int my_rank,
                  int row_base, int n_local, int64_t ld_bytes, int parity, uint64_t epoch, int64_t* slot_ptrs_dev,
                  int n_slots, double timeout_s, int32_t* err_dev, void* stream);
+/* The pull round's fetch of small payloads (ChocoWorkerGroup: the partners' compressed messages,
+ * in place of the sendrecv of communicator.py:214), on `stream` after mx_pull_gate: for every remote
+ * slot j below the round's remote count (word [1] of plan_rec_dev, the round's plan record), the
+ * first nbytes (rounded up to 16) at slot_ptrs_dev[n_local + j] -- a peer's snapshot row -- are
+ * copied to dst + j * dst_ld (dst_ld >= that, 16-byte aligned).  Every workgroup acquires at system
+ * scope first.  Grid: up to 64 workgroups per slot times max_remote slots. */
+int mx_pull_fetch(const int64_t* slot_ptrs_dev, int n_local, int max_remote, const int32_t* plan_rec_dev, void* dst,
+                  int64_t dst_ld, int64_t nbytes, void* stream);
 /* n zeroed int32 words of coherent mapped host memory: *host_out for the host, *dev_out for kernels. */
 int mx_host_words(int n, int32_t** host_out, int32_t** dev_out);
 int mx_host_words_free(int32_t* host);

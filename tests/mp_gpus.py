@@ -40,6 +40,8 @@ def main():
         "pull_rows_g2_placed": W.pull_rows_case(pkg, 2, 12_007, 20, placement="auto"),
         "pull_choco_g0_placed_long": W.choco_case(pkg, pkg.PullTransport(timeout_s=60), 20_011, 0.9, 12, seed=13,
                                                   placement="auto", back_to_back=True),
+        "pull_choco_direct_g0": W.choco_case(pkg, pkg.PullTransport(timeout_s=60), 20_011, 0.9, 8, seed=19,
+                                             back_to_back=True, pull_read="direct"),
     }
     torch.cuda.synchronize()
     flags = [None] * dist.get_world_size()

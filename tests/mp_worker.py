@@ -96,7 +96,7 @@ def pull_rows_case(pkg, gid, P, rounds, seed=21, placement=None):
     return bool(np.array_equal(got.view(np.uint32), X.view(np.uint32))) and adhoc > 0
 
 
-def choco_case(pkg, T, P, ratio, rounds, seed=9, placement=None, back_to_back=False):
+def choco_case(pkg, T, P, ratio, rounds, seed=9, placement=None, back_to_back=False, pull_read="fetch"):
     """x and x_hat of every worker vs the oracle's Choco rounds; with back_to_back all rounds are
     enqueued by step() with no host wait between them (the pull transport's device gate alone
     orders them across ranks)"""
@@ -108,8 +108,9 @@ def choco_case(pkg, T, P, ratio, rounds, seed=9, placement=None, back_to_back=Fa
     flags = (rng.uniform(size=(rounds, M)) < 0.6).astype(np.uint8)
     flags[0] = 1
     topo = Topo(gp.neighbors_info, 2 / 7, flags)
+    kw = {"pull_read": pull_read} if isinstance(T, pkg.PullTransport) else {}
     grp = pkg.ChocoWorkerGroup(topo, numel=P, ratio=ratio, consensus_lr=0.1, rank=rank, nranks=world, comm=T,
-                               placement=placement)
+                               placement=placement, **kw)
     X = np.stack([O.synth(99 + i, P) for i in range(n)])
     XH = np.zeros_like(X)
     S = np.zeros_like(X)
@@ -228,6 +229,8 @@ def main():
         "choco_g0_pull_long_placed": choco_case(pkg, pkg.PullTransport(), 20_011, 0.9, 14, seed=13,
                                                 placement="auto", back_to_back=True),
         "choco_g0_pull_rows_placed": choco_pull_rows_case(pkg, 15_013, 16, placement="auto"),
+        "choco_g0_pull_direct_long_placed": choco_case(pkg, pkg.PullTransport(), 20_011, 0.9, 14, seed=17,
+                                                       placement="auto", back_to_back=True, pull_read="direct"),
         # edge shapes under pull: one entry per message (k = 1, the reference's argmax branch) on a
         # row shorter than one 4096-element tile, and an odd k on a ragged last tile
         "choco_g0_pull_k1": choco_case(pkg, pkg.PullTransport(), 1_000, 0.9995, 5, seed=3, back_to_back=True),

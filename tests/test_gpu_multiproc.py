@@ -70,7 +70,8 @@ def test_bench_multiprocess_path(nproc):
     assert out["allreduce_baseline"]["parity_ok"] is True          # all-gather + mx_mean_rows_to, tree order
     assert out["choco"]["topk"]["calls_per_row"] > 0
     # Choco at N > 1: the RCCL-form (gloo here) and pull forms calibrated, the faster timed
-    assert set(out["choco"]["calib_ms"]) == {"rccl", "pull"} and out["choco"]["form"] in ("rccl", "pull")
+    assert set(out["choco"]["calib_ms"]) == {"rccl", "pull", "pull_direct"}
+    assert out["choco"]["form"] in ("rccl", "pull", "pull_direct")
     assert out["choco"]["pull_unavailable"] is None
     cp = out["choco"]["predicted"]
     for f in ("rccl", "pull"):
@@ -139,7 +140,7 @@ def test_bench_multiprocess_overlap_forms(nproc, overlap, pull):
         assert out["overlap"]["pull_rounds"] >= 6, out["overlap"]
         assert out["overlap"]["pull_gate_error"] is None, out["overlap"]
         ch = out["choco"]
-        assert ch["form"] == "pull" and ch["pull_rounds"] >= 6 and ch["pull_gate_error"] is None, ch
+        assert ch["form"] in ("pull", "pull_direct") and ch["pull_rounds"] >= 6 and ch["pull_gate_error"] is None, ch
         assert ch["parity_ok"] is True, ch
     elif overlap == "off" and pull == "off":
         assert out["overlap"] is None

@@ -101,3 +101,66 @@ def test_mean_kernel_name_matches_dispatch(pkg, O, nrows, count, order):
     pkg._lib.check(pkg.lib.mx_mean_rows(dev.data_ptr(), nrows, ld, count, order, out.data_ptr(), None))
     want = O.central_mean(rows[:, :count], "tree" if order == 0 else "sequential")
     assert np.array_equal(out.cpu().numpy().view(np.uint32), want.view(np.uint32))
+
+
+class _NoTransfer:
+    """a transport that moves nothing (the received message slots are filled by the test)"""
+    handle = None
+
+    def __init__(self, rank, nranks):
+        self.rank, self.nranks = rank, nranks
+
+    def exchange_round(self, *args):
+        return 0
+
+
+@pytest.mark.parametrize("rows,P", [(8, 300_007), (1, 70_001)])
+def test_choco_apply_slots_equals_strided(pkg, rows, P):
+    """mx_choco_apply_slots (the pull transport's apply: message `slot` read at a device table's
+    address) computes mx_choco_apply's bits: the round's messages are copied to a second buffer in
+    a shuffled slot order and the table points at them, the plan records carry the peer-reads bit
+    (every workgroup's system-scope acquire runs); x / x_hat / s uint32-equal after each of 3 rounds
+    -- 8 rows on one GPU, and one row of an 8-GPU layout whose received slots hold the top-k
+    messages of other rows (reference: communicator.py:200-230)."""
+    from conftest import Topo
+    gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, 8, 4, True)
+    M = len(gp.neighbors_info)
+    topo = Topo(gp.neighbors_info, 2 / 7, np.ones((4, M), np.uint8))
+    kw = dict(numel=P, ratio=0.99, consensus_lr=0.1)
+    if rows == 1:
+        kw.update(rank=3, nranks=8, comm=_NoTransfer(3, 8))
+    a = pkg.ChocoWorkerGroup(topo, **kw)
+    b = pkg.ChocoWorkerGroup(topo, **kw)
+    L, eng = pkg.lib, b.engine
+    n_slots = eng.n_slots
+    assert a.n_local == rows and (rows == 8 or n_slots > rows)
+    for g in (a, b):
+        for r in range(g.n_local):
+            pkg._lib.check(pkg.lib.mx_synth_fill(g.rows[r].data_ptr(), P, 50 + r, None))
+    pkg._lib.check(L.mx_plan_set_peer_reads(eng.plan.data_ptr(), eng.T + 1, b.n_local, eng.M, 1, None))
+    order = np.random.RandomState(7).permutation(n_slots)
+    shuffled = torch.empty_like(b.msgs)
+    table = torch.tensor([shuffled.data_ptr() + int(order[s]) * b.msg_ld for s in range(n_slots)],
+                         dtype=torch.int64, device="cuda")
+    stand_in = torch.from_numpy(np.stack([np.random.RandomState(90 + s).uniform(-1, 1, P).astype(np.float32)
+                                          for s in range(n_slots)])).cuda()
+    for it in range(3):
+        for g in (a, b):
+            if rows == 1:                                # received slots: the top-k of other rows
+                for s in range(g.n_local, n_slots):
+                    pkg._lib.check(L.mx_topk_abs_diff_rows(stand_in[s].data_ptr(), None, P, 1, P, g.k,
+                                                           g.msgs.data_ptr() + s * g.msg_ld, g.msg_ld,
+                                                           4 * g.kpad, g.bnd_off, g.work.data_ptr(), g.work_ld,
+                                                           None), "mx_topk_abs_diff_rows")
+            g.compress(it)
+        a.average(it)                                    # mx_choco_apply over the strided slots
+        for s in range(n_slots):
+            o = int(order[s]) * b.msg_ld
+            shuffled[o:o + b.msg_ld].copy_(b.msgs[s * b.msg_ld:(s + 1) * b.msg_ld])
+        pkg._lib.check(L.mx_choco_apply_slots(b.x.data_ptr(), b.x_hat.data_ptr(), b.s.data_ptr(), b.ld, P, b.k,
+                                              table.data_ptr(), n_slots, eng.plan.data_ptr(), it, b.n_local,
+                                              eng.M, eng.alpha32, b.gamma32, None), "mx_choco_apply_slots")
+        torch.cuda.synchronize()
+        for u, v in ((a.x, b.x), (a.x_hat, b.x_hat), (a.s, b.s)):
+            assert torch.equal(u.view(torch.int32), v.view(torch.int32)), it
+    assert bool((a.s != 0).any()) and bool((a.x_hat != 0).any())
