@@ -56,6 +56,12 @@ def test_invalid_arguments_report_errors(pkg):
                              out.ctypes.data, ctypes.byref(pos), None)
     assert rc == -1 and b"> 1" in L.mx_last_error()
     assert L.mx_topk_abs_diff(None, None, 10, 11, None, None, None, None) == -1
+    # the pull transport's Choco entries validate before touching a device
+    assert L.mx_pull_fetch(None, 1, 2, None, None, 256, 100, None) == -1 and b"null" in L.mx_last_error()
+    fake = ctypes.c_void_p(256)
+    assert L.mx_pull_fetch(fake, 1, 2, fake, fake, 96, 100, None) == -1 and b"dst_ld" in L.mx_last_error()
+    assert L.mx_choco_apply_slots(fake, fake, fake, 8, 8, 1, None, 2, fake, 0, 1, 1, 0.5, 0.1, None) == -1
+    assert b"slot table" in L.mx_last_error()
 
 
 def test_dropin_shims_resolve(pkg):
