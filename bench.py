@@ -649,7 +649,7 @@ def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99
     for name, mode in (("pull", "fetch"), ("pull_direct", "direct")):
         if not (any_remote and pull != "off") or pull_err is not None:
             break
-        gp = None
+        gp, err = None, None
         try:
             gp = pkg.ChocoWorkerGroup(GP, numel=P, ratio=ratio, consensus_lr=gamma, rank=rank, nranks=world,
                                       comm=pkg.PullTransport(timeout_s=PULL_TIMEOUT_S), placement=placement,
@@ -659,13 +659,14 @@ def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99
                 gp.step(it)
             gp.wait_round()                      # a gate that expired in the warmup raises here
         except pkg.MXError as e:
-            pull_err = str(e)
-        if gp is not None:
-            if max_over_ranks(float(pull_err is not None), world, dev) > 0:
-                pull_err = pull_err or "a peer's pull warmup failed"
-                gp.close()
-            else:
-                forms[name] = gp
+            err = str(e)
+        if gp is None:                           # bind failed: on every rank (all-or-nothing)
+            pull_err = f"{name}: {err}"
+        elif max_over_ranks(float(err is not None), world, dev) > 0:
+            pull_err = f"{name}: {err or 'a peer warmup failed'}"
+            gp.close()
+        else:
+            forms[name] = gp
     if len(forms) > 1:
         calib = {name: 1e3 * timed_loop(g.step, W, R, world, dev) / R for name, g in forms.items()}
         if pull == "on":
