@@ -1635,13 +1635,23 @@ struct Msg {
 };
 
 // message layout (mx_choco_msg_bytes): vals f32[kpad] | idx int64[k] | bnd int32[ntiles + 1]
-// SP = false: message `slot` at msgs + slot * msg_ld (one buffer); SP = true (mx_choco_apply_slots,
-// the pull transport): `msgs` is a device table of int64 message addresses, one per slot -- the
-// local rows' messages here, the partners' in their owners' IPC-mapped snapshot buffers
-template <bool SP>
-__device__ __forceinline__ Msg msg_at(const char* msgs, int64_t msg_ld, int64_t kpad, int64_t k, int slot) {
-    const char* b = SP ? reinterpret_cast<const char*>(reinterpret_cast<const int64_t*>(msgs)[slot])
-                       : msgs + (int64_t)slot * msg_ld;
+// Where message `slot` starts: MsgStride -- one buffer, msg_ld bytes per slot (mx_choco_apply);
+// MsgTable -- a device table of int64 addresses, one per slot (mx_choco_apply_slots, the pull
+// transport: the local rows' messages here, the partners' in their owners' IPC-mapped snapshot
+// buffers); the persistent apply copies either into LDS once per workgroup (MsgTable over LDS).
+struct MsgStride {
+    const char* m;
+    int64_t ld;
+    __device__ __forceinline__ const char* base(int slot) const { return m + (int64_t)slot * ld; }
+};
+struct MsgTable {
+    const int64_t* tab;
+    __device__ __forceinline__ const char* base(int slot) const { return reinterpret_cast<const char*>(tab[slot]); }
+};
+
+template <class MS>
+__device__ __forceinline__ Msg msg_at(const MS& ms, int64_t kpad, int64_t k, int slot) {
+    const char* b = ms.base(slot);
     return Msg{reinterpret_cast<const float*>(b), reinterpret_cast<const int64_t*>(b + 4 * kpad),
                reinterpret_cast<const int32_t*>(b + 4 * kpad + 8 * k)};
 }
@@ -1680,15 +1690,12 @@ __device__ __forceinline__ const int32_t* round_rec(const int32_t* rec, const in
 // GRAN: floats per dirty granule of s / x_hat written back.  16 (64 B) is the one instantiated: 32-B
 // granules measured 8 rows 639 -> 715 us per round (same-box A/B; partial non-temporal line writes),
 // one row unchanged
-template <bool NT, int GRAN, bool SP>
+template <bool NT, int GRAN, class MS>
 __device__ __forceinline__ void apply_tile(float* __restrict__ x, float* __restrict__ xh, float* __restrict__ s,
-                                           int64_t ld, int64_t P, const char* __restrict__ msgs, int64_t msg_ld,
-                                           int64_t kpad, int64_t k, const int32_t* __restrict__ rec, int n_local,
-                                           int M, float alpha, float g, float* ls, float* lh, uint8_t* ds,
-                                           uint8_t* dh) {
+                                           int64_t ld, int64_t P, const MS& ms, int64_t kpad, int64_t k,
+                                           const int32_t* __restrict__ rec, int n_local, int M, float alpha, float g,
+                                           float* ls, float* lh, uint8_t* ds, uint8_t* dh, int r, int64_t t) {
     constexpr int kGran = GRAN;
-    const int r = blockIdx.y;
-    const int64_t t = blockIdx.x;
     const int64_t t0 = t * kTile;
     const int len = (int)(P - t0 < kTile ? P - t0 : kTile);
     float* xr = x + (int64_t)r * ld + t0;
@@ -1718,7 +1725,7 @@ __device__ __forceinline__ void apply_tile(float* __restrict__ x, float* __restr
     const int d = deg[r];
     const int32_t* src = deg + 2 * n_local + r * M;
     for (int e = 0; e < d; ++e) {              // partners, ascending matching order
-        const Msg m = msg_at<SP>(msgs, msg_ld, kpad, k, src[e]);
+        const Msg m = msg_at(ms, kpad, k, src[e]);
         const int lo = max(m.bnd[t], 0), hi = min(m.bnd[t + 1], (int)k);   // clamped: a received
         for (int q = lo + tid; q < hi; q += kTPB) {                        // message is not trusted
             const int c = (int)(m.ix[q] - t0);                             // to stay in range
@@ -1730,7 +1737,7 @@ __device__ __forceinline__ void apply_tile(float* __restrict__ x, float* __restr
     }
     {                                          // own message
         const float sw = __int_as_float(deg[n_local + r]);
-        const Msg m = msg_at<SP>(msgs, msg_ld, kpad, k, r);
+        const Msg m = msg_at(ms, kpad, k, r);
         const int lo = max(m.bnd[t], 0), hi = min(m.bnd[t + 1], (int)k);
         for (int q = lo + tid; q < hi; q += kTPB) {
             const int c = (int)(m.ix[q] - t0);
@@ -1779,7 +1786,12 @@ __global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, floa
     peer_acquire(rec[2]);
     __shared__ float ls[kTile], lh[kTile];
     __shared__ uint8_t ds[kTile / GRAN], dh[kTile / GRAN];
-    apply_tile<NT, GRAN, SP>(x, xh, s, ld, P, msgs, msg_ld, kpad, k, rec, n_local, M, alpha, g, ls, lh, ds, dh);
+    if constexpr (SP)
+        apply_tile<NT, GRAN>(x, xh, s, ld, P, MsgTable{reinterpret_cast<const int64_t*>(msgs)}, kpad, k, rec, n_local,
+                             M, alpha, g, ls, lh, ds, dh, blockIdx.y, blockIdx.x);
+    else
+        apply_tile<NT, GRAN>(x, xh, s, ld, P, MsgStride{msgs, msg_ld}, kpad, k, rec, n_local, M, alpha, g, ls, lh,
+                             ds, dh, blockIdx.y, blockIdx.x);
 }
 
 // The same pass with the message phase's global reads moved under the tile's stream: the plan
@@ -1791,30 +1803,20 @@ __global__ __launch_bounds__(kTPB) void apply_kernel(float* __restrict__ x, floa
 // are loaded as in the plain kernel.  Same order of updates, same results.
 constexpr int kPfMsgs = 8;
 
-template <bool NT, bool SP>
-__global__ __launch_bounds__(kTPB) void apply_kernel_pf(float* __restrict__ x, float* __restrict__ xh,
-                                                        float* __restrict__ s, int64_t ld, int64_t P,
-                                                        const char* __restrict__ msgs, int64_t msg_ld,
-                                                        int64_t kpad, int64_t k,
-                                                        const int32_t* __restrict__ rec_in,
-                                                        const int64_t* __restrict__ iter_dev, int64_t n_iters,
-                                                        int64_t words, int n_local, int M,
-                                                        float alpha, float g) {
-    const int32_t* rec = round_rec(rec_in, iter_dev, n_iters, words);
-    if (!rec) return;
-    peer_acquire(rec[2]);
+template <bool NT, class MS>
+__device__ __forceinline__ void apply_pf_tile(float* __restrict__ x, float* __restrict__ xh, float* __restrict__ s,
+                                              int64_t ld, int64_t P, const MS& ms, int64_t kpad, int64_t k,
+                                              const int32_t* __restrict__ rec, int n_local, int M, float alpha,
+                                              float g, float* ls, float* lh, uint8_t* ds, uint8_t* dh, int r,
+                                              int64_t t) {
     constexpr int kGran = 16;
-    const int r = blockIdx.y;
-    const int64_t t = blockIdx.x;
     const int64_t t0 = t * kTile;
     const int len = (int)(P - t0 < kTile ? P - t0 : kTile);
     float* xr = x + (int64_t)r * ld + t0;
     float* sr = s + (int64_t)r * ld + t0;
     float* hr = xh + (int64_t)r * ld + t0;
-    __shared__ float ls[kTile], lh[kTile];
-    __shared__ uint8_t ds[kTile / kGran], dh[kTile / kGran];
     if (!(len == kTile && (((uintptr_t)xr | (uintptr_t)sr | (uintptr_t)hr) & 15) == 0)) {   // partial /
-        apply_tile<NT, 16, SP>(x, xh, s, ld, P, msgs, msg_ld, kpad, k, rec, n_local, M, alpha, g, ls, lh, ds, dh);
+        apply_tile<NT, 16>(x, xh, s, ld, P, ms, kpad, k, rec, n_local, M, alpha, g, ls, lh, ds, dh, r, t);
         return;                                                                         // unaligned tile
     }
     // from here on the whole-tile path is branch-free up to the message phase, so the waitcnt pass
@@ -1835,7 +1837,7 @@ __global__ __launch_bounds__(kTPB) void apply_kernel_pf(float* __restrict__ x, f
         const int e = lane < kPfMsgs ? lane : 0;
         const int sl = lane < kPfMsgs && e < d ? src[e] : r;
         my_sl = sl;
-        const Msg m = msg_at<SP>(msgs, msg_ld, kpad, k, sl);
+        const Msg m = msg_at(ms, kpad, k, sl);
         if (lane < kPfMsgs && e < nm) {
             my_lo = max(m.bnd[t], 0);              // clamped: a received message is not trusted
             my_hi = min(m.bnd[t + 1], (int)k);     // to stay in range
@@ -1857,7 +1859,7 @@ __global__ __launch_bounds__(kTPB) void apply_kernel_pf(float* __restrict__ x, f
         plo[e] = __builtin_amdgcn_readlane(my_lo, e);
         phi[e] = __builtin_amdgcn_readlane(my_hi, e);
         const int q = plo[e] + tid < phi[e] ? plo[e] + tid : 0;     // clamped: loads stay unconditional
-        const Msg m = msg_at<SP>(msgs, msg_ld, kpad, k, __builtin_amdgcn_readlane(my_sl, e));
+        const Msg m = msg_at(ms, kpad, k, __builtin_amdgcn_readlane(my_sl, e));
         pix[e] = m.ix[q];
         pv[e] = m.v[q];
     }
@@ -1885,14 +1887,14 @@ __global__ __launch_bounds__(kTPB) void apply_kernel_pf(float* __restrict__ x, f
         const bool own = e == d;
         if (plo[e] + tid < phi[e]) upd(own, pix[e], pv[e]);
         if (phi[e] - plo[e] > kTPB) {
-            const Msg m = msg_at<SP>(msgs, msg_ld, kpad, k, __builtin_amdgcn_readlane(my_sl, e));
+            const Msg m = msg_at(ms, kpad, k, __builtin_amdgcn_readlane(my_sl, e));
             for (int q = plo[e] + kTPB + tid; q < phi[e]; q += kTPB) upd(own, m.ix[q], m.v[q]);
         }
         __syncthreads();                       // a later message may touch the same element
     }
     for (int e = kPfMsgs; e < nm; ++e) {
         const bool own = e == d;
-        const Msg m = msg_at<SP>(msgs, msg_ld, kpad, k, own ? r : src[e]);
+        const Msg m = msg_at(ms, kpad, k, own ? r : src[e]);
         const int lo = max(m.bnd[t], 0), hi = min(m.bnd[t + 1], (int)k);
         for (int q = lo + tid; q < hi; q += kTPB) upd(own, m.ix[q], m.v[q]);
         __syncthreads();
@@ -1908,6 +1910,59 @@ __global__ __launch_bounds__(kTPB) void apply_kernel_pf(float* __restrict__ x, f
         st4<NT>(a, reinterpret_cast<f4*>(xr) + q);
         if (ds[q / (kGran / 4)]) st4<NT>(s4, reinterpret_cast<f4*>(sr) + q);
         if (dh[q / (kGran / 4)]) st4<NT>(h4, reinterpret_cast<f4*>(hr) + q);
+    }
+}
+
+template <bool NT, bool SP>
+__global__ __launch_bounds__(kTPB) void apply_kernel_pf(float* __restrict__ x, float* __restrict__ xh,
+                                                        float* __restrict__ s, int64_t ld, int64_t P,
+                                                        const char* __restrict__ msgs, int64_t msg_ld,
+                                                        int64_t kpad, int64_t k,
+                                                        const int32_t* __restrict__ rec_in,
+                                                        const int64_t* __restrict__ iter_dev, int64_t n_iters,
+                                                        int64_t words, int n_local, int M,
+                                                        float alpha, float g) {
+    const int32_t* rec = round_rec(rec_in, iter_dev, n_iters, words);
+    if (!rec) return;
+    peer_acquire(rec[2]);
+    __shared__ float ls[kTile], lh[kTile];
+    __shared__ uint8_t ds[kTile / 16], dh[kTile / 16];
+    if constexpr (SP)
+        apply_pf_tile<NT>(x, xh, s, ld, P, MsgTable{reinterpret_cast<const int64_t*>(msgs)}, kpad, k, rec, n_local,
+                          M, alpha, g, ls, lh, ds, dh, blockIdx.y, blockIdx.x);
+    else
+        apply_pf_tile<NT>(x, xh, s, ld, P, MsgStride{msgs, msg_ld}, kpad, k, rec, n_local, M, alpha, g, ls, lh, ds,
+                          dh, blockIdx.y, blockIdx.x);
+}
+
+// Persistent form (a grid of about the co-resident workgroups, each looping over the tiles
+// blockIdx.x, + gridDim.x, ... of row blockIdx.y): per workgroup, not per tile, the pull
+// transport's system-scope acquire (peer-reads bit) and the message addresses -- the slot table
+// (SP) or the strided addresses -- loaded once into LDS.  The per-tile work is apply_pf_tile's.
+constexpr int kLdsSlots = 256;
+
+template <bool NT, bool SP>
+__global__ __launch_bounds__(kTPB) void apply_kernel_persist(float* __restrict__ x, float* __restrict__ xh,
+                                                             float* __restrict__ s, int64_t ld, int64_t P,
+                                                             const char* __restrict__ msgs, int64_t msg_ld,
+                                                             int64_t kpad, int64_t k,
+                                                             const int32_t* __restrict__ rec_in,
+                                                             const int64_t* __restrict__ iter_dev, int64_t n_iters,
+                                                             int64_t words, int n_local, int M,
+                                                             float alpha, float g, int n_slots, int64_t ntiles) {
+    const int32_t* rec = round_rec(rec_in, iter_dev, n_iters, words);
+    if (!rec) return;
+    peer_acquire(rec[2]);
+    __shared__ float ls[kTile], lh[kTile];
+    __shared__ uint8_t ds[kTile / 16], dh[kTile / 16];
+    __shared__ int64_t ltab[kLdsSlots];
+    for (int i = threadIdx.x; i < n_slots; i += kTPB)
+        ltab[i] = SP ? reinterpret_cast<const int64_t*>(msgs)[i] : (int64_t)(msgs + (int64_t)i * msg_ld);
+    __syncthreads();
+    const MsgTable ms{ltab};
+    for (int64_t t = blockIdx.x; t < ntiles; t += gridDim.x) {
+        apply_pf_tile<NT>(x, xh, s, ld, P, ms, kpad, k, rec, n_local, M, alpha, g, ls, lh, ds, dh, blockIdx.y, t);
+        __syncthreads();                       // the next tile restages ls / lh / ds / dh
     }
 }
 
@@ -1930,6 +1985,7 @@ int g_compact_blocks = 0;     // persistent compaction blocks over all rows; 0 =
 int g_sample_pieces = 1;      // sampled 1024-element pieces per wave (sample_kernel grid)
 int g_apply_pf = 1;           // apply pass: 1 message entries prefetched under the tile stream, 0 plain
 int g_apply_nt = -1;          // apply pass non-temporal accesses: -1 auto (only with several rows), 0, 1
+int g_apply_persist = -1;     // persistent apply (apply_kernel_persist): -1 auto (the slot-table form only), 0, 1
 int g_compact_wave = 0;       // compaction with wave-owned chunks: 0 = off (block-owned chunks), c > 0 = about
                               // c chunks per wave
 int g_compact_pf2 = 0;        // compaction: 1 = two whole chunks in flight per wave (PF2), 0 = one
@@ -1994,6 +2050,9 @@ int64_t hist_capacity(const void* fn) {
     return cap;
 }
 
+// workgroups of the persistent apply the chip holds at once (x 7/8, as hist_capacity)
+int64_t persist_capacity(const void* fn) { return hist_capacity(fn); }
+
 int64_t sample_stride(int64_t P) {
     const int64_t nc = n_chunks(P);
     int64_t S = g_sample_stride > 0 ? g_sample_stride : (nc * kChunk) / kSampleTarget;
@@ -2030,6 +2089,11 @@ extern "C" int mx_topk_set(const char* key, int64_t value) {
     if (!strcmp(key, "apply_nt")) {
         MX_CHECK(value >= -1 && value <= 1, "mx_topk_set: apply_nt %lld", (long long)value);
         g_apply_nt = (int)value;
+        return MX_OK;
+    }
+    if (!strcmp(key, "apply_persist")) {
+        MX_CHECK(value >= -1 && value <= 1, "mx_topk_set: apply_persist %lld", (long long)value);
+        g_apply_persist = (int)value;
         return MX_OK;
     }
     if (!strcmp(key, "apply_pf")) {
@@ -2107,6 +2171,7 @@ extern "C" int64_t mx_topk_get(const char* key) {
     if (key && !strcmp(key, "apply_nt")) return g_apply_nt;
     if (key && !strcmp(key, "compact_store")) return g_compact_store;
     if (key && !strcmp(key, "apply_pf")) return g_apply_pf;
+    if (key && !strcmp(key, "apply_persist")) return g_apply_persist;
     if (key && !strcmp(key, "compact_pf2")) return g_compact_pf2;
     if (key && !strcmp(key, "compact_wave")) return g_compact_wave;
     if (key && !strcmp(key, "select")) return g_select;
@@ -2379,6 +2444,23 @@ int choco_apply(float* x, float* xhat, float* s, int64_t ld, int64_t P, int64_t 
     const char* m = static_cast<const char*>(msgs);
     MX_CHECK(nt <= 0x7fffffff, "mx_choco_apply: P too large");
     const bool nt_hint = g_apply_nt < 0 ? n_local > 1 : g_apply_nt > 0;
+    // auto: only the slot-table form of ONE row (the direct pull read of config 4's share at N = 8:
+    // 66 -> 57 us; with 2-8 rows, and for the strided form, the per-tile grid is faster --
+    // tools/choco_slots_ab.py, profiles/r05p2_apply_forms_ab.log)
+    const bool persist = n_slots <= kLdsSlots &&
+                         (g_apply_persist > 0 || (g_apply_persist < 0 && slot_table && n_local == 1));
+    if (persist) {
+        auto kern = slot_table ? (nt_hint ? apply_kernel_persist<true, true> : apply_kernel_persist<false, true>)
+                               : (nt_hint ? apply_kernel_persist<true, false> : apply_kernel_persist<false, false>);
+        // about the co-resident workgroups over the rows, an equal tile count each
+        const int64_t cap = persist_capacity(reinterpret_cast<const void*>(kern)) / n_local;
+        const int64_t per = (nt + (cap > 0 ? cap : 1) - 1) / (cap > 0 ? cap : 1);
+        const int64_t gx = (nt + per - 1) / per;
+        hipLaunchKernelGGL(kern, dim3((unsigned)gx, n_local), dim3(kTPB), 0, st, x, xhat, s, ld, P, m, msg_ld_bytes,
+                           kpad, k, rec, iter_dev, iter, words, n_local, M, alpha, gamma, n_slots, nt);
+        MX_LAUNCH_CHECK();
+        return MX_OK;
+    }
     auto kern = slot_table ? (g_apply_pf ? (nt_hint ? apply_kernel_pf<true, true> : apply_kernel_pf<false, true>)
                                          : (nt_hint ? apply_kernel<true, 16, true> : apply_kernel<false, 16, true>))
                            : (g_apply_pf ? (nt_hint ? apply_kernel_pf<true, false> : apply_kernel_pf<false, false>)

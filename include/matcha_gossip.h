@@ -212,6 +212,9 @@ size_t mx_topk_work_bytes(int64_t P);
  * 0 / 1 forced;
  * "apply_pf" = 1 (default): mx_choco_apply prefetches every message's tile bounds and first entries
  * under the tile stream, 0: the plain kernel (bounds and entries loaded per message);
+ * "apply_persist" = -1 (default): the slot-table apply (mx_choco_apply_slots) of ONE row runs
+ * persistent workgroups that acquire and load the message addresses once each, every other apply
+ * a workgroup per tile; 0 / 1: one form for all;
  * "select" = 0 (default): the selection after the compaction as four passes (candidate histograms
  * of the 10 and 9 low digits, threshold mark, placement), 1: as ONE launch (select_kernel: B
  * workgroups of 1024 threads per row meeting at two row barriers; measured slower);

@@ -114,14 +114,15 @@ class _NoTransfer:
         return 0
 
 
-@pytest.mark.parametrize("rows,P", [(8, 300_007), (1, 70_001)])
-def test_choco_apply_slots_equals_strided(pkg, rows, P):
+@pytest.mark.parametrize("rows,P,persist", [(8, 300_007, -1), (1, 70_001, -1), (8, 300_007, 1), (1, 70_001, 0)])
+def test_choco_apply_slots_equals_strided(pkg, rows, P, persist):
     """mx_choco_apply_slots (the pull transport's apply: message `slot` read at a device table's
     address) computes mx_choco_apply's bits: the round's messages are copied to a second buffer in
     a shuffled slot order and the table points at them, the plan records carry the peer-reads bit
     (every workgroup's system-scope acquire runs); x / x_hat / s uint32-equal after each of 3 rounds
     -- 8 rows on one GPU, and one row of an 8-GPU layout whose received slots hold the top-k
-    messages of other rows (reference: communicator.py:200-230)."""
+    messages of other rows; the persistent and the per-tile apply forced both ways (knob
+    apply_persist) (reference: communicator.py:200-230)."""
     from conftest import Topo
     gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, 8, 4, True)
     M = len(gp.neighbors_info)
@@ -157,10 +158,14 @@ def test_choco_apply_slots_equals_strided(pkg, rows, P):
         for s in range(n_slots):
             o = int(order[s]) * b.msg_ld
             shuffled[o:o + b.msg_ld].copy_(b.msgs[s * b.msg_ld:(s + 1) * b.msg_ld])
-        pkg._lib.check(L.mx_choco_apply_slots(b.x.data_ptr(), b.x_hat.data_ptr(), b.s.data_ptr(), b.ld, P, b.k,
-                                              table.data_ptr(), n_slots, eng.plan.data_ptr(), it, b.n_local,
-                                              eng.M, eng.alpha32, b.gamma32, None), "mx_choco_apply_slots")
-        torch.cuda.synchronize()
+        pkg._lib.check(L.mx_topk_set(b"apply_persist", persist))
+        try:
+            pkg._lib.check(L.mx_choco_apply_slots(b.x.data_ptr(), b.x_hat.data_ptr(), b.s.data_ptr(), b.ld, P, b.k,
+                                                  table.data_ptr(), n_slots, eng.plan.data_ptr(), it, b.n_local,
+                                                  eng.M, eng.alpha32, b.gamma32, None), "mx_choco_apply_slots")
+            torch.cuda.synchronize()
+        finally:
+            pkg._lib.check(L.mx_topk_set(b"apply_persist", -1))
         for u, v in ((a.x, b.x), (a.x_hat, b.x_hat), (a.s, b.s)):
             assert torch.equal(u.view(torch.int32), v.view(torch.int32)), it
     assert bool((a.s != 0).any()) and bool((a.x_hat != 0).any())

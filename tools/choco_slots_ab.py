@@ -2,9 +2,11 @@
 mx_choco_apply_slots (message addresses from a device slot table, the pull transport's form; here
 the table points at the same local buffer, the plan records carry the peer-reads bit so every
 workgroup's system-scope acquire runs).  VGG-16 size (P = 14,774,436, top-1 %), 8 rows on one GPU
-and one row of the 8-GPU layout (received slots = top-k messages of other synthetic rows).
-Four variants (strided / slot table, each without and with the peer-reads bit) to separate the
-table's cost from the per-workgroup acquire's.  Apply launches alone, per-launch HIP events, median
+and rank 0's 4 / 2 / 1 rows of the 2 / 4 / 8-GPU layouts (received slots = top-k messages of other
+synthetic rows).
+Variants: strided / slot table, each without and with the peer-reads bit (the table's cost vs the
+per-workgroup acquire's), the slot-table form per tile (apply_persist 0) and persistent (the
+default for it: acquire and addresses once per workgroup), and the strided form persistent.  Apply launches alone, per-launch HIP events, median
 of K, the variants interleaved 4 times.  One JSON line."""
 import importlib
 import json
@@ -28,10 +30,10 @@ gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, 8, 4, True)
 M = len(gp.neighbors_info)
 topo = Topo(gp.neighbors_info, 2 / 7, np.ones((K + 8, M), np.uint8))
 out = {"P": P, "K": K}
-for rows in (8, 1):
+for rows in (8, 4, 2, 1):
     kw = dict(numel=P, ratio=0.99, consensus_lr=0.1)
-    if rows == 1:
-        kw.update(rank=0, nranks=8, comm=NullComm(0, 8), placement="auto")
+    if rows < 8:                                  # rank 0's block of the 8 // rows - GPU layout
+        kw.update(rank=0, nranks=8 // rows, comm=NullComm(0, 8 // rows))
     g = pkg.ChocoWorkerGroup(topo, **kw)
     eng = g.engine
     for s in range(g.n_local, eng.n_slots):
@@ -61,8 +63,17 @@ for rows in (8, 1):
                                                   g.n_local, eng.M, eng.alpha32, g.gamma32, None))
         return f
 
-    variants = {"strided": strided(eng.plan), "strided_peer_bit": strided(plan_pr), "slots": slots(eng.plan),
-                "slots_peer_bit": slots(plan_pr)}
+    def knob(fn, persist):
+        def f(it):
+            pkg._lib.check(L.mx_topk_set(b"apply_persist", persist))
+            fn(it)
+            pkg._lib.check(L.mx_topk_set(b"apply_persist", -1))
+        return f
+
+    variants = {"strided": strided(eng.plan), "strided_peer_bit": strided(plan_pr),
+                "strided_persist": knob(strided(eng.plan), 1),
+                "slots_peer_bit_nonpersist": knob(slots(plan_pr), 0),
+                "slots": slots(eng.plan), "slots_peer_bit": slots(plan_pr)}
     res = {k: [] for k in variants}
     for rep in range(4):
         for name, fn in variants.items():
