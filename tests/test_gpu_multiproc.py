@@ -161,6 +161,18 @@ def test_pull_gate_stalled_peer_raises():
     assert 1.5 <= out["seconds"] < 30, out
 
 
+@pytest.mark.parametrize("nproc", [4, 8])
+def test_pull_rounds_with_drifting_ranks(nproc):
+    """The pull transport's device gate under drift: rounds enqueued back to back while every rank
+    sleeps a random 0-3 ms before some of them (ranks several rounds apart, gates really waiting),
+    whole rows (graph 2) and Choco messages (fetch and direct reads) -- every worker bit-exact vs the
+    oracle at the end."""
+    r = _torchrun(nproc, [os.path.join(HERE, "mp_pull_stress.py")], timeout=280)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert res["world"] == nproc and all(v for k, v in res.items() if k != "world"), res
+
+
 def test_bench_self_launch_gloo():
     """`python bench.py --gpus 2` WITHOUT torchrun: the parent starts the ranks
     as a child torch.distributed.run and relays rank 0's line -- n_gpus 2, the oracle self-check
