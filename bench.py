@@ -159,23 +159,33 @@ class Watchdog:
         self.rank, self.emit = rank, emit
         self.lock = threading.Lock()
         self.name = self.deadline = self.seconds = None
+        self.armed_at = time.monotonic()
         t = threading.Thread(target=self._run, daemon=True)
         t.start()
+
+    HEARTBEAT_S = 60.0          # rank 0: one stderr line per minute naming the running phase
 
     def arm(self, name, seconds):
         with self.lock:
             self.name, self.seconds, self.deadline = name, seconds, time.monotonic() + seconds
+            self.armed_at = time.monotonic()
 
     def disarm(self):
         with self.lock:
             self.deadline = None
 
     def _run(self):
+        beat = time.monotonic()
         while True:
             time.sleep(0.25)
             with self.lock:
                 fire = self.deadline is not None and time.monotonic() > self.deadline
                 name, secs = self.name, self.seconds
+                running = self.deadline is not None
+            if self.rank == 0 and running and time.monotonic() - beat > self.HEARTBEAT_S:
+                beat = time.monotonic()
+                sys.stderr.write(f"[bench] {name}: running for {beat - self.armed_at:.0f} s\n")
+                sys.stderr.flush()
             if fire:
                 msg = (f"{name}: no progress within {secs:.0f} s on rank {self.rank} (a peer rank did not take "
                        f"part or hung); the figures after it were not run")
