@@ -641,10 +641,11 @@ def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99
                  pull="auto"):
     """Secondary figure: ChocoSGD rounds (BASELINE config 4: VGG-16 size, top-1 %, graph 0, every
     matching active) on the same GPUs -- top-k compress + [N > 1] message exchange + fused apply.
-    N > 1: the messages travel over RCCL (mx_exchange_round) or, under the pull transport, are read
-    by the apply pass from the owners' IPC-mapped snapshot buffers (mx_choco_apply_slots behind the
-    device gate); both forms run R untimed rounds and the faster (max over ranks) is timed, unless
-    --pull on / off forces it.  Parity: one more round after the timed ones, x / x_hat / s of every
+    N > 1: the messages travel over RCCL (mx_exchange_round) or, under the pull transport, are taken
+    from the owners' IPC-mapped snapshot buffers behind the device gate -- fetched into the receive
+    slots (mx_pull_fetch, form "pull") or read in place by the apply (mx_choco_apply_slots, form
+    "pull_direct"); every form runs R untimed rounds and the fastest (max over ranks) is timed
+    (--pull on: the faster pull form; --pull off: RCCL only).  Parity: one more round after the timed ones, x / x_hat / s of every
     worker vs the oracle's round from the same state (choco_oracle_round)."""
     R = 4
     grp = pkg.ChocoWorkerGroup(GP, numel=P, ratio=ratio, consensus_lr=gamma, rank=rank, nranks=world,
