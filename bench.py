@@ -46,10 +46,11 @@ METRIC = "gossip rounds/sec (8 workers x 25.6M fp32 params, graph 0, full MATCHA
 # rccl_overhead.py, profiles/r05m_rccl_overhead.log: 7.3 us for 4 KB - 1.8 MB) -- a LOWER bound of a
 # cross-GPU group's cost, one per exchange (one per chunk for the pipelined form).
 PULL_FIXED_S = {2: 26e-6, 4: 31e-6, 8: 62e-6}
-# the same for a ChocoSGD round under the pull transport (message publish + gate + the apply's
-# remote reads, minus compress + apply with a transport that moves nothing; P = 100k, top-1 %:
-# profiles/r05p_overhead_n*.log)
-PULL_CHOCO_FIXED_S = {2: 10.6e-6, 4: 12.0e-6, 8: 41.8e-6}
+# the same for a ChocoSGD round under the pull transport, fetch form (message publish + gate + the
+# fetch of the partners' messages, minus compress + apply with a transport that moves nothing;
+# P = 100k, top-1 %: profiles/r05z_overhead_fetch_n*.log; the direct form measured 10.6 / 12.0 /
+# 41.8 us, profiles/r05p_overhead_n*.log)
+PULL_CHOCO_FIXED_S = {2: 11.9e-6, 4: 13.5e-6, 8: 47.5e-6}
 PULL_TIMEOUT_S = 20.0      # the pull gate's deadline in the bench (lockstep rounds of at most a few ms)
 RCCL_FIXED_S = 7.3e-6
 HEADLINE_HBM_FRAC = 0.75   # the mixing kernel's measured fraction of 8 TB/s (BENCH_r04, profiles/)

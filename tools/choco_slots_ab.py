@@ -86,6 +86,20 @@ for rows in (8, 4, 2, 1):
             res[name].append(float(np.median([a.elapsed_time(b) for a, b in ev])) * 1e3)
     out[f"rows{rows}"] = {"slots_total": int(eng.n_slots), "apply_us_median_per_rep": res,
                           **{k + "_us": float(np.median(v)) for k, v in res.items()}}
+    if eng.n_slots > g.n_local:
+        # mx_pull_fetch of the round's remote messages (here from this GPU's own slots: the
+        # kernel's launch + acquire + copy cost without xGMI), per-launch events
+        dst = torch.empty_like(g.msgs)
+        rec = eng.plan.data_ptr() + 4 * 0 * eng.plan_words
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(K)]
+        for a, b in ev:
+            a.record()
+            pkg._lib.check(L.mx_pull_fetch(table.data_ptr(), g.n_local, eng.n_slots - g.n_local, rec, dst.data_ptr(),
+                                           g.msg_ld, g.msg_bytes, None))
+            b.record()
+        torch.cuda.synchronize()
+        out[f"rows{rows}"]["fetch_us"] = float(np.median([a.elapsed_time(b) for a, b in ev])) * 1e3
+        out[f"rows{rows}"]["fetch_bytes"] = int((eng.n_slots - g.n_local) * g.msg_bytes)
     del g
     torch.cuda.empty_cache()
 print(json.dumps(out), flush=True)
