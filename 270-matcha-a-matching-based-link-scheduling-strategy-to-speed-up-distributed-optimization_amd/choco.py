@@ -18,8 +18,7 @@ import time
 import numpy as np
 import torch
 
-from ._lib import check, lib, require_device, stream_ptr
-from ._lib import MXError
+from ._lib import MXError, check, lib, require_device, stream_ptr
 from .engine import (PULL_HEADER, GossipEngine, PullTransport, ROW_ALIGN, default_comm, owner_table, partition,
                      wait_round)
 
@@ -174,7 +173,8 @@ class ChocoWorkerGroup:
                                  stream_ptr(stream)), "mx_choco_apply")
 
     def _average_pull(self, it, stream=None):
-        """PullTransport averaging, four launches and no host wait: the local messages into
+        """PullTransport averaging, four launches (three with pull_read="direct") and no host wait:
+        the local messages into
         snapshot `round % 2` (system-scope release per workgroup), the gate (this rank's epoch out,
         bounded waits for the partners', remote slot table -> their snapshots), the fetch of the
         round's partner messages from their owners' HBM into the receive slots, the apply.  A gate
