@@ -174,11 +174,10 @@ class ChocoWorkerGroup:
 
     def _average_pull(self, it, stream=None):
         """PullTransport averaging, four launches (three with pull_read="direct") and no host wait:
-        the local messages into
-        snapshot `round % 2` (system-scope release per workgroup), the gate (this rank's epoch out,
-        bounded waits for the partners', remote slot table -> their snapshots), the fetch of the
-        round's partner messages from their owners' HBM into the receive slots, the apply.  A gate
-        that expired earlier raises here."""
+        the local messages into snapshot `round % 2` (system-scope release per workgroup), the gate
+        (this rank's epoch out, bounded waits for the partners', remote slot table -> their
+        snapshots), the fetch of the round's partner messages from their owners' HBM into the
+        receive slots, the apply.  A gate that expired earlier raises here."""
         st = self._pull
         msg = st.error()
         if msg:
