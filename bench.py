@@ -109,6 +109,9 @@ def parse():
                     "the watchdog's")
     ap.add_argument("--debug-skip", default="", help="test hook FIGURE:RANK -- that rank skips that figure "
                     "(its peers then wait in the figure's collectives: exercises the watchdog)")
+    ap.add_argument("--debug-no-rccl", action="store_true", help="test hook: behave as if the library's RCCL "
+                    "communicator could not be created on any rank (the gossip then runs over the pull transport "
+                    "alone)")
     ap.add_argument("--debug-stall", default="", help="test hook FIGURE:RANK -- that rank stalls inside that "
                     "figure (a hung peer: exercises the watchdog)")
     return ap.parse_args()
@@ -654,11 +657,14 @@ def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99
     fill_synth(pkg, grp)
     for it in range(W):
         grp.step(it)
-    forms, calib, pull_err = {"rccl": grp}, None, None
+    pull_only = isinstance(comm, pkg.PullTransport)          # the RCCL communicator was unavailable
+    forms, calib, pull_err = {"pull" if pull_only else "rccl": grp}, None, None
     any_remote = world > 1 and max_over_ranks(float(grp.engine.max_remote), world, dev) > 0   # collective
     # the pull forms: "pull" fetches the partner messages into the receive slots, "pull_direct" lets
     # the apply read them in place (ChocoWorkerGroup pull_read); one alive at a time while warming up
     for name, mode in (("pull", "fetch"), ("pull_direct", "direct")):
+        if name in forms:
+            continue
         if not (any_remote and pull != "off") or pull_err is not None:
             break
         gp, err = None, None
@@ -691,7 +697,7 @@ def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99
         grp = forms[chosen]
         W += R
     else:
-        chosen = "rccl" if world > 1 else None
+        chosen = next(iter(forms)) if world > 1 else None
     el = timed_loop(grp.step, W, K, world, dev)
     st = np.zeros(5 * grp.n_local, np.int64)
     pkg._lib.check(pkg.lib.mx_topk_stats(grp.work.data_ptr(), grp.work_ld, grp.n_local, grp.numel, st.ctypes.data,
@@ -883,9 +889,10 @@ def er_figure(pkg, args, rank, world, comm, dev):
     # bytes per parameter column on this GPU for each exchange form
     forms = {"local": n_local} if world == 1 else {}
     if world > 1:
-        forms["rccl"] = n_local + max_remote
-        forms["rccl_chunked"] = n_local + 2 * max_remote / 4.0 if max_remote else n_local
-        if args.pull != "off":
+        if not isinstance(comm, pkg.PullTransport):          # else: the RCCL communicator was unavailable
+            forms["rccl"] = n_local + max_remote
+            forms["rccl_chunked"] = n_local + 2 * max_remote / 4.0 if max_remote else n_local
+        if args.pull != "off" or not forms:
             forms["pull"] = 3 * n_local
     torch.cuda.empty_cache()
     free, total = torch.cuda.mem_get_info()
@@ -1164,13 +1171,28 @@ def run(args, world, rank, line, wd):
     import importlib
     pkg = importlib.import_module(PKG_NAME)
     comm = None
+    rccl_err = None
     if world > 1:
-        if gloo:
-            sys.path.insert(0, os.path.join(ROOT, "tests"))
-            from gloo_transport import GlooTransport
-            comm = GlooTransport(pkg)
-        else:
-            comm = pkg.engine.RcclComm(timeout_s=min(args.figure_timeout, args.headline_timeout) * 0.8)
+        try:
+            if args.debug_no_rccl:
+                raise pkg.MXError("--debug-no-rccl")
+            if gloo:
+                sys.path.insert(0, os.path.join(ROOT, "tests"))
+                from gloo_transport import GlooTransport
+                comm = GlooTransport(pkg)
+            else:
+                comm = pkg.engine.RcclComm(timeout_s=min(args.figure_timeout, args.headline_timeout) * 0.8)
+        except pkg.MXError as e:
+            rccl_err = str(e)
+        if max_over_ranks(float(rccl_err is not None), world, dev) > 0:
+            # the library's RCCL communicator is unusable on some rank: every rank drops it and the
+            # gossip runs over the pull transport alone (the line says why; the RCCL-only figures
+            # -- exchange alone, the centralized all-gather -- then report errors)
+            if isinstance(comm, pkg.engine.RcclComm):
+                comm.abort()
+            comm = pkg.PullTransport(timeout_s=PULL_TIMEOUT_S)
+            rccl_err = rccl_err or "a peer rank's RCCL communicator failed"
+    pull_only = isinstance(comm, pkg.PullTransport)
     # the ranks RCCL itself holds (ncclCommCount on the library's communicator): proof that the
     # exchange really spans N processes / GPUs
     rccl_ranks = comm.count() if isinstance(comm, pkg.engine.RcclComm) else None
@@ -1200,9 +1222,9 @@ def run(args, world, rank, line, wd):
     timed, overlap = group, None
     any_remote = world > 1 and max_over_ranks(float(group.engine.max_remote), world, dev) > 0   # collective
     base_it = W + DMAX + 2 * K
-    forms = {"rccl": group}
+    forms = {"pull" if pull_only else "rccl": group}
     C = None
-    if any_remote and args.overlap != "off":
+    if any_remote and args.overlap != "off" and not pull_only:
         # column pipelining: chunk c+1 of every exchanged row travels on a side stream while chunk c
         # is mixed (bit-identical results)
         C = args.chunk_cols or ((P + 3) // 4 + 63) // 64 * 64
@@ -1214,7 +1236,7 @@ def run(args, world, rank, line, wd):
         run(gchunk, base_it)                     # first chunked round (side stream, events) untimed
         forms["rccl_chunked"] = gchunk
     pull_err = None
-    if any_remote and args.pull != "off":
+    if any_remote and args.pull != "off" and not pull_only:
         # the pull transport: partner rows read straight from the peers' HBM (IPC-mapped
         # snapshots) by the mixing kernel -- no RCCL copies; collective setup, all ranks agree
         # (bench rounds run in lockstep: a device gate that waits PULL_TIMEOUT_S has met a fault,
@@ -1260,6 +1282,9 @@ def run(args, world, rank, line, wd):
                 del forms[name]
     elif pull_err is not None:
         overlap = {"pull_unavailable": pull_err}
+    if pull_only:
+        overlap = {"mode": args.overlap, "pull": args.pull, "chosen_form": "pull", "calib_ms": None,
+                   "note": "the library's RCCL communicator was unavailable (rccl_unavailable): pull transport only"}
     # per-round HIP events of the whole round (diagnostic): real rounds run BEFORE the timed region,
     # in blocks of K, for at least --settle-ms (an idle MI355X takes ~10 ms of streaming to reach
     # its steady clocks: profiles/r02_clock_ramp.log), so the timed rounds measure the steady state of the loop
@@ -1363,6 +1388,7 @@ def run(args, world, rank, line, wd):
                    "placement": group.placement if world > 1 else None,
                    "transport": args.transport if world > 1 else None},
         "rccl_ranks": rccl_ranks,
+        "rccl_unavailable": rccl_err,
         "parity_ok": None,
         "round_us": {"events_min": 1e3 * float(step_ms.min()), "events_median": 1e3 * float(np.median(step_ms)),
                      "events_mean": 1e3 * avg_ms, "events_last_block_mean": 1e3 * float(step_ms[-K:].mean()),
@@ -1456,7 +1482,7 @@ def run(args, world, rank, line, wd):
         wd.disarm()
         return res
 
-    if world > 1:
+    if world > 1 and not pull_only:
         def _xo():
             s, per = exchange_only(group, timed_first, K, world, dev)
             out["xgmi"].update({"exchange_only_ms": 1e3 * s, "exchange_only_ms_per_rank": [1e3 * x for x in per],
@@ -1484,7 +1510,9 @@ def run(args, world, rank, line, wd):
                                     args.budget >= 1.0)
     out["allreduce_baseline"] = figure("allreduce", lambda: allreduce_figure(
         pkg, args, rank, world, n, P, max(5, K), 2, comm, dev,
-        arena=group.arena if world == 1 else None), bool(args.allreduce))
+        arena=group.arena if world == 1 else None), bool(args.allreduce) and not pull_only)
+    if pull_only and args.allreduce:
+        out["allreduce_baseline"] = {"skipped": "the all-gather needs the RCCL communicator (rccl_unavailable)"}
     # the headline groups are done: release them before the large figures
     for g in {id(g): g for g in (timed, group)}.values():
         g.close()
@@ -1505,7 +1533,7 @@ def run(args, world, rank, line, wd):
     if world > 1:
         wd.arm("teardown", args.figure_timeout)
         dist.barrier()
-        if not gloo:
+        if isinstance(comm, pkg.engine.RcclComm):
             comm.close()
         dist.destroy_process_group()
         wd.disarm()

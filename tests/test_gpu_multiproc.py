@@ -148,6 +148,27 @@ def test_bench_multiprocess_overlap_forms(nproc, overlap, pull):
         assert set(out["overlap"]["calib_ms"]) == {"rccl", "rccl_chunked", "pull"}
 
 
+def test_bench_falls_back_to_pull_without_rccl():
+    """N > 1 when the library's RCCL communicator cannot be created (--debug-no-rccl: as if it
+    failed on every rank): the gossip runs over the pull transport alone -- headline, MATCHA,
+    Choco (both pull reads calibrated) and the configs each pass the oracle self-check, the line
+    says why (rccl_unavailable) and the RCCL-only figures are skipped, not failed."""
+    r = _torchrun(2, ["bench.py", "--gpus", "2", "--transport", "gloo", "--debug-no-rccl", "--steps", "3",
+                      "--warmup", "1", "--params", "100000", "--choco-params", "100000", "--cpu-seconds", "0",
+                      "--wrn-params", "50000", "--resnet-params", "20000", "--er-params", "20000",
+                      "--er-rounds", "1", "--er-budgets", "1.0"], timeout=280)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert "error" not in out, out["error"]
+    assert out["rccl_unavailable"] and out["overlap"]["chosen_form"] == "pull" and out["parity_ok"] is True
+    assert out["overlap"]["pull_rounds"] >= 6 and out["overlap"]["pull_gate_error"] is None
+    assert out["matcha_schedule"]["parity_ok"] is True
+    assert set(out["choco"]["calib_ms"]) == {"pull", "pull_direct"} and out["choco"]["parity_ok"] is True
+    assert all(v["parity_ok"] is True for k, v in out["configs"].items() if k != "parity"), out["configs"]
+    assert out["er64_sweep"]["form"] == "pull" and out["er64_sweep"]["parity_ok"] is True
+    assert "skipped" in out["allreduce_baseline"] and out["xgmi"]["exchange_only_ms"] is None
+
+
 def test_pull_gate_stalled_peer_raises():
     """PullTransport without a host barrier: a rank whose peer stops publishing is held by the
     device gate's BOUNDED wait (mx_pull_gate, 2 s deadline here) and communicate() raises MXError
