@@ -53,6 +53,7 @@ PULL_FIXED_S = {2: 26e-6, 4: 31e-6, 8: 62e-6}
 PULL_CHOCO_FIXED_S = {2: 11.9e-6, 4: 13.5e-6, 8: 47.5e-6}
 PULL_TIMEOUT_S = 20.0      # the pull gate's deadline in the bench (lockstep rounds of at most a few ms)
 RCCL_FIXED_S = 7.3e-6
+RCCL_WARMUP_WAIT_S = 60.0  # N > 1: deadline of the headline's first RCCL exchanges (then: pull transport)
 HEADLINE_HBM_FRAC = 0.75   # the mixing kernel's measured fraction of 8 TB/s (BENCH_r04, profiles/)
 
 
@@ -1218,6 +1219,22 @@ def run(args, world, rank, line, wd):
 
     for it in range(W):
         run(group, it)
+    if isinstance(comm, pkg.engine.RcclComm):
+        # the first cross-GPU exchanges, waited for with a deadline (an exchange that never completes
+        # aborts the communicator instead of hanging the stream), before any torch collective queues
+        # behind them; on expiry on any rank every rank continues over the pull transport
+        try:
+            comm.wait(timeout_s=RCCL_WARMUP_WAIT_S)
+        except pkg.MXError as e:
+            rccl_err = f"warmup exchange: {e}"
+        if max_over_ranks(float(rccl_err is not None), world, dev) > 0:
+            rccl_err = rccl_err or "a peer rank's warmup exchange did not complete"
+            comm.abort()
+            comm, pull_only = pkg.PullTransport(timeout_s=PULL_TIMEOUT_S), True
+            group = pkg.VirtualWorkerGroup(GP, numel=P, rank=rank, nranks=world, comm=comm, placement=args.placement)
+            fill_synth(pkg, group)
+            for it in range(W):
+                run(group, it)
     torch.cuda.synchronize()
     timed, overlap = group, None
     any_remote = world > 1 and max_over_ranks(float(group.engine.max_remote), world, dev) > 0   # collective
