@@ -652,28 +652,48 @@ static_assert(sizeof(hipIpcMemHandle_t) == 64, "hipIpcMemHandle_t is expected to
 
 extern "C" int mx_ipc_handle_bytes(void) { return (int)sizeof(hipIpcMemHandle_t); }
 
+// Sizes are rounded up to whole 2 MiB and an allocation whose export is refused is retried
+// (the refused one held until the retry is done, so it cannot come back): late in a long test
+// session a small exportable hipMalloc was observed to be refused by hipIpcGetMemHandle with
+// "invalid argument" (profiles/r05zz2_suite_ipc_failure.log) while the same request succeeds in a
+// fresh process -- consistent with a small allocation carved from a shared block, which cannot be
+// exported on its own.
 extern "C" int mx_ipc_alloc(int64_t bytes, void** ptr_out, void* handle_out) {
     MX_CHECK(bytes > 0 && ptr_out && handle_out, "mx_ipc_alloc: bad arguments");
-    void* p = nullptr;
-    MX_HIP(hipMalloc(&p, (size_t)bytes));
-    // zero-filled (the pull header's epoch starts at 0) and complete before the handle is shared
-    hipError_t e = hipMemset(p, 0, (size_t)bytes);
-    if (e == hipSuccess) e = hipDeviceSynchronize();
-    if (e != hipSuccess) {
-        (void)hipFree(p);
-        mx::set_error("mx_ipc_alloc: hipMemset -> %s", hipGetErrorString(e));
-        return MX_ERR_HIP;
+    constexpr size_t kGran = (size_t)2 << 20;
+    constexpr int kTries = 4;
+    void* refused[kTries] = {nullptr};
+    int nref = 0;
+    hipError_t e = hipSuccess;
+    for (int t = 0; t < kTries; ++t) {
+        const size_t n = ((size_t)bytes + kGran - 1) / kGran * kGran + (size_t)t * kGran;
+        void* p = nullptr;
+        e = hipMalloc(&p, n);
+        if (e != hipSuccess) break;
+        // zero-filled (the pull header's epoch starts at 0) and complete before the handle is shared
+        e = hipMemset(p, 0, n);
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        if (e != hipSuccess) {
+            (void)hipFree(p);
+            for (int i = 0; i < nref; ++i) (void)hipFree(refused[i]);
+            mx::set_error("mx_ipc_alloc: hipMemset -> %s", hipGetErrorString(e));
+            return MX_ERR_HIP;
+        }
+        hipIpcMemHandle_t h;
+        e = hipIpcGetMemHandle(&h, p);
+        if (e == hipSuccess) {
+            for (int i = 0; i < nref; ++i) (void)hipFree(refused[i]);
+            memcpy(handle_out, &h, sizeof(h));
+            *ptr_out = p;
+            return MX_OK;
+        }
+        (void)hipGetLastError();
+        refused[nref++] = p;
     }
-    hipIpcMemHandle_t h;
-    e = hipIpcGetMemHandle(&h, p);
-    if (e != hipSuccess) {
-        (void)hipFree(p);
-        mx::set_error("mx_ipc_alloc: hipIpcGetMemHandle -> %s", hipGetErrorString(e));
-        return MX_ERR_HIP;
-    }
-    memcpy(handle_out, &h, sizeof(h));
-    *ptr_out = p;
-    return MX_OK;
+    for (int i = 0; i < nref; ++i) (void)hipFree(refused[i]);
+    mx::set_error("mx_ipc_alloc: %s -> %s (%d tries)", nref ? "hipIpcGetMemHandle" : "hipMalloc", hipGetErrorString(e),
+                  nref);
+    return MX_ERR_HIP;
 }
 
 extern "C" int mx_ipc_open(const void* handle, void** ptr_out) {

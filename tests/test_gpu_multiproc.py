@@ -27,6 +27,13 @@ def _port():
     return p
 
 
+def _why(r):
+    """the failing ranks' own error lines first (the launcher's summary hides them), then the tails"""
+    err = [l for l in r.stderr.splitlines() if ("Error" in l or "error" in l or "Traceback" in l)
+           and "Gloo" not in l and "error_file" not in l]
+    return "\n".join(err[:40]) + "\n--- stdout ---\n" + r.stdout[-2000:] + "\n--- stderr ---\n" + r.stderr[-2000:]
+
+
 def _torchrun(nproc, args, timeout=200):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", "--master-port", str(_port())] + args
@@ -39,7 +46,7 @@ def test_multiprocess_rounds_match_oracle(nproc):
     """nproc 3: uneven worker blocks (8 -> 3, 3, 2; 16 -> 6, 5, 5), so the pull transport's peers'
     snapshot buffers differ in size (per-rank n_local in the device rank table)."""
     r = _torchrun(nproc, [os.path.join(HERE, "mp_worker.py")])
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, _why(r)
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     res = json.loads(line)
     assert res["world"] == nproc and all(v for k, v in res.items() if k != "world"), res
@@ -56,7 +63,7 @@ def test_bench_multiprocess_path(nproc):
                           "--params", "200000", "--choco-params", "300000", "--cpu-seconds", "0",
                           "--wrn-params", "70000", "--resnet-params", "30000", "--er-params", "20000",
                           "--er-rounds", "2", "--er-budgets", "0.3,1.0"], timeout=280)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, _why(r)
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     out = json.loads(line)
     assert "error" not in out, out["error"]
@@ -111,7 +118,7 @@ def test_bench_watchdog_line_on_hang():
                       "--params", "100000", "--cpu-seconds", "0", "--configs", "0", "--er", "0",
                       "--figure-timeout", "15", "--debug-skip", "allreduce:1"], timeout=240)
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, r.stdout[-3000:] + r.stderr[-3000:]
+    assert len(lines) == 1, _why(r)
     out = json.loads(lines[0])
     assert out["value"] > 0 and out["parity_ok"] is True
     errs = [out.get("error")] + [v.get("error") for v in out.values() if isinstance(v, dict)]
@@ -128,7 +135,7 @@ def test_bench_multiprocess_overlap_forms(nproc, overlap, pull):
     r = _torchrun(nproc, ["bench.py", "--gpus", str(nproc), "--transport", "gloo", "--steps", "3", "--warmup", "1",
                           "--params", "100000", "--cpu-seconds", "0", "--overlap", overlap,
                           "--pull", pull, "--configs", "0", "--er", "0", "--allreduce", "0"] + choco)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, _why(r)
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["value"] > 0 and out["parity_ok"] is True
     if overlap == "on":
@@ -157,14 +164,16 @@ def test_bench_falls_back_to_pull_without_rccl():
                       "--warmup", "1", "--params", "100000", "--choco-params", "100000", "--cpu-seconds", "0",
                       "--wrn-params", "50000", "--resnet-params", "20000", "--er-params", "20000",
                       "--er-rounds", "1", "--er-budgets", "1.0"], timeout=280)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, _why(r)
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert "error" not in out, out["error"]
     assert out["rccl_unavailable"] and out["overlap"]["chosen_form"] == "pull" and out["parity_ok"] is True
     assert out["overlap"]["pull_rounds"] >= 6 and out["overlap"]["pull_gate_error"] is None
     assert out["matcha_schedule"]["parity_ok"] is True
     assert set(out["choco"]["calib_ms"]) == {"pull", "pull_direct"} and out["choco"]["parity_ok"] is True
-    assert all(v["parity_ok"] is True for k, v in out["configs"].items() if k != "parity"), out["configs"]
+    cf = out["configs"]
+    assert "error" not in cf and "skipped" not in cf, cf
+    assert all(v["parity_ok"] is True for k, v in cf.items() if k != "parity"), cf
     assert out["er64_sweep"]["form"] == "pull" and out["er64_sweep"]["parity_ok"] is True
     assert "skipped" in out["allreduce_baseline"] and out["xgmi"]["exchange_only_ms"] is None
 
@@ -175,7 +184,7 @@ def test_pull_gate_stalled_peer_raises():
     naming the peer -- no hang; the error is sticky (the next step raises at once); the stalled
     peer's own round completes once it resumes."""
     r = _torchrun(2, [os.path.join(HERE, "mp_pull_stall.py")], timeout=150)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, _why(r)
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["first_rounds_ok"] and out["raised"] and out["sticky"] and out["peer_round_ok"], out
     assert "rank 1 did not publish" in out["message"], out
@@ -189,7 +198,7 @@ def test_pull_rounds_with_drifting_ranks(nproc):
     whole rows (graph 2) and Choco messages (fetch and direct reads) -- every worker bit-exact vs the
     oracle at the end."""
     r = _torchrun(nproc, [os.path.join(HERE, "mp_pull_stress.py")], timeout=280)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, _why(r)
     res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert res["world"] == nproc and all(v for k, v in res.items() if k != "world"), res
 
@@ -202,7 +211,7 @@ def test_bench_self_launch_gloo():
                         "--warmup", "1", "--params", "100000", "--choco", "0", "--cpu-seconds", "0", "--configs",
                         "0", "--er", "0", "--allreduce", "1"], cwd=ROOT, capture_output=True, text=True,
                        timeout=240, env=dict(os.environ, OMP_NUM_THREADS="2"))
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, _why(r)
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout[-3000:]
     out = json.loads(lines[0])
@@ -216,7 +225,7 @@ def test_dropin_communicators_one_process_per_worker():
     ChocoCommunicator(rank, 8, GP, ...).communicate(model) with GPU- and CPU-resident models,
     bit-exact vs the oracle every round (8 ranks share GPU 0; gloo transport)."""
     r = _torchrun(8, [os.path.join(HERE, "mp_dropin.py")], timeout=280)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, _why(r)
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     res = json.loads(line)
     assert res["world"] == 8 and all(v for k, v in res.items() if k != "world"), res
@@ -228,7 +237,7 @@ def test_rank_trainer_matches_virtual_trainer():
     pull transport (decen and Choco) -- ends with every worker's parameters bit-identical to the
     single-process VirtualTrainer's (2 epochs, MATCHA 0.5, momentum 0.9)."""
     r = _torchrun(8, [os.path.join(HERE, "mp_trainer.py")], timeout=280)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, _why(r)
     res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert res["world"] == 8 and all(v for k, v in res.items() if k != "world"), res
 
@@ -238,7 +247,7 @@ def test_rccl_single_rank_linkage():
     all-reduce mean, an exchange round with nothing to move, destroy) under torchrun with the nccl
     backend -- the N > 1 transport's linkage against the RCCL torch loaded."""
     r = _torchrun(1, [os.path.join(HERE, "rccl_single.py")], timeout=150)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, _why(r)
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out == {"rank": 0, "nranks": 1, "nonblocking": True, "allreduce_identity": True, "decen_bit_exact": True,
                    "post_self_exchange": True, "post_validates": True, "post_validates_peer": True,
@@ -253,9 +262,9 @@ def test_bench_watchdog_line_on_stall():
     r = _torchrun(2, ["bench.py", "--gpus", "2", "--transport", "gloo", "--steps", "3", "--warmup", "1",
                       "--params", "100000", "--choco-params", "100000", "--cpu-seconds", "0", "--configs", "0",
                       "--er", "0", "--figure-timeout", "15", "--debug-stall", "choco:1"], timeout=240)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, _why(r)
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, r.stdout[-3000:] + r.stderr[-3000:]
+    assert len(lines) == 1, _why(r)
     out = json.loads(lines[0])
     assert out["value"] > 0 and out["parity_ok"] is True
     assert "choco" in out["error"] and "no progress" in out["error"], out["error"]
@@ -267,7 +276,7 @@ def test_rccl_init_deadline():
     MX_ERR_RCCL ("timed out") after its 4 s deadline instead of hanging, and the process exits."""
     r = subprocess.run([sys.executable, os.path.join(HERE, "rccl_deadline.py")], cwd=ROOT, capture_output=True,
                        text=True, timeout=120)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, _why(r)
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["rc"] == -3 and out["handle_null"] and "never joined" in out["message"], out
     assert 3.5 <= out["seconds"] < 60, out
@@ -294,7 +303,7 @@ def test_cross_gpu_transports_match_oracle():
     coherence protocol), every worker's row bit-exact vs the oracle.  Skipped on a one-GPU box."""
     n = min(4, torch.cuda.device_count())
     r = _torchrun(n, [os.path.join(HERE, "mp_gpus.py")], timeout=280)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, _why(r)
     res = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert res["world"] == n and all(v for k, v in res.items() if k != "world"), res
 
@@ -306,7 +315,7 @@ def test_bench_single_gpu_line():
                         "--choco-params", "200000", "--cpu-seconds", "1", "--er-params", "3e6",
                         "--er-budgets", "0.2,1.0"], cwd=ROOT, capture_output=True,
                        text=True, timeout=280, env=dict(os.environ, OMP_NUM_THREADS="2"))
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert r.returncode == 0, _why(r)
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["n_gpus"] == 1 and out["steps"] == 4 and out["warmup"] == 2 and out["value"] > 0
     assert "error" not in out and out["parity_ok"] is True and "oracle" in out["parity"]
