@@ -202,48 +202,53 @@ class PullTransport:
     def bind(self, vwg, row_bytes=None):
         """Collective: allocate vwg's snapshot buffer, exchange handles, map the peers'.  Every
         rank takes part in every exchange even when its own step failed, and all ranks raise
-        together (MXError) if any failed, so a refusal on one GPU cannot leave the others waiting.
+        together (MXError) if any failed, so a refusal on one GPU cannot leave the others waiting --
+        after one collective retry with fresh buffers (an export or import refused once, as seen
+        late in long test sessions, does not cost the transport).
         row_bytes: the stride of one worker's snapshot (default: a whole row, vwg.ld floats; a
         ChocoWorkerGroup passes its message stride)."""
         import torch.distributed as dist
         hb = int(lib.mx_ipc_handle_bytes())
         half = vwg.n_local * (int(row_bytes) if row_bytes is not None else vwg.ld * 4)
-        own = ctypes.c_void_p()
-        handle = (ctypes.c_char * hb)()
-        err = None
-        try:
-            check(lib.mx_ipc_alloc(PULL_HEADER + 2 * half, ctypes.byref(own), ctypes.cast(handle, ctypes.c_void_p)),
-                  "mx_ipc_alloc")
-        except MXError as e:
-            err = str(e)
-        objs = [None] * self.nranks
-        dist.all_gather_object(objs, (self.rank, None if err else bytes(handle)), group=self.group)
-        peers = [0] * self.nranks
-        opened = []
-        if err is None and all(h is not None for _, h in objs):
+        for attempt in range(2):     # one collective retry with fresh buffers (a refused export / import)
+            own = ctypes.c_void_p()
+            handle = (ctypes.c_char * hb)()
+            err = None
             try:
-                for r, h in objs:
-                    if r == self.rank:
-                        peers[r] = own.value
-                        continue
-                    buf = (ctypes.c_char * hb).from_buffer_copy(h)
-                    p = ctypes.c_void_p()
-                    check(lib.mx_ipc_open(ctypes.cast(buf, ctypes.c_void_p), ctypes.byref(p)), "mx_ipc_open")
-                    peers[r] = p.value
-                    opened.append(p.value)
+                check(lib.mx_ipc_alloc(PULL_HEADER + 2 * half, ctypes.byref(own), ctypes.cast(handle, ctypes.c_void_p)),
+                      "mx_ipc_alloc")
             except MXError as e:
                 err = str(e)
-        elif err is None:
-            err = "a peer could not allocate its snapshot buffer"
-        oks = [None] * self.nranks
-        dist.all_gather_object(oks, err, group=self.group)
-        bad = [(r, e) for r, e in enumerate(oks) if e is not None]
-        if bad:
+            objs = [None] * self.nranks
+            dist.all_gather_object(objs, (self.rank, None if err else bytes(handle)), group=self.group)
+            peers = [0] * self.nranks
+            opened = []
+            if err is None and all(h is not None for _, h in objs):
+                try:
+                    for r, h in objs:
+                        if r == self.rank:
+                            peers[r] = own.value
+                            continue
+                        buf = (ctypes.c_char * hb).from_buffer_copy(h)
+                        p = ctypes.c_void_p()
+                        check(lib.mx_ipc_open(ctypes.cast(buf, ctypes.c_void_p), ctypes.byref(p)), "mx_ipc_open")
+                        peers[r] = p.value
+                        opened.append(p.value)
+                except MXError as e:
+                    err = str(e)
+            elif err is None:
+                err = "a peer could not allocate its snapshot buffer"
+            oks = [None] * self.nranks
+            dist.all_gather_object(oks, err, group=self.group)
+            bad = [(r, e) for r, e in enumerate(oks) if e is not None]
+            if not bad:
+                break
             for p in opened:
                 lib.mx_ipc_close(p)
             if own.value:
                 lib.mx_ipc_free(own.value)
-            raise MXError(f"pull transport unavailable: rank {bad[0][0]}: {bad[0][1]}")
+            if attempt:
+                raise MXError(f"pull transport unavailable: rank {bad[0][0]}: {bad[0][1]}")
         return _PullState(self, vwg, own.value, peers, opened, half)
 
 

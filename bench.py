@@ -53,6 +53,7 @@ PULL_FIXED_S = {2: 26e-6, 4: 31e-6, 8: 62e-6}
 PULL_CHOCO_FIXED_S = {2: 11.9e-6, 4: 13.5e-6, 8: 47.5e-6}
 PULL_TIMEOUT_S = 20.0      # the pull gate's deadline in the bench (lockstep rounds of at most a few ms)
 RCCL_FIXED_S = 7.3e-6
+PEER_GONE = ("Connection closed by peer", "Connection reset by peer", "Broken pipe")   # gloo / c10d errors
 RCCL_WARMUP_WAIT_S = 60.0  # N > 1: deadline of the headline's first RCCL exchanges (then: pull transport)
 HEADLINE_HBM_FRAC = 0.75   # the mixing kernel's measured fraction of 8 TB/s (BENCH_r04, profiles/)
 
@@ -1497,6 +1498,12 @@ def run(args, world, rank, line, wd):
             time.sleep(10 * args.figure_timeout)
         res = guarded(name, fn)
         wd.disarm()
+        if world > 1 and isinstance(res, dict) and any(m in str(res.get("error", "")) for m in PEER_GONE):
+            # a peer rank left the job (its watchdog fired first, or it died): no later collective
+            # can complete -- as the watchdog does, rank 0 prints the line so far and every rank leaves
+            line.emit(f"{name}: no progress -- a peer rank left the job ({res['error']}); the figures after it "
+                      f"were not run")
+            os._exit(0)
         return res
 
     if world > 1 and not pull_only:
