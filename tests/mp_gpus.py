@@ -21,6 +21,7 @@ for p in (ROOT, HERE, os.path.join(ROOT, "oracle")):
         sys.path.insert(0, p)
 from conftest import PKG_NAME  # noqa: E402
 import mp_worker as W  # noqa: E402
+import mp_pull_stress as ST  # noqa: E402
 
 
 def main():
@@ -42,6 +43,10 @@ def main():
                                                   placement="auto", back_to_back=True),
         "pull_choco_direct_g0": W.choco_case(pkg, pkg.PullTransport(timeout_s=60), 20_011, 0.9, 8, seed=19,
                                              back_to_back=True, pull_read="direct"),
+        # the drift stress across GPUs: ranks several rounds apart, gates waiting over xGMI
+        "pull_stress_decen": ST.decen(pkg, dist.get_rank(), dist.get_world_size()),
+        "pull_stress_choco_fetch": ST.choco(pkg, dist.get_rank(), dist.get_world_size(), "fetch"),
+        "pull_stress_choco_direct": ST.choco(pkg, dist.get_rank(), dist.get_world_size(), "direct"),
     }
     torch.cuda.synchronize()
     flags = [None] * dist.get_world_size()
