@@ -7,7 +7,7 @@ package without it fails.
 """
 from ._lib import MXError, lib
 from .graph_manager import GraphProcessor, FixedProcessor, MatchaProcessor
-from .engine import GossipEngine, VirtualWorkerGroup, RcclComm, PullTransport, Layout, partition
+from .engine import GossipEngine, VirtualWorkerGroup, RcclComm, PullTransport, Layout, partition, pull_stats
 from .choco import ChocoWorkerGroup, topk_count
 from .communicator import Communicator, decenCommunicator, ChocoCommunicator, centralizedCommunicator
 from .comm_helpers import flatten_tensors, unflatten_tensors, scatter_tensors
@@ -20,7 +20,7 @@ from .placement import best_placement, placement_cost
 
 __all__ = [
     "MXError", "lib", "GraphProcessor", "FixedProcessor", "MatchaProcessor", "GossipEngine",
-    "VirtualWorkerGroup", "RcclComm", "PullTransport", "Layout", "partition", "ChocoWorkerGroup", "topk_count",
+    "VirtualWorkerGroup", "RcclComm", "PullTransport", "Layout", "partition", "pull_stats", "ChocoWorkerGroup", "topk_count",
     "Communicator", "decenCommunicator", "ChocoCommunicator", "centralizedCommunicator",
     "flatten_tensors", "unflatten_tensors", "scatter_tensors", "get_top_k", "check_top_k", "select_graph",
     "erdos_renyi", "GRAPH_SIZES", "solver", "harness", "placement", "best_placement", "placement_cost",

@@ -68,7 +68,7 @@ SIGNATURES = {
     "mx_allgather": (c_int, [c_p, c_p, c_i64, c_p, c_p]),
     "mx_mean_rows": (c_int, [c_p, c_int, c_i64, c_i64, c_int, c_p, c_p]),
     "mx_mean_rows_to": (c_int, [c_p, c_int, c_i64, c_i64, c_int, c_p, c_int, c_i64, c_p]),
-    "mx_mean_kernel_name": (ctypes.c_char_p, [c_int, c_i64, c_int]),
+    "mx_mean_kernel_name": (ctypes.c_char_p, [c_p, c_int, c_i64, c_i64, c_int, c_p, c_int, c_i64]),
     "mx_pull_gate": (c_int, [c_p, c_p, c_int, c_p, c_int, c_p, c_p, c_int, c_int, c_int, c_int, c_i64, c_int, c_u64,
                              c_p, c_int, c_f64, c_p, c_p]),
     "mx_host_words": (c_int, [c_int, c_p, c_p]),
@@ -76,9 +76,13 @@ SIGNATURES = {
     "mx_synth_fill": (c_int, [c_p, c_i64, c_u64, c_p]),
     "mx_max_weight_matching": (c_int, [c_int, c_p, c_p, c_p, c_int, c_p, c_p, c_p]),
     "mx_snapshot_publish": (c_int, [c_p, c_p, c_i64, c_p]),
+    "mx_snapshot_publish_rows": (c_int, [c_p, c_i64, c_p, c_i64, c_i64, c_int, c_p, c_int, c_p, c_int, c_int, c_p]),
     "mx_plan_set_peer_reads": (c_int, [c_p, c_i64, c_int, c_int, c_int, c_p]),
     "mx_ipc_handle_bytes": (c_int, []),
     "mx_ipc_alloc": (c_int, [c_i64, c_p, c_p]),
+    "mx_ipc_stats": (c_int, [c_p, c_p]),
+    "mx_ipc_set": (c_int, [ctypes.c_char_p, c_i64]),
+    "mx_ipc_get": (c_i64, [ctypes.c_char_p]),
     "mx_ipc_open": (c_int, [c_p, c_p]),
     "mx_ipc_close": (c_int, [c_p]),
     "mx_ipc_free": (c_int, [c_p]),

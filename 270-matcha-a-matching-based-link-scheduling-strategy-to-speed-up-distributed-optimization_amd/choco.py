@@ -6,7 +6,8 @@ persistent Choco state x_hat and s (all [n_local, P] in HBM).  Per round:
     [N > 1] RCCL exchange of the messages   mx_exchange_round  (12 k bytes per edge direction)
     s / x_hat updates + dense x update      mx_choco_apply     (averaging, 200-230; one fused pass)
 Under PullTransport (N > 1, one process per GPU of a node) the messages are not sent: every rank
-publishes its rows' messages into its IPC-shared snapshot buffer (mx_snapshot_publish), the device
+publishes the messages its peers read this round into its IPC-shared snapshot buffer
+(mx_snapshot_publish_rows), the device
 gate (mx_pull_gate) waits for the partners' epochs and points a device slot table at their
 snapshots, mx_pull_fetch copies the round's partner messages from the owners' HBM into the receive
 slots, and the apply pass runs as under RCCL (pull_read="fetch"; "direct": the apply reads them in
@@ -110,6 +111,12 @@ class ChocoWorkerGroup:
     def rows(self):
         return self.x[:, :self.numel]
 
+    @property
+    def publish_cols(self):
+        """Floats of a message slot the pull round publishes (msg_bytes rounded up to 16 bytes: what
+        mx_pull_fetch and mx_choco_apply_slots read)."""
+        return (self.msg_bytes + 15) // 16 * 4
+
     def message(self, slot):
         """(values float32[k], indices int64[k]) views of message `slot` (index-sorted)."""
         base = slot * self.msg_ld
@@ -174,7 +181,8 @@ class ChocoWorkerGroup:
 
     def _average_pull(self, it, stream=None):
         """PullTransport averaging, four launches (three with pull_read="direct") and no host wait:
-        the local messages into snapshot `round % 2` (system-scope release per workgroup), the gate
+        the local messages a peer reads this round into snapshot `round % 2` (system-scope release
+        per workgroup), the gate
         (this rank's epoch out, bounded waits for the partners', remote slot table -> their
         snapshots), the fetch of the round's partner messages from their owners' HBM into the
         receive slots, the apply.  A gate that expired earlier raises here."""
@@ -186,9 +194,12 @@ class ChocoWorkerGroup:
         par = st.round & 1
         st.round += 1
         s = stream_ptr(stream)
-        check(lib.mx_snapshot_publish(self.msgs.data_ptr(), st.own + PULL_HEADER + par * st.half,
-                                      self.n_local * self.msg_ld // 4, s), "mx_snapshot_publish")
         frow = (eng._adhoc_flags.data_ptr() if it == eng.T else eng.flags_dev.data_ptr() + it * eng.M)
+        # the messages of the rows a peer reads this round (an active partner in another block)
+        check(lib.mx_snapshot_publish_rows(self.msgs.data_ptr(), self.msg_ld // 4, st.own + PULL_HEADER + par * st.half,
+                                           self.msg_ld // 4, self.publish_cols, self.n_local, frow, eng.M,
+                                           eng.partner_dev.data_ptr(), eng.n, self.row_base, s),
+              "mx_snapshot_publish_rows")
         tr = st.transport
         check(lib.mx_pull_gate(frow, st.prev_row.data_ptr(), eng.M, eng.partner_dev.data_ptr(), eng.n,
                                st.owner_dev.data_ptr(), st.ranks_dev.data_ptr(), tr.nranks, tr.rank, self.row_base,

@@ -1975,8 +1975,18 @@ unsigned clamp_grid(int64_t n, int64_t per, int64_t cap) {
 }  // namespace
 
 int g_sample_stride = 0;   // 0 = auto (about kSampleTarget sampled elements per row)
-uint64_t g_spin_ticks_host = kSpinTicks;   // host copy of g_spin_ticks_dev (mx_topk_get)
-int g_compact_trace = 0;                   // host copy of g_ctrace_on
+// host copies of the two device-side knobs, per device: hipMemcpyToSymbol writes the CURRENT
+// device's copy of the symbol only, so mx_topk_set applies them to the current device and
+// mx_topk_get reports the current device's value (a process driving several GPUs sets
+// them per device; setting every device would create a context on each)
+constexpr int kMaxDev = 64;
+uint64_t g_spin_ticks_host[kMaxDev];       // 0 = never set on that device: kSpinTicks
+int g_compact_trace[kMaxDev];
+int cur_dev() {
+    int d = 0;
+    if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= kMaxDev) d = 0;
+    return d;
+}
 int g_compact_blocks = 0;     // persistent compaction blocks over all rows; 0 = auto: ~720 for one
                               // row (an even chunk count each), 2560 for several (same-box sweeps: one row 256 / 384 / 512 / 640 /
                               // 1024 / 2048 blocks 131 / 121 / 116.4 / 116.2 / 119 / 134 us per round,
@@ -2143,14 +2153,14 @@ extern "C" int mx_topk_set(const char* key, int64_t value) {
     if (!strcmp(key, "compact_trace")) {
         const int on = value != 0;
         MX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_ctrace_on), &on, sizeof(on)));
-        g_compact_trace = on;
+        g_compact_trace[cur_dev()] = on;
         return MX_OK;
     }
     if (!strcmp(key, "spin_ticks")) {
         MX_CHECK(value >= 0, "mx_topk_set: spin_ticks %lld", (long long)value);
         const uint64_t v = (uint64_t)value;
         MX_HIP(hipMemcpyToSymbol(HIP_SYMBOL(g_spin_ticks_dev), &v, sizeof(v)));
-        g_spin_ticks_host = v;
+        g_spin_ticks_host[cur_dev()] = v + 1;        // stored + 1: 0 marks "never set"
         return MX_OK;
     }
     if (!strcmp(key, "sample_pieces")) {
@@ -2162,8 +2172,11 @@ extern "C" int mx_topk_set(const char* key, int64_t value) {
 }
 
 extern "C" int64_t mx_topk_get(const char* key) {
-    if (key && !strcmp(key, "spin_ticks")) return (int64_t)g_spin_ticks_host;
-    if (key && !strcmp(key, "compact_trace")) return g_compact_trace;
+    if (key && !strcmp(key, "spin_ticks")) {
+        const uint64_t v = g_spin_ticks_host[cur_dev()];
+        return (int64_t)(v ? v - 1 : kSpinTicks);
+    }
+    if (key && !strcmp(key, "compact_trace")) return g_compact_trace[cur_dev()];
     if (key && !strcmp(key, "sample_stride")) return g_sample_stride;
     if (key && !strcmp(key, "compact_blocks")) return g_compact_blocks;
     if (key && !strcmp(key, "sample_pieces")) return g_sample_pieces;

@@ -19,6 +19,7 @@
 
 #include <atomic>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <thread>
 #include <vector>
@@ -514,6 +515,14 @@ extern "C" int mx_allreduce_mean(void* comm_v, float* buf, int64_t count, int nr
 extern "C" int mx_mean_rows_to(const float* rows, int nrows, int64_t ld, int64_t count, int order, float* dst,
                                int ndst, int64_t dst_ld, void* stream);
 
+// mx_mean_rows_to's 16-byte path: everything 16-byte aligned and the <= 8-row tree or rank order
+// (shared with mx_mean_kernel_name, so the name reported is the kernel launched)
+static bool mean_vec_path(const float* rows, int nrows, int64_t ld, int64_t count, int order, const float* dst,
+                          int ndst, int64_t dst_ld) {
+    return count >= 4 && ld % 4 == 0 && (ndst <= 1 || dst_ld % 4 == 0) &&
+           ((uintptr_t)rows | (uintptr_t)dst) % 16 == 0 && (order == 1 || nrows <= 8);
+}
+
 // One destination row: the same kernels as mx_mean_rows_to (identical summation order and bits).
 extern "C" int mx_mean_rows(const float* rows, int nrows, int64_t ld, int64_t count, int order, float* out,
                             void* stream) {
@@ -545,8 +554,7 @@ extern "C" int mx_mean_rows_to(const float* rows, int nrows, int64_t ld, int64_t
     }
     hipStream_t st = mx::as_stream(stream);
     const float d = (float)nrows;
-    const bool vec = count >= 4 && ld % 4 == 0 && (ndst <= 1 || dst_ld % 4 == 0) &&
-                     ((uintptr_t)rows | (uintptr_t)dst) % 16 == 0 && (order == 1 || nrows <= 8);
+    const bool vec = mean_vec_path(rows, nrows, ld, count, order, dst, ndst, dst_ld);
     if (vec) {
         const int64_t c4 = count / 4, tail = count - 4 * c4;
         if (tail) {                               // the last 1-3 columns: scalar lanes, same order
@@ -608,12 +616,13 @@ extern "C" int mx_mean_rows_to(const float* rows, int nrows, int64_t ld, int64_t
     return MX_OK;
 }
 
-// The kernel that moves the bulk of an mx_mean_rows_to call on 16-byte aligned rows (ld, dst_ld
-// multiples of 4) -- the same dispatch as above, for reports (bench.py's centralized figure).
-extern "C" const char* mx_mean_kernel_name(int nrows, int64_t count, int order) {
-    if (nrows < 1 || count < 0 || (order != 0 && order != 1)) return "invalid";
-    const bool vec = count >= 4 && (order == 1 || nrows <= 8);
-    if (vec) {
+// The kernel that moves the bulk of the mx_mean_rows_to call with the same arguments -- the same
+// dispatch as above, alignment included (nothing is launched or dereferenced), for reports
+// (bench.py's centralized figure).
+extern "C" const char* mx_mean_kernel_name(const float* rows, int nrows, int64_t ld, int64_t count, int order,
+                                           const float* dst, int ndst, int64_t dst_ld) {
+    if (nrows < 1 || count < 0 || ld < count || (order != 0 && order != 1)) return "invalid";
+    if (mean_vec_path(rows, nrows, ld, count, order, dst, ndst, dst_ld)) {
         if (nrows <= 8 && count / 4 >= 128) return order == 1 ? "mean_tile_kernel<0>" : "mean_tile_kernel<1>";
         return order == 1 ? "mean4_kernel<0, 4>" : "mean4_kernel<1, 4>";
     }
@@ -652,48 +661,77 @@ static_assert(sizeof(hipIpcMemHandle_t) == 64, "hipIpcMemHandle_t is expected to
 
 extern "C" int mx_ipc_handle_bytes(void) { return (int)sizeof(hipIpcMemHandle_t); }
 
-// Sizes are rounded up to whole 2 MiB and an allocation whose export is refused is retried
-// (the refused one held until the retry is done, so it cannot come back): late in a long test
-// session a small exportable hipMalloc was observed to be refused by hipIpcGetMemHandle with
-// "invalid argument" (profiles/r05zz2_suite_ipc_failure.log) while the same request succeeds in a
-// fresh process -- consistent with a small allocation carved from a shared block, which cannot be
-// exported on its own.
+// Export accounting: every hipIpcGetMemHandle call and every refusal is
+// counted, process-wide, and read back by engine.PullTransport.bind (mx_ipc_stats) -- the bench
+// line's ipc_refused and the multi-process tests' zero assertions come from here.  There is no retry:
+// the one refusal ever recorded (profiles/r05zz2_suite_ipc_failure.log) did not reproduce in the
+// probe that replays its allocation sequence unrounded (tests/test_gpu_round6.py, 294 exports, 0
+// refused: profiles/r06_ipc_probe.json), so a refusal is reported, not absorbed.  Sizes are still
+// rounded up to the export granule (default 2 MiB, knob "granule": a whole-page allocation of its
+// own, never a piece of a shared block).
+namespace {
+std::atomic<int64_t> g_ipc_granule{(int64_t)2 << 20};
+std::atomic<int> g_ipc_exports{0};     // hipIpcGetMemHandle calls
+std::atomic<int> g_ipc_refused{0};     // ... that returned an error
+}  // namespace
+
+extern "C" int mx_ipc_set(const char* key, int64_t value) {
+    MX_CHECK(key, "mx_ipc_set: null key");
+    if (!strcmp(key, "granule")) {
+        MX_CHECK(value >= 1 && value <= ((int64_t)1 << 30), "mx_ipc_set: granule %lld (1 .. 1 GiB)", (long long)value);
+        g_ipc_granule = value;
+        return MX_OK;
+    }
+    mx::set_error("mx_ipc_set: unknown key '%s' (granule)", key);
+    return MX_ERR_INVALID;
+}
+
+extern "C" int64_t mx_ipc_get(const char* key) {
+    if (key && !strcmp(key, "granule")) return g_ipc_granule.load();
+    return -1;
+}
+
+extern "C" int mx_ipc_stats(int* exports, int* refused) {
+    MX_CHECK(exports && refused, "mx_ipc_stats: null pointer");
+    *exports = g_ipc_exports.load();
+    *refused = g_ipc_refused.load();
+    return MX_OK;
+}
+
 extern "C" int mx_ipc_alloc(int64_t bytes, void** ptr_out, void* handle_out) {
     MX_CHECK(bytes > 0 && ptr_out && handle_out, "mx_ipc_alloc: bad arguments");
-    constexpr size_t kGran = (size_t)2 << 20;
-    constexpr int kTries = 4;
-    void* refused[kTries] = {nullptr};
-    int nref = 0;
-    hipError_t e = hipSuccess;
-    for (int t = 0; t < kTries; ++t) {
-        const size_t n = ((size_t)bytes + kGran - 1) / kGran * kGran + (size_t)t * kGran;
-        void* p = nullptr;
-        e = hipMalloc(&p, n);
-        if (e != hipSuccess) break;
-        // zero-filled (the pull header's epoch starts at 0) and complete before the handle is shared
-        e = hipMemset(p, 0, n);
-        if (e == hipSuccess) e = hipDeviceSynchronize();
-        if (e != hipSuccess) {
-            (void)hipFree(p);
-            for (int i = 0; i < nref; ++i) (void)hipFree(refused[i]);
-            mx::set_error("mx_ipc_alloc: hipMemset -> %s", hipGetErrorString(e));
-            return MX_ERR_HIP;
-        }
-        hipIpcMemHandle_t h;
-        e = hipIpcGetMemHandle(&h, p);
-        if (e == hipSuccess) {
-            for (int i = 0; i < nref; ++i) (void)hipFree(refused[i]);
-            memcpy(handle_out, &h, sizeof(h));
-            *ptr_out = p;
-            return MX_OK;
-        }
-        (void)hipGetLastError();
-        refused[nref++] = p;
+    const size_t gran = (size_t)g_ipc_granule.load();
+    const size_t n = ((size_t)bytes + gran - 1) / gran * gran;
+    void* p = nullptr;
+    MX_HIP(hipMalloc(&p, n));
+    // zero-filled (the pull header's epoch starts at 0) and complete before the handle is shared; on
+    // a private stream waited for alone -- a device-wide synchronize would also wait for other groups'
+    // rounds (a pull gate may be spinning on a peer for its whole deadline)
+    hipStream_t st = nullptr;
+    hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipMemsetAsync(p, 0, n, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (st) (void)hipStreamDestroy(st);
+    if (e != hipSuccess) {
+        (void)hipFree(p);
+        mx::set_error("mx_ipc_alloc: zero fill -> %s", hipGetErrorString(e));
+        return MX_ERR_HIP;
     }
-    for (int i = 0; i < nref; ++i) (void)hipFree(refused[i]);
-    mx::set_error("mx_ipc_alloc: %s -> %s (%d tries)", nref ? "hipIpcGetMemHandle" : "hipMalloc", hipGetErrorString(e),
-                  nref);
-    return MX_ERR_HIP;
+    hipIpcMemHandle_t h;
+    ++g_ipc_exports;
+    e = hipIpcGetMemHandle(&h, p);
+    if (e != hipSuccess) {
+        ++g_ipc_refused;
+        (void)hipGetLastError();
+        (void)hipFree(p);
+        fprintf(stderr, "[matcha_gossip] mx_ipc_alloc: hipIpcGetMemHandle refused a %zu-byte allocation (%s)\n", n,
+                hipGetErrorString(e));
+        mx::set_error("mx_ipc_alloc: hipIpcGetMemHandle -> %s (%zu bytes)", hipGetErrorString(e), n);
+        return MX_ERR_HIP;
+    }
+    memcpy(handle_out, &h, sizeof(h));
+    *ptr_out = p;
+    return MX_OK;
 }
 
 extern "C" int mx_ipc_open(const void* handle, void** ptr_out) {

@@ -82,6 +82,37 @@ __global__ __launch_bounds__(kTPB) void publish_kernel(const f4* __restrict__ sr
     }
 }
 
+// The same copy restricted to the rows a peer reads this round (mx_snapshot_publish_rows): workgroup
+// (x, r) first decides, for local row r, whether an active matching pairs worker row_base + r with
+// a worker of another block -- the rows mx_pull_gate's peers point their receive slots at -- and a
+// workgroup of an unread row leaves before its first store (so it owes no release either).
+__global__ __launch_bounds__(kTPB) void publish_rows_kernel(const f4* __restrict__ src, int64_t src_ld4,
+                                                            f4* __restrict__ dst, int64_t dst_ld4, int64_t n4,
+                                                            const uint8_t* __restrict__ flags, int M,
+                                                            const int32_t* __restrict__ partner, int n, int row_base,
+                                                            int n_local) {
+    const int r = blockIdx.y;
+    const int w = row_base + r;
+    int read = 0;
+    for (int g = threadIdx.x; g < M; g += kTPB) {
+        if (flags[g]) {
+            const int q = partner[(int64_t)g * n + w];
+            read |= q >= 0 && (q < row_base || q >= row_base + n_local);
+        }
+    }
+    if (!__syncthreads_or(read)) return;                      // workgroup-uniform
+    const f4* s = src + (int64_t)r * src_ld4;
+    f4* d = dst + (int64_t)r * dst_ld4;
+    for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < n4; i += (int64_t)gridDim.x * kTPB)
+        __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), d + i);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");        // system scope: buffer_wbl2 sc0 sc1
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+
 unsigned grid_for(int64_t total) {
     int64_t g = (total + kTile - 1) / kTile;
     if (g > 4096) g = 4096;
@@ -141,6 +172,35 @@ extern "C" int mx_snapshot_publish(const float* src, float* dst, int64_t n, void
     if (g > 4 * (int64_t)cus) g = 4 * (int64_t)cus;    // persistent: one release per workgroup at its end
     hipLaunchKernelGGL(publish_kernel, dim3((unsigned)g), dim3(kTPB), 0, mx::as_stream(stream),
                        reinterpret_cast<const f4*>(src), reinterpret_cast<f4*>(dst), n4);
+    MX_LAUNCH_CHECK();
+    return MX_OK;
+}
+
+extern "C" int mx_snapshot_publish_rows(const float* src, int64_t src_ld, float* dst, int64_t dst_ld, int64_t n,
+                                        int n_local, const uint8_t* flags_row_dev, int M, const int32_t* partner_dev,
+                                        int n_global, int row_base, void* stream) {
+    MX_CHECK(n >= 0 && n_local >= 0, "mx_snapshot_publish_rows: n %lld, n_local %d", (long long)n, n_local);
+    if (n == 0 || n_local == 0) return MX_OK;
+    MX_CHECK(src && dst && flags_row_dev && partner_dev, "mx_snapshot_publish_rows: null pointer");
+    MX_CHECK(n_local <= 65535 && M >= 1 && row_base >= 0 && row_base + n_local <= n_global,
+             "mx_snapshot_publish_rows: block [%d, %d) of %d workers, M %d", row_base, row_base + n_local, n_global, M);
+    MX_CHECK(n % 4 == 0 && src_ld % 4 == 0 && dst_ld % 4 == 0 && src_ld >= n && dst_ld >= n &&
+                 ((uintptr_t)src | (uintptr_t)dst) % 16 == 0,
+             "mx_snapshot_publish_rows: n %lld, src_ld %lld, dst_ld %lld must be multiples of 4 (ld >= n), buffers "
+             "16-byte aligned", (long long)n, (long long)src_ld, (long long)dst_ld);
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) cus = v;
+    }
+    const int64_t n4 = n / 4;
+    int64_t gx = (n4 + kTPB - 1) / kTPB;
+    const int64_t cap = (4 * (int64_t)cus + n_local - 1) / n_local;   // ~4 workgroups per CU over all rows
+    if (gx > cap) gx = cap;
+    if (gx < 1) gx = 1;
+    hipLaunchKernelGGL(publish_rows_kernel, dim3((unsigned)gx, (unsigned)n_local), dim3(kTPB), 0,
+                       mx::as_stream(stream), reinterpret_cast<const f4*>(src), src_ld / 4, reinterpret_cast<f4*>(dst),
+                       dst_ld / 4, n4, flags_row_dev, M, partner_dev, n_global, row_base, n_local);
     MX_LAUNCH_CHECK();
     return MX_OK;
 }

@@ -17,8 +17,8 @@ after the measurements, never timed and never on the measured path.
 Secondary figures (MATCHA C_b = 0.5, all-reduce, ChocoSGD, host-resident models, the WRN-28-10 /
 CIFAR-ResNet configs, the ER(64) budget sweep) each run under a watchdog deadline
 (--figure-timeout) and a total budget (--figures-budget): a figure that hangs (e.g. a peer rank
-gone) makes rank 0 print the line measured so far with an "error" field and every rank exit,
-instead of losing the headline.
+gone) makes rank 0 print the line measured so far with an "error" field and every rank exit with
+status 3 (EXIT_ABORTED), instead of losing the headline or hanging.
 """
 import argparse
 import json
@@ -55,6 +55,10 @@ PULL_TIMEOUT_S = 20.0      # the pull gate's deadline in the bench (lockstep rou
 RCCL_FIXED_S = 7.3e-6
 PEER_GONE = ("Connection closed by peer", "Connection reset by peer", "Broken pipe")   # gloo / c10d errors
 RCCL_WARMUP_WAIT_S = 60.0  # N > 1: deadline of the headline's first RCCL exchanges (then: pull transport)
+LAUNCH_BOUND_ROUNDS = 400  # rounds per measurement of a launch-bound config (P < 1e6: ~6 us rounds)
+WARM_BURST_ROUNDS = 4000   # untimed rounds before a launch-bound config's measurements (N = 1; N > 1: a tenth)
+EXIT_PARITY = 4            # exit status when the headline's oracle self-check failed (its value withheld)
+EXIT_ABORTED = 3           # exit status of a rank whose run was cut short (watchdog, peer gone, SIGTERM)
 HEADLINE_HBM_FRAC = 0.75   # the mixing kernel's measured fraction of 8 TB/s (BENCH_r04, profiles/)
 
 
@@ -158,8 +162,9 @@ def oracle_column_parity(topology, init, final, applied):
 class Watchdog:
     """Deadline on a phase of the run.  When the armed deadline passes (a collective whose peer
     never arrives, a hang), rank 0 prints the line built so far with an "error" field and every
-    rank leaves with os._exit(0) -- an exit, never an exec; a zero status so the launcher does not
-    tear down rank 0 before it has printed."""
+    rank leaves with os._exit(EXIT_ABORTED) -- an exit, never an exec, and a NON-zero status, so the
+    launcher's (and the driver's) exit code tells an aborted run from a clean one.  A rank that
+    leaves first makes the launcher SIGTERM the others: rank 0 then prints from on_term (main)."""
 
     def __init__(self, rank, emit):
         self.rank, self.emit = rank, emit
@@ -199,7 +204,7 @@ class Watchdog:
                 sys.stderr.flush()
                 if self.rank == 0:
                     self.emit(msg)
-                os._exit(0)
+                os._exit(EXIT_ABORTED)
 
 
 class Line:
@@ -289,6 +294,30 @@ def pmc_traffic(kernel_prefix="mix_kernel"):
     return (max(vals) if vals else None), os.path.relpath(files[-1], ROOT)
 
 
+RATE_KEYS = ("value", "ms_per_step", "rounds_per_s", "ms_per_round", "graph_rounds_per_s", "graph_us_per_round",
+             "hbm_TBps", "hbm_TBps_rank0", "roofline", "busiest_link_GBps")
+
+
+def withhold_unverified(obj):
+    """A figure whose oracle self-check failed reports no rate: its rate keys move under
+    "unverified" (recursively: configs' entries, the ER sweep's budgets) -- a fast wrong result is
+    not a number (the pull forms' cross-GPU coherence is pinned only by this check
+    until tests/mp_gpus.py runs on >= 2 GPUs).  Returns True if anything was withheld."""
+    hit = False
+    if isinstance(obj, dict):
+        if obj.get("parity_ok") is False:
+            moved = {k: obj.pop(k) for k in list(obj) if k in RATE_KEYS}
+            if moved:
+                obj["unverified"] = moved
+            hit = True
+        for v in list(obj.values()):
+            hit |= withhold_unverified(v)
+    elif isinstance(obj, list):
+        for v in obj:
+            hit |= withhold_unverified(v)
+    return hit
+
+
 def guarded(name, fn):
     """A secondary figure: an exception is reported in the line as {"error": ...} instead of
     losing the headline line; traceback to stderr."""
@@ -300,13 +329,28 @@ def guarded(name, fn):
         return {"error": f"{name}: {type(e).__name__}: {e}"}
 
 
-def max_over_ranks(x, world, dev):
+def max_over_ranks(x, world, dev="cpu"):
     import torch.distributed as dist
     if world == 1:
         return x
-    t = torch.tensor([x], device=dev)
+    t = torch.tensor([float(x)], device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def pull_counts(pkg, world):
+    """The pull transport's bind accounting so far, summed over ranks (collective at N > 1):
+    binds, failed binds and refused IPC exports (engine.pull_stats) -- a refusal shows here and in
+    the multi-process tests' zero checks, never silently."""
+    st = pkg.pull_stats()
+    keys = ("binds", "bind_failures", "ipc_exports", "ipc_refused")
+    v = [float(st[k]) for k in keys]
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor(v)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        v = t.tolist()
+    return {k: int(x) for k, x in zip(keys, v)}
 
 
 def barrier(world):
@@ -412,12 +456,26 @@ def round_bytes(partner, owner, flags_rows, rank, row_base, n_local, P):
     return hbm, link, pair_b, total
 
 
+def published_rows(partner, flags_rows, row_base, n_local):
+    """Mean over rounds of the local rows a pull round publishes (mx_snapshot_publish_rows): rows
+    with an active partner outside [row_base, row_base + n_local)."""
+    cnt = []
+    for f in flags_rows:
+        c = 0
+        for r in range(row_base, row_base + n_local):
+            c += any(f[g] and partner[g, r] >= 0 and not (row_base <= partner[g, r] < row_base + n_local)
+                     for g in range(len(f)))
+        cnt.append(c)
+    return float(np.mean(cnt)) if cnt else 0.0
+
+
 def predict_round(form, world, link_bytes, mix_s, publish_bytes, chunks=4, mix_source="measured"):
     """What a round of `form` should cost at N = world, from its parts: the busiest
     xGMI link's bytes at 153 GB/s, the mixing kernel on this GPU (mix_s), the form's fixed cost
     (PULL_FIXED_S measured / RCCL_FIXED_S a measured lower bound) and, for pull, the snapshot copy at the headline's
-    HBM fraction.  plain RCCL: exchange, then mix (one stream); pipelined: the longer of the two
-    plus one chunk of the shorter; pull: publish, then the mix reading partners over xGMI."""
+    HBM fraction (publish_bytes: read + write of the rows a peer reads, published_rows).  plain RCCL:
+    exchange, then mix (one stream); pipelined: the longer of the two plus one chunk of the shorter;
+    pull: publish, then the mix reading partners over xGMI."""
     t_link = link_bytes / XGMI_LINK_PEAK
     if form == "pull":
         fixed = PULL_FIXED_S.get(world, max(PULL_FIXED_S.values()))
@@ -455,12 +513,14 @@ def predict_choco(form, world, link_bytes, local_s, publish_bytes):
             "rounds_per_s": 1.0 / t if t > 0 else None}
 
 
-def p2p_probe(rank, world, nbytes, dev, reps=5):
-    """N > 1: one xGMI link through RCCL (torch.distributed send/recv on the nccl group), ranks 0
-    and 1 only: unidirectional 0 -> 1 and bidirectional 0 <-> 1, seconds per transfer (max over
-    the two ranks)."""
+def p2p_probe(rank, world, nbytes, dev, reps=5, rccl=True):
+    """N > 1: one xGMI link through RCCL (torch.distributed send/recv on an nccl group created for
+    this figure -- the job's own process group is gloo), ranks 0 and 1 only: unidirectional 0 -> 1
+    and bidirectional 0 <-> 1, seconds per transfer (max over the two ranks).  rccl=False (the gloo
+    test transport): host buffers over the gloo group."""
     import torch.distributed as dist
-    buf = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+    grp = dist.new_group(backend="nccl") if rccl else None       # collective: every rank
+    buf = torch.empty(nbytes // 4, dtype=torch.float32, device="cuda" if rccl else "cpu")
     rbuf = torch.empty_like(buf)
     res = {}
     for mode in ("uni", "bi"):
@@ -472,9 +532,9 @@ def p2p_probe(rank, world, nbytes, dev, reps=5):
                 peer = 1 - rank
                 ops = []
                 if mode == "bi" or rank == 0:
-                    ops.append(dist.P2POp(dist.isend, buf, peer))
+                    ops.append(dist.P2POp(dist.isend, buf, peer, group=grp))
                 if mode == "bi" or rank == 1:
-                    ops.append(dist.P2POp(dist.irecv, rbuf, peer))
+                    ops.append(dist.P2POp(dist.irecv, rbuf, peer, group=grp))
                 for w in dist.batch_isend_irecv(ops):
                     w.wait()
             torch.cuda.synchronize()
@@ -581,7 +641,7 @@ def allreduce_figure(pkg, args, rank, world, n, P, K, W, comm, dev, arena=None):
     if world == 1:
         alg = 2 * n * P * 4
         kern_ms = ev[0].elapsed_time(ev[1]) / K
-        kname = L.mx_mean_kernel_name(n, P, 0).decode()          # the dispatch mx_mean_rows_to launches
+        kname = L.mx_mean_kernel_name(rows.data_ptr(), n, ld, P, 0, rows.data_ptr(), n, ld).decode()   # its dispatch
         out["roofline"] = {"bound": "hbm", "kernel": f"{kname} (mx_mean_rows_to, tree order)", "bytes_per_launch": alg,
                            "avg_launch_ms": kern_ms, "achieved": alg / (kern_ms * 1e-3) / 1e9,
                            "peak": HBM_PEAK / 1e9, "unit": "GB/s", "frac": alg / (kern_ms * 1e-3) / HBM_PEAK,
@@ -732,7 +792,8 @@ def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99
         local_s = timed_loop(loc.step, W, K, world, dev) / K
         del loc
         lb = float(np.mean(link_b))
-        out["predicted"] = {f: predict_choco(f, world, lb, local_s, grp.n_local * grp.msg_ld) for f in ("rccl", "pull")}
+        pub = 2 * published_rows(eng.partner, flags, grp.row_base, grp.n_local) * grp.publish_cols * 4
+        out["predicted"] = {f: predict_choco(f, world, lb, local_s, pub) for f in ("rccl", "pull")}
         out["predicted"]["pull_direct"] = out["predicted"]["pull"]
         pr = out["predicted"][chosen]
         out["predicted"]["timed_form"] = chosen
@@ -740,6 +801,7 @@ def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99
                                     "fetch form); the calibration ranks them")
         out["predicted"]["achieved_over_predicted"] = pr["round_ms"] / (1e3 * el / K)
         out["message_bytes"] = int(grp.msg_bytes)
+        out.update(pull_counts(pkg, world))                  # collective: binds / failures / refused exports
     out["parity_ok"] = choco_oracle_round(pkg, grp, GP, W + K, ratio, gamma, rank, world)
     out["parity"] = (f"round {W + K} (after the {W} warmup / calibration + {K} timed rounds) of every worker: x, "
                      f"x_hat, s vs the oracle's Choco round from the same state, uint32")
@@ -810,46 +872,77 @@ def config_figures(pkg, args, rank, world, n, K, W, comm, dev):
     (36,546,980 params per worker) under MATCHA C_b = 0.5 and full rounds, and the repo's CIFAR
     ResNet (181,668 params, launch-bound) under MATCHA C_b = 0.5; rounds/s, at N = 1 HBM bytes / s
     over the algorithmic bytes of the rounds run, and oracle parity of every worker's 64 sampled
-    columns over every round the group ran (eager and graph-replayed)."""
+    columns over every round the group ran (eager and graph-replayed).
+
+    Every config also carries per-round HIP events (kernel time, `round_us_events`) beside the
+    host-clocked rate.  A launch-bound config (P < 1e6) runs a warm burst of untimed rounds first
+    (an idle GPU's clocks ramp over ~10 ms of work: profiles/r02_clock_ramp.log) and at least
+    LAUNCH_BOUND_ROUNDS rounds per measurement, so the fixed cost of the two host barriers and
+    synchronizes around the timed region is not spread over a handful of 6-us rounds (the driver's
+    --steps 20 against the builder's 50 explained its 8.1 vs 6.0 us)."""
     out = {}
     for name, P, budget in (("wrn28_10_matcha0.5", args.wrn_params, 0.5), ("wrn28_10_full", args.wrn_params, 1.0),
                             ("resnet18_100_matcha0.5", args.resnet_params, 0.5)):
+        lb = P < 1_000_000
+        Kc = max(K, LAUNCH_BOUND_ROUNDS) if lb else K
+        warm = (WARM_BURST_ROUNDS if world == 1 else WARM_BURST_ROUNDS // 10) if lb else 0
         np.random.seed(1234)
-        GPc = pkg.MatchaProcessor(pkg.select_graph(0), budget, rank, n, W + K, True)
+        GPc = pkg.MatchaProcessor(pkg.select_graph(0), budget, rank, n, W + warm + 3 * Kc, True)
         g = pkg.VirtualWorkerGroup(GPc, numel=P, rank=rank, nranks=world, comm=comm, placement=args.placement)
         fill_synth(pkg, g)
-        applied = list(range(W + K))
-        for it in range(W):
+        applied = list(range(W + warm + 3 * Kc))
+        for it in range(W + warm):                # warmup + warm burst (untimed)
             g.step(it)
-        el = timed_loop(g.step, W, K, world, dev)
+        torch.cuda.synchronize()
+        ev = timed_rounds(lambda grp, it: grp.step(it), g, W + warm, Kc)    # per-round events
+        torch.cuda.synchronize()
+        us = np.array([a.elapsed_time(b) for a, b in ev]) * 1e3
+        blk = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+        blk[0].record()                           # one event pair around Kc back-to-back rounds
+        for it in range(W + warm + Kc, W + warm + 2 * Kc):
+            g.step(it)
+        blk[1].record()
+        torch.cuda.synchronize()
+        blk_us = 1e3 * blk[0].elapsed_time(blk[1]) / Kc
+        first = W + warm + 2 * Kc
+        el = timed_loop(g.step, first, Kc, world, dev)
         partner = np.asarray(GPc.neighbors_info, np.int32)
         byts = 0
-        for f in np.asarray(GPc.active_flags[W:W + K], np.uint8):
+        for f in np.asarray(GPc.active_flags[first:first + Kc], np.uint8):
             deg = (partner[f.astype(bool)] >= 0).sum(axis=0) if f.any() else np.zeros(n, int)
             byts += 2 * int((deg > 0).sum()) * P * 4
-        out[name] = {"params_per_worker": P, "budget": budget, "rounds_per_s": K / el, "ms_per_round": 1e3 * el / K,
+        out[name] = {"params_per_worker": P, "budget": budget, "rounds_per_s": Kc / el, "ms_per_round": 1e3 * el / Kc,
+                     "rounds": Kc, "warm_rounds": warm,
+                     "round_us_events": {"median": float(np.median(us)), "min": float(us.min()),
+                                         "mean": float(us.mean()), "block_per_round": blk_us,
+                                         "note": f"this rank's GPU time per round, no host barrier / synchronize: "
+                                                 f"median / min / mean of per-round HIP event pairs over {Kc} "
+                                                 f"rounds (each pair adds its own records between launches), "
+                                                 f"block_per_round = one event pair around {Kc} back-to-back "
+                                                 f"rounds / {Kc}"},
                      "hbm_TBps": byts / el / 1e12 if world == 1 else None}
-        if world == 1 and P < 1_000_000:
-            # launch-bound rows: the same K rounds replayed from one captured HIP graph
+        if world == 1 and lb:
+            # launch-bound rows: the timed rounds replayed from one captured HIP graph
             # (device_rounds: the rounds read their iteration from a device counter)
             gr = torch.cuda.CUDAGraph()
             cs = torch.cuda.Stream()
             cs.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(cs):
                 with torch.cuda.graph(gr):
-                    g.device_rounds(K)
+                    g.device_rounds(Kc)
             torch.cuda.synchronize()
-            g.iter_dev.fill_(W)
+            g.iter_dev.fill_(first)
             gr.replay()                           # warm replay of the same rounds' shapes
-            g.iter_dev.fill_(W)
+            g.iter_dev.fill_(first)
             torch.cuda.synchronize()
             t = time.perf_counter()
             gr.replay()
             torch.cuda.synchronize()
             elg = time.perf_counter() - t
-            applied += list(range(W, W + K)) * 2
-            out[name]["graph_rounds_per_s"] = K / elg
-            out[name]["graph_note"] = f"{K} rounds (iterations {W}..{W + K - 1}) replayed from one HIP graph"
+            applied += list(range(first, first + Kc)) * 2
+            out[name]["graph_rounds_per_s"] = Kc / elg
+            out[name]["graph_us_per_round"] = 1e6 * elg / Kc
+            out[name]["graph_note"] = f"{Kc} rounds (iterations {first}..{first + Kc - 1}) replayed from one HIP graph"
             del gr
         cols = sample_columns(P)
         final = gather_columns(g, torch.from_numpy(cols).cuda(), world, dev)
@@ -953,6 +1046,7 @@ def er_figure(pkg, args, rank, world, comm, dev):
         applied += list(range(Wer, Wer + Ker))
         flags = np.asarray(GPb.active_flags, np.uint8)[Wer:Wer + Ker]
         eng = g.engine
+        g_row_base = g.row_base
         hbm, link, _, _ = round_bytes(eng.partner, eng.owner, flags, rank, g.row_base, g.n_local, P)
         xo = None
         if world > 1 and chosen == "rccl" and flags.any():        # whole rows into the slab: plain form only
@@ -970,7 +1064,8 @@ def er_figure(pkg, args, rank, world, comm, dev):
         pred = None
         if world > 1:
             mix_est = float(np.mean(hbm)) / (HEADLINE_HBM_FRAC * HBM_PEAK)
-            pred = predict_round(chosen, world, float(np.mean(link)), mix_est, 2 * n_local * P * 4,
+            pub = 2 * published_rows(eng.partner, flags, g_row_base, n_local) * P * 4
+            pred = predict_round(chosen, world, float(np.mean(link)), mix_est, pub,
                                  mix_source="this GPU's algorithmic HBM bytes at the headline kernel's 0.75 of 8 TB/s")
             pred["achieved_over_predicted"] = pred["round_ms"] / (1e3 * el / Ker)
         row = {"budget": b, "rounds_per_s": Ker / el, "ms_per_round": 1e3 * el / Ker, "predicted": pred,
@@ -1114,6 +1209,16 @@ def self_launch(args, argv, popen=None):
     return rc
 
 
+def term_handler(line, wd):
+    """SIGTERM (the launcher stops every rank when one fails or leaves): rank 0 prints the line so
+    far with an "error" naming the running phase, and the rank exits EXIT_ABORTED."""
+    def on_term(signum, _frame):
+        line.emit(f"terminated by signal {signum} during {wd.name or 'the run'} (the launcher stops every rank "
+                  f"when one rank fails or leaves)")
+        os._exit(EXIT_ABORTED)
+    return on_term
+
+
 def main():
     """The run happens on a worker thread; the main thread only waits, so it stays free to take
     SIGTERM -- what the launcher (torchrun) sends every rank when one rank dies -- and rank 0
@@ -1129,17 +1234,13 @@ def main():
     line = Line(rank)
     wd = Watchdog(rank, line.emit)
     failed = []
+    signal.signal(signal.SIGTERM, term_handler(line, wd))
 
-    def on_term(signum, _frame):
-        line.emit(f"terminated by signal {signum} during {wd.name or 'the run'} (the launcher stops every rank "
-                  f"when one rank fails)")
-        os._exit(0)
-
-    signal.signal(signal.SIGTERM, on_term)
+    status = [0]
 
     def body():
         try:
-            run(args, world, rank, line, wd)
+            run(args, world, rank, line, wd, status)
         except BaseException as e:                   # noqa: BLE001 -- reported in the line, then re-raised
             import traceback
             traceback.print_exc()
@@ -1152,9 +1253,13 @@ def main():
         t.join(0.5)
     if failed:
         sys.exit(1)
+    if status[0]:
+        sys.exit(status[0])
 
 
-def run(args, world, rank, line, wd):
+def run(args, world, rank, line, wd, status=None):
+    """The whole run; status[0] is set to EXIT_PARITY (rank 0) when the headline's self-check fails."""
+    status = status if status is not None else [0]
     local = int(os.environ.get("LOCAL_RANK", "0"))
     wd.arm("startup (process group / RCCL communicator)", args.headline_timeout)
     import datetime
@@ -1164,12 +1269,14 @@ def run(args, world, rank, line, wd):
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     pg_timeout = datetime.timedelta(seconds=args.pg_timeout)
-    if world > 1 and gloo:
+    if world > 1:
+        # the job's own agreement, timing barriers, max-over-ranks and result gathers run over gloo
+        # (host tensors) whatever the gossip transport: none of them depends on RCCL, so the no-RCCL
+        # fallback below really does without it and a collective never queues behind an
+        # RCCL kernel on the GPU stream.  RCCL itself is the library's communicator (RcclComm,
+        # bootstrapped over this group) and torch's nccl group of the p2p probe figure.
         dist.init_process_group("gloo", rank=rank, world_size=world, timeout=pg_timeout)
-    elif world > 1:
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local),
-                                timeout=pg_timeout)
-    dev = "cpu" if gloo else "cuda"
+    dev = "cpu"
     import importlib
     pkg = importlib.import_module(PKG_NAME)
     comm = None
@@ -1303,6 +1410,10 @@ def run(args, world, rank, line, wd):
     if pull_only:
         overlap = {"mode": args.overlap, "pull": args.pull, "chosen_form": "pull", "calib_ms": None,
                    "note": "the library's RCCL communicator was unavailable (rccl_unavailable): pull transport only"}
+    if world > 1:
+        ipc = pull_counts(pkg, world)                       # collective
+        if overlap is not None:
+            overlap.update(ipc)
     # per-round HIP events of the whole round (diagnostic): real rounds run BEFORE the timed region,
     # in blocks of K, for at least --settle-ms (an idle MI355X takes ~10 ms of streaming to reach
     # its steady clocks: profiles/r02_clock_ramp.log), so the timed rounds measure the steady state of the loop
@@ -1453,7 +1564,7 @@ def run(args, world, rank, line, wd):
         # the expected round of every form, from its parts (achieved / predicted names the term that is off)
         mix_s = float(np.median(mix_ms)) * 1e-3
         mix_s = max_over_ranks(mix_s, world, dev)
-        pub = 2 * group.n_local * P * 4
+        pub = 2 * published_rows(partner, flags, group.row_base, group.n_local) * P * 4   # read + write
         chunks = overlap.get("chunks") if overlap and overlap.get("chunks") else 4
         out["predicted"] = {f: predict_round(f, world, lb, mix_s, pub, chunks,
                                              "mixing-alone launches of this run (max over ranks)")
@@ -1470,6 +1581,12 @@ def run(args, world, rank, line, wd):
         out["parity"] = (f"every worker's {len(cols)} sampled columns after all {len(applied[id(timed)])} rounds "
                          f"this run applied, vs the CPU oracle's decen rounds (oracle/matcha_oracle.c) on the "
                          f"same columns from the same synthetic initial values (uint32 compare)")
+        if not out["parity_ok"]:
+            # a wrong result is not a throughput: the headline value is withheld and the run fails
+            out["unverified"] = {"value": out.pop("value"), "ms_per_step": out.pop("ms_per_step")}
+            out["value"], out["ms_per_step"] = None, None
+            out["error"] = "headline: the oracle self-check failed -- value withheld (unverified)"
+            status[0] = EXIT_PARITY
 
     # ------------------------------------------------------------------ secondary figures
     t_fig = time.monotonic()
@@ -1498,12 +1615,14 @@ def run(args, world, rank, line, wd):
             time.sleep(10 * args.figure_timeout)
         res = guarded(name, fn)
         wd.disarm()
+        if rank == 0 and withhold_unverified(res):
+            sys.stderr.write(f"[bench] {name}: oracle self-check FAILED -- its rates are withheld (unverified)\n")
         if world > 1 and isinstance(res, dict) and any(m in str(res.get("error", "")) for m in PEER_GONE):
             # a peer rank left the job (its watchdog fired first, or it died): no later collective
             # can complete -- as the watchdog does, rank 0 prints the line so far and every rank leaves
             line.emit(f"{name}: no progress -- a peer rank left the job ({res['error']}); the figures after it "
                       f"were not run")
-            os._exit(0)
+            os._exit(EXIT_ABORTED)
         return res
 
     if world > 1 and not pull_only:
@@ -1517,7 +1636,7 @@ def run(args, world, rank, line, wd):
         xo = figure("exchange_only", _xo)
         if isinstance(xo, dict):
             out["xgmi"]["exchange_only_error"] = xo
-        probe = figure("p2p_probe", lambda: p2p_probe(rank, world, P * 4, dev))
+        probe = figure("p2p_probe", lambda: p2p_probe(rank, world, P * 4, dev, rccl=not gloo))
         if probe and "uni" in probe:
             out["xgmi"]["p2p_probe"] = {"bytes": P * 4, "uni_ms": 1e3 * probe["uni"],
                                         "uni_GBps": P * 4 / probe["uni"] / 1e9, "bi_ms": 1e3 * probe["bi"],
@@ -1553,6 +1672,8 @@ def run(args, world, rank, line, wd):
                             bool(args.configs))
     out["er64_sweep"] = figure("er64", lambda: er_figure(pkg, args, rank, world, comm, dev), bool(args.er))
     out["figures_s"] = time.monotonic() - t_fig
+    if world > 1:
+        out["pull_transport"] = pull_counts(pkg, world)     # the whole run's binds, summed over ranks
     line.emit()
     if world > 1:
         wd.arm("teardown", args.figure_timeout)

@@ -232,7 +232,9 @@ size_t mx_topk_work_bytes(int64_t P);
  * scratch (diagnostic, tools/select_trace.py).
  * Knobs tune speed only, never results -- except the test knob "spin_ticks": the bounded row-barrier
  * waits' deadline in 100 MHz ticks (default 2^28, ~2.7 s); 0 makes every wait that has to wait
- * expire, so tests can drive the error path below on purpose.
+ * expire, so tests can drive the error path below on purpose.  "spin_ticks" and "compact_trace"
+ * live on the device: they apply to the CURRENT device only (set them per device in a process
+ * driving several), and mx_topk_get reports the current device's value; every other knob is host-side.
  * mx_topk_get also reads "hist_grid" (the last call's first-candidate-pass grid per row) and
  * "hist_capacity" (the co-resident block cap that grid was held to with sampling on, 0 without). */
 int mx_topk_set(const char* key, int64_t value);
@@ -372,6 +374,15 @@ int mx_exchange_round(void* comm, const uint8_t* flags_row, int M, const int32_t
  * aligned), and every workgroup ends with a system-scope release (its stores written back past
  * this GPU's L2 to HBM), so a peer's load over xGMI after the round's barrier sees them. */
 int mx_snapshot_publish(const float* src, float* dst, int64_t n, void* stream);
+/* The same copy for only the rows a peer reads this round: local row r
+ * (0 <= r < n_local, worker row_base + r) is copied -- src + r * src_ld -> dst + r * dst_ld, n floats
+ * (multiple of 4, all 16-byte aligned), then the system-scope release -- iff some matching g with
+ * flags_row_dev[g] != 0 pairs it with a worker outside [row_base, row_base + n_local) (partner_dev
+ * int32 [M][n_global]: the set mx_pull_gate's peers point their slots at); other rows are not
+ * touched.  One launch, n_local rows of workgroups; the row test runs on the device. */
+int mx_snapshot_publish_rows(const float* src, int64_t src_ld, float* dst, int64_t dst_ld, int64_t n, int n_local,
+                             const uint8_t* flags_row_dev, int M, const int32_t* partner_dev, int n_global,
+                             int row_base, void* stream);
 /* Plan word [2] bit 1: the receive slots of these records point at peer GPUs' IPC-mapped memory;
  * the mixing kernels then start with a system-scope acquire per workgroup (buffer_inv sc0 sc1: no
  * line of a peer's buffer cached on this GPU from an earlier round is served).  on = 1 / 0. */
@@ -412,7 +423,17 @@ int mx_pull_fetch(const int64_t* slot_ptrs_dev, int n_local, int max_remote, con
 int mx_host_words(int n, int32_t** host_out, int32_t** dev_out);
 int mx_host_words_free(int32_t* host);
 int mx_ipc_handle_bytes(void);
+/* A zero-filled device buffer of at least `bytes` whose IPC handle is exported: the size is rounded up
+ * to the export granule (default 2 MiB); a refused export (hipIpcGetMemHandle) is logged to stderr,
+ * counted (mx_ipc_stats) and returned as MX_ERR_HIP -- no retry. */
 int mx_ipc_alloc(int64_t bytes, void** ptr_out, void* handle_out);
+/* Export accounting, process-wide since load: hipIpcGetMemHandle calls and refusals (engine.PullTransport
+ * reads the deltas around bind: the bench line's ipc_refused, the multi-process tests' zero checks). */
+int mx_ipc_stats(int* exports, int* refused);
+/* mx_ipc_alloc's knob "granule" (bytes, 1 = unrounded .. 1 GiB); mx_ipc_get returns it (-1: unknown
+ * key).  Test hook of the export-refusal probe (tests/test_gpu_round6.py). */
+int mx_ipc_set(const char* key, int64_t value);
+int64_t mx_ipc_get(const char* key);
 int mx_ipc_open(const void* handle, void** ptr_out);
 int mx_ipc_close(void* ptr);
 int mx_ipc_free(void* ptr);
@@ -440,13 +461,14 @@ int mx_mean_rows(const float* rows, int nrows, int64_t ld, int64_t count, int or
  * row with the mean in place (each column of every row is read before that column is written);
  * after an mx_allgather, dst = this rank's own rows.  16-byte accesses when everything is 16-byte
  * aligned and the order is the <= 8-row tree or rank order; up to 8 rows in 512-column tiles
- * staged in LDS. */
+ * staged in LDS.  A dst that overlaps the rows other than at whole-row offsets (offset and dst_ld
+ * multiples of ld) is refused (MX_ERR_INVALID). */
 int mx_mean_rows_to(const float* rows, int nrows, int64_t ld, int64_t count, int order, float* dst, int ndst,
                     int64_t dst_ld, void* stream);
-/* The kernel that carries the bulk of mx_mean_rows_to(nrows, count, order) on 16-byte aligned rows
- * (static string, e.g. "mean_tile_kernel<1>"), for reports.  A dst that overlaps the rows other
- * than at whole-row offsets (offset and dst_ld multiples of ld) is refused (MX_ERR_INVALID). */
-const char* mx_mean_kernel_name(int nrows, int64_t count, int order);
+/* The kernel that carries the bulk of mx_mean_rows_to with the same arguments (static string, e.g.
+ * "mean_tile_kernel<1>"; the same dispatch, alignment included; nothing launched), for reports. */
+const char* mx_mean_kernel_name(const float* rows, int nrows, int64_t ld, int64_t count, int order, const float* dst,
+                                int ndst, int64_t dst_ld);
 
 /* ---------------------------------------------------------------- host: matching decomposition
  * nx.max_weight_matching (graph_manager.py:64, inside GraphProcessor.getSubGraphs 57-83) without

@@ -14,6 +14,34 @@ for p in (ROOT, os.path.join(ROOT, "oracle")):
         sys.path.insert(0, p)
 
 
+def pull_clean(pkg, min_binds=1):
+    """The multi-process scripts' zero check: this process bound the pull
+    transport at least `min_binds` times, no bind failed and the library refused no IPC export
+    (pkg.pull_stats -> mx_ipc_stats) -- a refusal fails the test instead of vanishing."""
+    st = pkg.pull_stats()
+    ok = st["binds"] >= min_binds and st["bind_failures"] == 0 and st["ipc_refused"] == 0
+    if not ok:
+        sys.stderr.write(f"[pull_clean] {st}\n")
+    return ok
+
+
+def report_rank_errors(main):
+    """Run a multi-process script's main(); an exception on this rank is printed to stderr as
+    '[rank R] ...' lines (the test's _why() shows them) before the rank exits 1, so a rank that
+    leaves early always says why -- e.g. a refusal inside PullTransport.bind."""
+    try:
+        main()
+    except SystemExit:
+        raise
+    except BaseException:                        # noqa: BLE001 -- printed, then the rank fails
+        import traceback
+        rank = os.environ.get("RANK", "?")
+        for line in traceback.format_exc().splitlines():
+            sys.stderr.write(f"[rank {rank}] {line}\n")
+        sys.stderr.flush()
+        sys.exit(1)
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
 

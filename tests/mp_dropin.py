@@ -21,7 +21,7 @@ for p in (ROOT, HERE, os.path.join(ROOT, "oracle")):
     if p not in sys.path:
         sys.path.insert(0, p)
 import oracle as O  # noqa: E402
-from conftest import PKG_NAME  # noqa: E402
+from conftest import PKG_NAME, pull_clean, report_rank_errors  # noqa: E402
 from gloo_transport import GlooTransport  # noqa: E402
 
 
@@ -114,6 +114,7 @@ def main():
            "decen_gpu_models_pull": decen_case(pkg, pkg.PullTransport(), "cuda"),
            "choco_gpu_models_pull": choco_case(pkg, pkg.PullTransport(), "cuda"),
            "choco_cpu_models_pull": choco_case(pkg, pkg.PullTransport(), "cpu")}
+    res["pull_ipc_clean"] = pull_clean(pkg, min_binds=3)
     torch.cuda.synchronize()
     flags = [None] * dist.get_world_size()
     dist.all_gather_object(flags, all(res.values()))
@@ -125,4 +126,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    report_rank_errors(main)

@@ -19,7 +19,7 @@ ROOT = os.path.dirname(HERE)
 for p in (ROOT, HERE, os.path.join(ROOT, "oracle")):
     if p not in sys.path:
         sys.path.insert(0, p)
-from conftest import PKG_NAME  # noqa: E402
+from conftest import PKG_NAME, pull_clean, report_rank_errors  # noqa: E402
 import mp_worker as W  # noqa: E402
 import mp_pull_stress as ST  # noqa: E402
 
@@ -48,6 +48,7 @@ def main():
         "pull_stress_choco_fetch": ST.choco(pkg, dist.get_rank(), dist.get_world_size(), "fetch"),
         "pull_stress_choco_direct": ST.choco(pkg, dist.get_rank(), dist.get_world_size(), "direct"),
     }
+    res["pull_ipc_clean"] = pull_clean(pkg, min_binds=7)
     torch.cuda.synchronize()
     flags = [None] * dist.get_world_size()
     dist.all_gather_object(flags, all(res.values()))
@@ -60,4 +61,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    report_rank_errors(main)

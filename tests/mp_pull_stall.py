@@ -20,7 +20,7 @@ ROOT = os.path.dirname(HERE)
 for p in (ROOT, HERE):
     if p not in sys.path:
         sys.path.insert(0, p)
-from conftest import PKG_NAME, Topo  # noqa: E402
+from conftest import PKG_NAME, Topo, pull_clean, report_rank_errors  # noqa: E402
 
 TIMEOUT_S = 2.0
 
@@ -53,6 +53,7 @@ def main():
             res["sticky"] = False
         except pkg.MXError:
             res["sticky"] = True
+    res["pull_ipc_clean"] = pull_clean(pkg, min_binds=1)
     objs = [None, None]
     dist.all_gather_object(objs, res)
     grp._pull.close()                               # the ranks met above; nothing reads any more
@@ -60,10 +61,11 @@ def main():
     if rank == 0:
         out = dict(objs[0])
         out["peer_round_ok"] = bool(objs[1].get("peer_round_ok"))
+        out["pull_ipc_clean"] = all(o["pull_ipc_clean"] for o in objs)
         print(json.dumps(out), flush=True)
     dist.barrier()
     dist.destroy_process_group()
 
 
 if __name__ == "__main__":
-    main()
+    report_rank_errors(main)

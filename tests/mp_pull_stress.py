@@ -21,7 +21,7 @@ for p in (ROOT, HERE, os.path.join(ROOT, "oracle")):
     if p not in sys.path:
         sys.path.insert(0, p)
 import oracle as O  # noqa: E402
-from conftest import PKG_NAME, Topo  # noqa: E402
+from conftest import PKG_NAME, Topo, pull_clean, report_rank_errors  # noqa: E402
 from gloo_transport import gather_rows  # noqa: E402
 from mp_worker import by_worker  # noqa: E402
 
@@ -91,6 +91,7 @@ def main():
     res = {"decen_g2": decen(pkg, rank, world),
            "choco_fetch": choco(pkg, rank, world, "fetch"),
            "choco_direct": choco(pkg, rank, world, "direct")}
+    res["pull_ipc_clean"] = pull_clean(pkg, min_binds=3)
     torch.cuda.synchronize()
     flags = [None] * world
     dist.all_gather_object(flags, all(res.values()))
@@ -102,4 +103,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    report_rank_errors(main)

@@ -19,7 +19,7 @@ ROOT = os.path.dirname(HERE)
 for p in (ROOT, HERE):
     if p not in sys.path:
         sys.path.insert(0, p)
-from conftest import PKG_NAME  # noqa: E402
+from conftest import PKG_NAME, pull_clean, report_rank_errors  # noqa: E402
 from gloo_transport import GlooTransport  # noqa: E402
 
 
@@ -59,6 +59,7 @@ def main():
     res = {"decen_gloo": case(pkg, H, False, GlooTransport(pkg), rank, world),
            "decen_pull": case(pkg, H, False, pkg.PullTransport(), rank, world),
            "choco_pull": case(pkg, H, True, pkg.PullTransport(), rank, world)}
+    res["pull_ipc_clean"] = pull_clean(pkg, min_binds=2)
     torch.cuda.synchronize()
     if rank == 0:
         print(json.dumps({"world": world, **res}), flush=True)
@@ -68,4 +69,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    report_rank_errors(main)

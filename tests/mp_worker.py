@@ -19,7 +19,7 @@ for p in (ROOT, HERE, os.path.join(ROOT, "oracle")):
     if p not in sys.path:
         sys.path.insert(0, p)
 import oracle as O  # noqa: E402
-from conftest import PKG_NAME, Topo  # noqa: E402
+from conftest import PKG_NAME, Topo, pull_clean, report_rank_errors  # noqa: E402
 from gloo_transport import GlooTransport, gather_rows  # noqa: E402
 from reforder import mpi4py_sum as _mpi4py_sum  # noqa: E402
 
@@ -236,6 +236,7 @@ def main():
         "choco_g0_pull_k1": choco_case(pkg, pkg.PullTransport(), 1_000, 0.9995, 5, seed=3, back_to_back=True),
         "choco_g0_pull_odd_k": choco_case(pkg, pkg.PullTransport(), 12_389, 0.99, 5, seed=4),
     }
+    res["pull_ipc_clean"] = pull_clean(pkg, min_binds=8)     # no refused export, no failed bind
     torch.cuda.synchronize()
     if dist.get_rank() == 0:
         print(json.dumps({"world": dist.get_world_size(), **res}), flush=True)
@@ -245,4 +246,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    report_rank_errors(main)

@@ -96,3 +96,66 @@ def test_oracle_central_mean_is_mpi4py_order(O, n, order):
     want = mpi4py_sum(list(X), order) / np.float32(n)
     got = O.central_mean(X, order)
     assert np.array_equal(got.view(np.uint32), want.astype(np.float32).view(np.uint32))
+
+
+_WD_SCRIPT = r"""
+import os, signal, sys, time
+sys.path.insert(0, {root!r})
+import bench
+line = bench.Line(0)
+line.out["value"] = 1.0
+wd = bench.Watchdog(0, line.emit)
+if {mode!r} == "watchdog":
+    wd.arm("figure_x", 0.5)
+    time.sleep(30)
+else:
+    wd.arm("figure_y", 600)
+    signal.signal(signal.SIGTERM, bench.term_handler(line, wd))
+    print("ready", file=sys.stderr, flush=True)
+    time.sleep(30)
+"""
+
+
+@pytest.mark.parametrize("mode", ["watchdog", "sigterm"])
+def test_aborted_run_exits_nonzero_with_one_error_line(mode):
+    """a figure that hangs (the watchdog's deadline) or a SIGTERM from the
+    launcher prints the line so far with an "error" field ONCE and exits EXIT_ABORTED (3), never 0,
+    so the driver's exit code tells an aborted N > 1 bench from a clean one."""
+    import signal
+    import time
+    p = subprocess.Popen([sys.executable, "-c", _WD_SCRIPT.format(root=ROOT, mode=mode)], cwd=ROOT,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    if mode == "sigterm":
+        t0 = time.time()
+        while p.stderr.readline().strip() != "ready":
+            assert time.time() - t0 < 120 and p.poll() is None
+        p.send_signal(signal.SIGTERM)
+    out, err = p.communicate(timeout=120)
+    import bench
+    assert p.returncode == bench.EXIT_ABORTED == 3, err[-2000:]
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, out
+    d = json.loads(lines[0])
+    assert d["value"] == 1.0 and d["error"], d
+    if mode == "watchdog":
+        assert "figure_x" in d["error"] and "no progress" in d["error"]
+    else:
+        assert "figure_y" in d["error"] and "signal 15" in d["error"]
+
+
+def test_failed_self_check_withholds_rates():
+    """a figure whose oracle self-check failed reports no rate -- its rate keys move
+    under "unverified", recursively (configs' entries, the ER sweep's budgets); passing ones keep
+    theirs."""
+    import bench
+    fig = {"rounds_per_s": 5.0, "parity_ok": True,
+           "a": {"rounds_per_s": 1.0, "ms_per_round": 1.0, "parity_ok": False, "budget": 0.5},
+           "sweep": [{"rounds_per_s": 2.0, "parity_ok": True}, {"rounds_per_s": 3.0, "hbm_TBps_rank0": 4.0,
+                                                              "parity_ok": False}]}
+    assert bench.withhold_unverified(fig) is True
+    assert fig["rounds_per_s"] == 5.0 and fig["sweep"][0]["rounds_per_s"] == 2.0
+    assert "rounds_per_s" not in fig["a"] and fig["a"]["unverified"] == {"rounds_per_s": 1.0, "ms_per_round": 1.0}
+    assert fig["a"]["budget"] == 0.5
+    assert fig["sweep"][1]["unverified"] == {"rounds_per_s": 3.0, "hbm_TBps_rank0": 4.0}
+    assert bench.withhold_unverified({"rounds_per_s": 1.0, "parity_ok": True}) is False
+    assert bench.withhold_unverified(None) is False

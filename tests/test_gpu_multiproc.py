@@ -29,9 +29,10 @@ def _port():
 
 def _why(r):
     """the failing ranks' own error lines first (the launcher's summary hides them), then the tails"""
-    err = [l for l in r.stderr.splitlines() if ("Error" in l or "error" in l or "Traceback" in l)
-           and "Gloo" not in l and "error_file" not in l]
-    return "\n".join(err[:40]) + "\n--- stdout ---\n" + r.stdout[-2000:] + "\n--- stderr ---\n" + r.stderr[-2000:]
+    err = [l for l in r.stderr.splitlines() if (l.startswith("[rank ") or l.startswith("[matcha_gossip]") or
+                                                 l.startswith("[pull_clean]") or "Error" in l or "error" in l or
+                                                 "Traceback" in l) and "Gloo" not in l and "error_file" not in l]
+    return "\n".join(err[:80]) + "\n--- stdout ---\n" + r.stdout[-2000:] + "\n--- stderr ---\n" + r.stderr[-2000:]
 
 
 def _torchrun(nproc, args, timeout=200):
@@ -80,6 +81,10 @@ def test_bench_multiprocess_path(nproc):
     assert set(out["choco"]["calib_ms"]) == {"rccl", "pull", "pull_direct"}
     assert out["choco"]["form"] in ("rccl", "pull", "pull_direct")
     assert out["choco"]["pull_unavailable"] is None
+    # every pull bind of the run succeeded with no refused IPC export
+    for obj in (out["overlap"], out["choco"], out["pull_transport"]):
+        assert obj["ipc_refused"] == 0 and obj["bind_failures"] == 0, obj
+    assert out["pull_transport"]["binds"] >= out["choco"]["binds"] > 0
     cp = out["choco"]["predicted"]
     for f in ("rccl", "pull"):
         assert cp[f]["busiest_link_bytes"] > 0 and cp[f]["local_ms"] > 0 and cp[f]["round_ms"] > 0, cp[f]
@@ -112,17 +117,18 @@ def test_bench_watchdog_line_on_hang():
     """A rank that skips a figure's collectives (--debug-skip allreduce:1) desynchronises the job:
     its peer waits in the figure (then the watchdog fires), or the mismatched collectives abort a
     rank and the launcher SIGTERMs the others.  Either way rank 0 prints the line measured so far
-    -- the headline intact -- with an "error" field, and the job ends instead of hanging (the exit
-    status is the launcher's: non-zero when a rank aborted)."""
+    -- the headline intact -- with an "error" field, and the job ends instead of hanging, with a
+    NON-zero exit status (the driver's rc must tell an aborted run from a
+    clean one)."""
     r = _torchrun(2, ["bench.py", "--gpus", "2", "--transport", "gloo", "--steps", "3", "--warmup", "1",
                       "--params", "100000", "--cpu-seconds", "0", "--configs", "0", "--er", "0",
                       "--figure-timeout", "15", "--debug-skip", "allreduce:1"], timeout=240)
+    assert r.returncode != 0, _why(r)
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, _why(r)
     out = json.loads(lines[0])
     assert out["value"] > 0 and out["parity_ok"] is True
-    errs = [out.get("error")] + [v.get("error") for v in out.values() if isinstance(v, dict)]
-    assert any(errs), out
+    assert out.get("error"), out
 
 
 @pytest.mark.parametrize("nproc,overlap,pull", [(2, "on", "off"), (4, "off", "off"), (2, "off", "on"),
@@ -149,6 +155,10 @@ def test_bench_multiprocess_overlap_forms(nproc, overlap, pull):
         ch = out["choco"]
         assert ch["form"] in ("pull", "pull_direct") and ch["pull_rounds"] >= 6 and ch["pull_gate_error"] is None, ch
         assert ch["parity_ok"] is True, ch
+        assert ch["ipc_refused"] == 0 and ch["bind_failures"] == 0 and ch["binds"] > 0, ch
+    if pull != "off":
+        ov = out["overlap"]
+        assert ov["ipc_refused"] == 0 and ov["bind_failures"] == 0 and ov["binds"] > 0, ov
     elif overlap == "off" and pull == "off":
         assert out["overlap"] is None
     else:
@@ -176,6 +186,8 @@ def test_bench_falls_back_to_pull_without_rccl():
     assert all(v["parity_ok"] is True for k, v in cf.items() if k != "parity"), cf
     assert out["er64_sweep"]["form"] == "pull" and out["er64_sweep"]["parity_ok"] is True
     assert "skipped" in out["allreduce_baseline"] and out["xgmi"]["exchange_only_ms"] is None
+    pt = out["pull_transport"]
+    assert pt["binds"] > 0 and pt["ipc_refused"] == 0 and pt["bind_failures"] == 0, pt
 
 
 def test_pull_gate_stalled_peer_raises():
@@ -187,6 +199,7 @@ def test_pull_gate_stalled_peer_raises():
     assert r.returncode == 0, _why(r)
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["first_rounds_ok"] and out["raised"] and out["sticky"] and out["peer_round_ok"], out
+    assert out["pull_ipc_clean"], out
     assert "rank 1 did not publish" in out["message"], out
     assert 1.5 <= out["seconds"] < 30, out
 
@@ -257,17 +270,19 @@ def test_rccl_single_rank_linkage():
 
 def test_bench_watchdog_line_on_stall():
     """A rank that hangs inside a figure (--debug-stall choco:1): its peer waits in the figure's
-    collectives until the watchdog's deadline, rank 0 prints the line measured so far with an error
-    naming the figure, and every rank exits 0 (the launcher then returns 0)."""
+    collectives until the watchdog's deadline, rank 0 prints the line measured so far with ONE error
+    naming the figure (its own watchdog's, or -- when rank 1's watchdog fired first and the launcher
+    stopped rank 0 -- the SIGTERM handler's), and the job exits NON-zero (bench.EXIT_ABORTED per
+    rank)."""
     r = _torchrun(2, ["bench.py", "--gpus", "2", "--transport", "gloo", "--steps", "3", "--warmup", "1",
                       "--params", "100000", "--choco-params", "100000", "--cpu-seconds", "0", "--configs", "0",
                       "--er", "0", "--figure-timeout", "15", "--debug-stall", "choco:1"], timeout=240)
-    assert r.returncode == 0, _why(r)
+    assert r.returncode != 0, _why(r)
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, _why(r)
     out = json.loads(lines[0])
     assert out["value"] > 0 and out["parity_ok"] is True
-    assert "choco" in out["error"] and "no progress" in out["error"], out["error"]
+    assert "choco" in out["error"] and ("no progress" in out["error"] or "signal 15" in out["error"]), out["error"]
     assert out["allreduce_baseline"]["rounds_per_s"] > 0 and out.get("choco") is None
 
 

@@ -83,7 +83,8 @@ def test_host_tensor_expired_wait_raises_at_once(pkg, O):
 def test_mean_kernel_name_matches_dispatch(pkg, O, nrows, count, order):
     """mx_mean_kernel_name names the kernel the bench's centralized figure times; every named
     dispatch computes the oracle's bits (mpi4py tree / rank order, then the division)."""
-    name = pkg.lib.mx_mean_kernel_name(nrows, count, order).decode()
+    ld0 = (count + 63) // 64 * 64
+    name = pkg.lib.mx_mean_kernel_name(1 << 40, nrows, ld0, count, order, 1 << 40, nrows, ld0).decode()
     if nrows <= 8 and count // 4 >= 128:
         assert name == f"mean_tile_kernel<{1 - order}>"
     elif nrows <= 8 or order == 1:
@@ -115,14 +116,16 @@ class _NoTransfer:
 
 
 @pytest.mark.parametrize("rows,P,persist", [(8, 300_007, -1), (1, 70_001, -1), (8, 300_007, 1), (1, 70_001, 0)])
-def test_choco_apply_slots_equals_strided(pkg, rows, P, persist):
+def test_choco_apply_slots_equals_strided(pkg, O, rows, P, persist):
     """mx_choco_apply_slots (the pull transport's apply: message `slot` read at a device table's
-    address) computes mx_choco_apply's bits: the round's messages are copied to a second buffer in
-    a shuffled slot order and the table points at them, the plan records carry the peer-reads bit
-    (every workgroup's system-scope acquire runs); x / x_hat / s uint32-equal after each of 3 rounds
+    address) computes mx_choco_apply's bits AND the oracle's: the round's messages are copied to a
+    second buffer in a shuffled slot order and the table points at them, the plan records carry the
+    peer-reads bit (every workgroup's system-scope acquire runs); x / x_hat / s uint32-equal to the
+    strided apply and to the oracle's ChocoCommunicator round (O.choco_round) after each of 3 rounds
     -- 8 rows on one GPU, and one row of an 8-GPU layout whose received slots hold the top-k
-    messages of other rows; the persistent and the per-tile apply forced both ways (knob
-    apply_persist) (reference: communicator.py:200-230)."""
+    messages of other rows (the oracle runs the same round with those rows as the partners'
+    x - x_hat); the persistent and the per-tile apply forced both ways (knob apply_persist)
+    (reference: communicator.py:175-230, compressors.py:3-19)."""
     from conftest import Topo
     gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, 8, 4, True)
     M = len(gp.neighbors_info)
@@ -143,8 +146,25 @@ def test_choco_apply_slots_equals_strided(pkg, rows, P, persist):
     shuffled = torch.empty_like(b.msgs)
     table = torch.tensor([shuffled.data_ptr() + int(order[s]) * b.msg_ld for s in range(n_slots)],
                          dtype=torch.int64, device="cuda")
-    stand_in = torch.from_numpy(np.stack([np.random.RandomState(90 + s).uniform(-1, 1, P).astype(np.float32)
-                                          for s in range(n_slots)])).cuda()
+    stand_np = np.stack([np.random.RandomState(90 + s).uniform(-1, 1, P).astype(np.float32) for s in range(n_slots)])
+    stand_in = torch.from_numpy(stand_np).cuda()
+    # the oracle's state of all 8 workers; with one local row (worker b.workers[0]) the partner
+    # workers are stand-ins: before every round partner p_j = the worker of received slot
+    # n_local + j (plan_kernel's numbering: distinct remote partners in matching order) gets
+    # x = stand_in[n_local + j], x_hat = s = 0, so its message is the stand-in's top-k
+    partner = np.asarray(gp.neighbors_info, np.int32)
+    X = np.zeros((8, P), np.float32)
+    for r in range(b.n_local):
+        X[b.workers[r]] = O.synth(50 + r, P)
+    XH, S = np.zeros_like(X), np.zeros_like(X)
+    slot_worker = []
+    if rows == 1:
+        me = b.workers[0]
+        for gi in range(M):
+            q = int(partner[gi, me])
+            if q >= 0 and q not in slot_worker:
+                slot_worker.append(q)
+        assert len(slot_worker) == n_slots - 1
     for it in range(3):
         for g in (a, b):
             if rows == 1:                                # received slots: the top-k of other rows
@@ -168,4 +188,10 @@ def test_choco_apply_slots_equals_strided(pkg, rows, P, persist):
             pkg._lib.check(L.mx_topk_set(b"apply_persist", -1))
         for u, v in ((a.x, b.x), (a.x_hat, b.x_hat), (a.s, b.s)):
             assert torch.equal(u.view(torch.int32), v.view(torch.int32)), it
+        for j, w in enumerate(slot_worker):
+            X[w], XH[w], S[w] = stand_np[b.n_local + j], 0.0, 0.0
+        O.choco_round(X, XH, S, partner, np.ones(M, np.uint8), 2 / 7, b.k, 0.1)
+        for r, w in enumerate(b.workers):
+            for got, want in ((b.x, X), (b.x_hat, XH), (b.s, S)):
+                assert np.array_equal(got[r, :P].cpu().numpy().view(np.uint32), want[w].view(np.uint32)), (it, r)
     assert bool((a.s != 0).any()) and bool((a.x_hat != 0).any())

@@ -136,9 +136,41 @@ def test_mean_rows_to_refuses_partial_overlap_and_names_kernels(pkg):
     assert rc == -1 and b"column offset" in L.mx_last_error()
     rc = L.mx_mean_rows_to(base, 8, ld, count, 0, base + 4 * (3 * ld + 5), 1, count, None)
     assert rc == -1 and b"column offset" in L.mx_last_error()
-    assert L.mx_mean_kernel_name(8, 25_600_000, 0) == b"mean_tile_kernel<1>"
-    assert L.mx_mean_kernel_name(8, 25_600_000, 1) == b"mean_tile_kernel<0>"
-    assert L.mx_mean_kernel_name(8, 400, 0) == b"mean4_kernel<1, 4>"
-    assert L.mx_mean_kernel_name(16, 4096, 1) == b"mean4_kernel<0, 4>"
-    assert L.mx_mean_kernel_name(16, 4096, 0) == b"mean_to_kernel<float, 1, 64>"
-    assert L.mx_mean_kernel_name(65, 4096, 0) == b"mean_to_kernel<float, 2, 1>"
+    A = 1 << 40                                       # 16-byte aligned fake addresses (nothing launched)
+
+    def name(nrows, count, order, ld=None, base=A, dst_ld=None):
+        ld = ld if ld is not None else (count + 63) // 64 * 64
+        return L.mx_mean_kernel_name(base, nrows, ld, count, order, base, nrows, dst_ld if dst_ld else ld)
+    assert name(8, 25_600_000, 0) == b"mean_tile_kernel<1>"
+    assert name(8, 25_600_000, 1) == b"mean_tile_kernel<0>"
+    assert name(8, 400, 0) == b"mean4_kernel<1, 4>"
+    assert name(16, 4096, 1) == b"mean4_kernel<0, 4>"
+    assert name(16, 4096, 0) == b"mean_to_kernel<float, 1, 64>"
+    assert name(65, 4096, 0) == b"mean_to_kernel<float, 2, 1>"
+    # the dispatch's alignment conditions -- unaligned rows / ld / dst_ld take the scalar path
+    assert name(8, 25_600_000, 0, base=A + 4) == b"mean_to_kernel<float, 1, 8>"
+    assert name(8, 25_600_000, 1, ld=25_600_002) == b"mean_to_kernel<float, 0, 1>"
+    assert name(8, 25_600_000, 0, dst_ld=25_600_006) == b"mean_to_kernel<float, 1, 8>"
+    assert name(8, 100, 0, ld=50) == b"invalid"
+
+
+def test_ipc_knobs_and_publish_rows_validation(pkg):
+    """mx_ipc_set / mx_ipc_get (the export probe's knobs, include/matcha_gossip.h) and the host-side
+    argument checks of mx_snapshot_publish_rows (no launch: fake device addresses)."""
+    import ctypes
+    L = pkg.lib
+    g0 = L.mx_ipc_get(b"granule")
+    assert g0 == 2 << 20 and L.mx_ipc_get(b"tries") == -1 and L.mx_ipc_get(b"nope") == -1
+    try:
+        assert L.mx_ipc_set(b"granule", 1) == 0 and L.mx_ipc_get(b"granule") == 1
+        assert L.mx_ipc_set(b"granule", 0) != 0 and L.mx_ipc_set(b"tries", 2) != 0
+        assert L.mx_ipc_set(b"nope", 1) != 0 and b"unknown" in L.mx_last_error()
+    finally:
+        L.mx_ipc_set(b"granule", g0)
+    ex, ref = ctypes.c_int(-1), ctypes.c_int(-1)
+    assert L.mx_ipc_stats(ctypes.byref(ex), ctypes.byref(ref)) == 0 and ex.value >= 0 and ref.value >= 0
+    fake = 1 << 40
+    assert L.mx_snapshot_publish_rows(fake, 8, fake, 8, 6, 2, fake, 5, fake, 8, 0, None) != 0      # n % 4
+    assert L.mx_snapshot_publish_rows(fake, 8, fake, 8, 8, 2, fake, 5, fake, 8, 7, None) != 0      # block
+    assert L.mx_snapshot_publish_rows(None, 8, fake, 8, 8, 2, fake, 5, fake, 8, 0, None) != 0      # null
+    assert L.mx_snapshot_publish_rows(fake, 8, fake, 8, 0, 2, fake, 5, fake, 8, 0, None) == 0      # nothing to do

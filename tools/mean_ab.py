@@ -70,6 +70,6 @@ print(json.dumps({"kernel": pkg.engine.mix_kernel_name(n), "ms_min": round(min(m
 for v in variants:
     ms = min(res[v])
     knobs(v)
-    print(json.dumps({"variant": v, "kernel": L.mx_mean_kernel_name(n, P, 0).decode(), "ms_min": round(ms, 4),
+    print(json.dumps({"variant": v, "kernel": L.mx_mean_kernel_name(rows.data_ptr(), n, ld, P, 0, rows.data_ptr(), n, ld).decode(), "ms_min": round(ms, 4),
                       "ms_all": [round(x, 4) for x in res[v]], "frac_8TBps": round(2 * n * P * 4 / (ms * 1e-3) / 8e12, 4),
                       "checksum": sums[v], "same_bits": sums[v] == sums[variants[0]]}), flush=True)
