@@ -76,7 +76,7 @@ def main():
                 row[kind] = {"rows_ms_mean": float(np.mean(ms)), "rows_published_mean": float(np.mean(nrow)),
                              "vs_all": float(np.mean(ms)) / all_ms}
             ranks.append(row)
-        res["layouts"][world] = {"placement": [int(x) for x in perm], "ranks": ranks}
+        res["layouts"][world] = {"placement": [int(x) for x in perm] if perm is not None else "identity", "ranks": ranks}
     print(json.dumps(res), flush=True)
 
 
