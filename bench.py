@@ -878,8 +878,10 @@ def config_figures(pkg, args, rank, world, n, K, W, comm, dev):
     host-clocked rate.  A launch-bound config (P < 1e6) runs a warm burst of untimed rounds first
     (an idle GPU's clocks ramp over ~10 ms of work: profiles/r02_clock_ramp.log) and at least
     LAUNCH_BOUND_ROUNDS rounds per measurement, so the fixed cost of the two host barriers and
-    synchronizes around the timed region is not spread over a handful of 6-us rounds (the driver's
-    --steps 20 against the builder's 50 explained its 8.1 vs 6.0 us)."""
+    synchronizes around the timed region is not spread over a handful of 6-us rounds, and one host
+    hiccup cannot double the figure: on one box 20 rounds measured 6.5 / 12.3 us per round (idle /
+    warm), 400 rounds 5.5 us (tools/latency_bound.py, profiles/r06_latency_bound.json) -- the
+    driver's r05 8.14 us was a 20-round sample."""
     out = {}
     for name, P, budget in (("wrn28_10_matcha0.5", args.wrn_params, 0.5), ("wrn28_10_full", args.wrn_params, 1.0),
                             ("resnet18_100_matcha0.5", args.resnet_params, 0.5)):
