@@ -55,8 +55,8 @@ PULL_TIMEOUT_S = 20.0      # the pull gate's deadline in the bench (lockstep rou
 RCCL_FIXED_S = 7.3e-6
 PEER_GONE = ("Connection closed by peer", "Connection reset by peer", "Broken pipe")   # gloo / c10d errors
 RCCL_WARMUP_WAIT_S = 60.0  # N > 1: deadline of the headline's first RCCL exchanges (then: pull transport)
-LAUNCH_BOUND_ROUNDS = 400  # rounds per measurement of a launch-bound config (P < 1e6: ~6 us rounds)
-WARM_BURST_ROUNDS = 4000   # untimed rounds before a launch-bound config's measurements (N = 1; N > 1: a tenth)
+LAUNCH_BOUND_ROUNDS = 400  # rounds per measurement of a launch-bound config (P < 1e6: ~6 us rounds), --lb-rounds
+WARM_BURST = 10            # untimed warm-burst rounds before them, per measured round (N = 1; N > 1: 1)
 EXIT_PARITY = 4            # exit status when the headline's oracle self-check failed (its value withheld)
 EXIT_ABORTED = 3           # exit status of a rank whose run was cut short (watchdog, peer gone, SIGTERM)
 HEADLINE_HBM_FRAC = 0.75   # the mixing kernel's measured fraction of 8 TB/s (BENCH_r04, profiles/)
@@ -84,6 +84,8 @@ def parse():
                     "rounds (BASELINE configs 2-3) on the same GPUs")
     ap.add_argument("--wrn-params", type=int, default=36_546_980, help="config 3 row size (WRN-28-10)")
     ap.add_argument("--resnet-params", type=int, default=181_668, help="config 2 row size (ResNet(18,100))")
+    ap.add_argument("--lb-rounds", type=int, default=LAUNCH_BOUND_ROUNDS, help="rounds per measurement of a "
+                    "launch-bound config (P < 1e6), after a warm burst of 10x as many (N = 1; N > 1: as many)")
     ap.add_argument("--er", type=int, default=1, help="also run config 5: the ER(64, 0.1, 1234) MATCHA budget "
                     "sweep 0.1 .. 1.0 (1e9 params per worker where memory allows)")
     ap.add_argument("--er-params", type=float, default=1e9, help="config 5 row size (reduced to what fits, "
@@ -877,7 +879,7 @@ def config_figures(pkg, args, rank, world, n, K, W, comm, dev):
     Every config also carries per-round HIP events (kernel time, `round_us_events`) beside the
     host-clocked rate.  A launch-bound config (P < 1e6) runs a warm burst of untimed rounds first
     (an idle GPU's clocks ramp over ~10 ms of work: profiles/r02_clock_ramp.log) and at least
-    LAUNCH_BOUND_ROUNDS rounds per measurement, so the fixed cost of the two host barriers and
+    --lb-rounds (LAUNCH_BOUND_ROUNDS) rounds per measurement, so the fixed cost of the two host barriers and
     synchronizes around the timed region is not spread over a handful of 6-us rounds, and one host
     hiccup cannot double the figure: on one box 20 rounds measured 6.5 / 12.3 us per round (idle /
     warm), 400 rounds 5.5 us (tools/latency_bound.py, profiles/r06_latency_bound.json) -- the
@@ -886,8 +888,8 @@ def config_figures(pkg, args, rank, world, n, K, W, comm, dev):
     for name, P, budget in (("wrn28_10_matcha0.5", args.wrn_params, 0.5), ("wrn28_10_full", args.wrn_params, 1.0),
                             ("resnet18_100_matcha0.5", args.resnet_params, 0.5)):
         lb = P < 1_000_000
-        Kc = max(K, LAUNCH_BOUND_ROUNDS) if lb else K
-        warm = (WARM_BURST_ROUNDS if world == 1 else WARM_BURST_ROUNDS // 10) if lb else 0
+        Kc = max(K, args.lb_rounds) if lb else K
+        warm = (WARM_BURST * args.lb_rounds if world == 1 else args.lb_rounds) if lb else 0
         np.random.seed(1234)
         GPc = pkg.MatchaProcessor(pkg.select_graph(0), budget, rank, n, W + warm + 3 * Kc, True)
         g = pkg.VirtualWorkerGroup(GPc, numel=P, rank=rank, nranks=world, comm=comm, placement=args.placement)

@@ -62,7 +62,7 @@ def test_bench_multiprocess_path(nproc):
     driver's 8-GPU layout (one worker per rank; ER(64): 8 workers per rank) on one GPU."""
     r = _torchrun(nproc, ["bench.py", "--gpus", str(nproc), "--transport", "gloo", "--steps", "3", "--warmup", "1",
                           "--params", "200000", "--choco-params", "300000", "--cpu-seconds", "0",
-                          "--wrn-params", "70000", "--resnet-params", "30000", "--er-params", "20000",
+                          "--wrn-params", "70000", "--resnet-params", "30000", "--lb-rounds", "20", "--er-params", "20000",
                           "--er-rounds", "2", "--er-budgets", "0.3,1.0"], timeout=280)
     assert r.returncode == 0, _why(r)
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
@@ -172,7 +172,7 @@ def test_bench_falls_back_to_pull_without_rccl():
     says why (rccl_unavailable) and the RCCL-only figures are skipped, not failed."""
     r = _torchrun(2, ["bench.py", "--gpus", "2", "--transport", "gloo", "--debug-no-rccl", "--steps", "3",
                       "--warmup", "1", "--params", "100000", "--choco-params", "100000", "--cpu-seconds", "0",
-                      "--wrn-params", "50000", "--resnet-params", "20000", "--er-params", "20000",
+                      "--wrn-params", "50000", "--resnet-params", "20000", "--lb-rounds", "20", "--er-params", "20000",
                       "--er-rounds", "1", "--er-budgets", "1.0"], timeout=280)
     assert r.returncode == 0, _why(r)
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
