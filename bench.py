@@ -120,6 +120,10 @@ def parse():
     ap.add_argument("--debug-no-rccl", action="store_true", help="test hook: behave as if the library's RCCL "
                     "communicator could not be created on any rank (the gossip then runs over the pull transport "
                     "alone)")
+    ap.add_argument("--debug-share-gpu", action="store_true", help="test hook: with the rccl transport, ranks "
+                    "share the visible GPUs (local rank modulo their count), so creating the library's RCCL "
+                    "communicator fails for real (RCCL refuses two ranks on one device) and the gossip falls back "
+                    "to the pull transport")
     ap.add_argument("--debug-stall", default="", help="test hook FIGURE:RANK -- that rank stalls inside that "
                     "figure (a hung peer: exercises the watchdog)")
     return ap.parse_args()
@@ -1269,7 +1273,7 @@ def run(args, world, rank, line, wd, status=None):
     import datetime
     import torch.distributed as dist
     gloo = args.transport == "gloo"
-    if gloo:
+    if gloo or args.debug_share_gpu:
         local = local % torch.cuda.device_count()
     torch.cuda.set_device(local)
     pg_timeout = datetime.timedelta(seconds=args.pg_timeout)
@@ -1391,20 +1395,32 @@ def run(args, world, rank, line, wd, status=None):
         # same) is the one timed -- unless one is forced (--overlap on / --pull on)
         calib_ms = {name: 1e3 * timed_loop(lambda it, g=g: run(g, it), base_it + 1, R, world, dev) / R
                     for name, g in forms.items()}
-        if args.pull == "on" and "pull" in forms:
+        # a form is eligible only if every round it ran so far matches the oracle (rank 0's verdict,
+        # shared): a transport that returns wrong bits -- e.g. a cross-GPU coherence fault of the pull
+        # form, whose cross-L2 case no one-GPU test can reach -- is never the one timed
+        init_cols = synth_columns(range(n), cols) if rank == 0 else None
+        calib_ok = {}
+        for name, g in forms.items():
+            got = gather_columns(g, cols_dev, world, dev)
+            ok = oracle_column_parity(GP, init_cols, got, applied[id(g)]) if rank == 0 else True
+            calib_ok[name] = max_over_ranks(float(not ok), world, dev) == 0
+        eligible = {k: v for k, v in calib_ms.items() if calib_ok[k]} or calib_ms
+        if args.pull == "on" and "pull" in eligible:
             chosen = "pull"
-        elif args.overlap == "on" and "rccl_chunked" in forms:
+        elif args.overlap == "on" and "rccl_chunked" in eligible:
             chosen = "rccl_chunked"
         else:
-            chosen = min(calib_ms, key=calib_ms.get)
+            chosen = min(eligible, key=eligible.get)
         timed = forms[chosen]
         overlap = {"mode": args.overlap, "pull": args.pull, "chunk_cols": C if "rccl_chunked" in forms else None,
                    "chunks": len(forms["rccl_chunked"].chunks) if "rccl_chunked" in forms else None,
-                   "calib_ms": calib_ms, "calib_ms_unchunked": calib_ms.get("rccl"),
+                   "calib_ms": calib_ms, "calib_parity_ok": calib_ok, "calib_ms_unchunked": calib_ms.get("rccl"),
                    "calib_ms_chunked": calib_ms.get("rccl_chunked"), "chosen_form": chosen,
                    "chosen": "chunked" if chosen == "rccl_chunked" else "unchunked",
                    "pull_unavailable": pull_err,
-                   "note": f"{R} untimed rounds per exchange form before the timed region, max over ranks"}
+                   "note": f"{R} untimed rounds per exchange form before the timed region, max over ranks; "
+                           f"only a form whose rounds so far pass the oracle self-check (calib_parity_ok) is "
+                           f"eligible for the timed region"}
         for name in list(forms):
             if forms[name] is not timed and forms[name] is not group:
                 forms[name].close()

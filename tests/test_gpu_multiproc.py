@@ -160,6 +160,9 @@ def test_bench_multiprocess_overlap_forms(nproc, overlap, pull):
         assert out["overlap"] is None
     else:
         assert set(out["overlap"]["calib_ms"]) == {"rccl", "rccl_chunked", "pull"}
+    if out["overlap"] is not None and out["overlap"].get("calib_ms"):
+        # every calibrated form's rounds passed the oracle before one was chosen
+        assert out["overlap"]["calib_parity_ok"] == {k: True for k in out["overlap"]["calib_ms"]}, out["overlap"]
     if pull != "off":                     # every pull bind succeeded, no refused export
         ov = out["overlap"]
         assert ov["ipc_refused"] == 0 and ov["bind_failures"] == 0 and ov["binds"] > 0, ov
@@ -186,6 +189,28 @@ def test_bench_falls_back_to_pull_without_rccl():
     assert all(v["parity_ok"] is True for k, v in cf.items() if k != "parity"), cf
     assert out["er64_sweep"]["form"] == "pull" and out["er64_sweep"]["parity_ok"] is True
     assert "skipped" in out["allreduce_baseline"] and out["xgmi"]["exchange_only_ms"] is None
+    pt = out["pull_transport"]
+    assert pt["binds"] > 0 and pt["ipc_refused"] == 0 and pt["bind_failures"] == 0, pt
+
+
+def test_bench_real_rccl_refusal_falls_back_to_pull():
+    """the same fallback driven by a REAL RCCL failure, not the test hook -- the rccl
+    transport with both ranks on GPU 0 (--debug-share-gpu), so ncclCommInitRankConfig refuses
+    ("invalid usage": RCCL takes no two ranks on one device).  The bench's own collectives run on
+    its gloo process group, so nothing else depends on RCCL: every rank continues over the pull
+    transport, every figure's oracle self-check passes and the run exits 0."""
+    r = _torchrun(2, ["bench.py", "--gpus", "2", "--debug-share-gpu", "--steps", "3", "--warmup", "1",
+                      "--params", "100000", "--choco-params", "100000", "--cpu-seconds", "0", "--wrn-params", "50000",
+                      "--resnet-params", "20000", "--lb-rounds", "20", "--er-params", "20000", "--er-rounds", "1",
+                      "--er-budgets", "1.0", "--figure-timeout", "60"], timeout=280)
+    assert r.returncode == 0, _why(r)
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert "error" not in out, out["error"]
+    assert "ncclCommInitRank" in out["rccl_unavailable"] and out["rccl_ranks"] is None, out["rccl_unavailable"]
+    assert out["overlap"]["chosen_form"] == "pull" and out["parity_ok"] is True
+    assert out["matcha_schedule"]["parity_ok"] is True and out["choco"]["parity_ok"] is True
+    assert all(v["parity_ok"] is True for k, v in out["configs"].items() if k != "parity"), out["configs"]
+    assert out["er64_sweep"]["parity_ok"] is True
     pt = out["pull_transport"]
     assert pt["binds"] > 0 and pt["ipc_refused"] == 0 and pt["bind_failures"] == 0, pt
 
