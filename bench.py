@@ -1026,7 +1026,7 @@ def er_figure(pkg, args, rank, world, comm, dev):
         fill_synth(pkg, g)
         return g
 
-    calib = {}
+    calib, calib_ok = {}, {}
     chosen = cand[0]
     if len(cand) > 1:
         for form in cand:                         # one form alive at a time
@@ -1037,10 +1037,15 @@ def er_figure(pkg, args, rank, world, comm, dev):
                 continue
             g.step(0)
             calib[form] = 1e3 * timed_loop(g.step, 1, R, world, dev) / R
+            got = gather_columns(g, cols_dev, world, dev)
+            ok = oracle_column_parity(GP0, init, got, range(R + 1)) if rank == 0 else True
+            calib_ok[form] = max_over_ranks(float(not ok), world, dev) == 0      # rank 0's verdict, shared
             g.close()
             del g
             torch.cuda.empty_cache()
         timed = {k: v for k, v in calib.items() if isinstance(v, float)}
+        # only a form whose calibration rounds passed the oracle is eligible (as the headline's)
+        timed = {k: v for k, v in timed.items() if calib_ok.get(k)} or timed
         chosen = min(timed, key=timed.get)
     sweep = []
     for b in budgets:
@@ -1089,6 +1094,7 @@ def er_figure(pkg, args, rank, world, comm, dev):
     out = {"graph": f"ER({n}, 0.1, seed {seed})", "matchings": len(sub), "edges": int(sum(len(m) for m in sub)),
            "params_per_worker": P, "params_requested": P_req, "rows_per_gpu": n_local,
            "max_remote_partners_rank0": max_remote, "form": chosen, "calib_ms": calib or None,
+           "calib_parity_ok": calib_ok or None,
            "rounds_per_budget": Ker, "sweep": sweep}
     if rank == 0:
         out["parity_ok"] = all(r.get("parity_ok") for r in sweep)

@@ -103,6 +103,7 @@ def test_bench_multiprocess_path(nproc):
     assert full["budget"] == 1.0 and full["max_link_bytes_per_round"] > 0 and full["rounds_per_s"] > 0
     assert (full["exchange_only_ms"] or 0) > 0 or er["form"] != "rccl"
     assert set(er["calib_ms"]) == {"rccl", "rccl_chunked", "pull"}
+    assert er["calib_parity_ok"] == {"rccl": True, "rccl_chunked": True, "pull": True}, er["calib_parity_ok"]
     assert len(out["xgmi"]["exchange_only_ms_per_rank"]) == nproc
     # the expected round of every form from its parts: present and positive
     pr = out["predicted"]
