@@ -84,6 +84,7 @@ def parse():
                     "rounds (BASELINE configs 2-3) on the same GPUs")
     ap.add_argument("--wrn-params", type=int, default=36_546_980, help="config 3 row size (WRN-28-10)")
     ap.add_argument("--resnet-params", type=int, default=181_668, help="config 2 row size (ResNet(18,100))")
+    ap.add_argument("--mlp-params", type=int, default=666_547, help="config 1 row size (MNIST_MLP(47))")
     ap.add_argument("--lb-rounds", type=int, default=LAUNCH_BOUND_ROUNDS, help="rounds per measurement of a "
                     "launch-bound config (P < 1e6), after a warm burst of 10x as many (N = 1; N > 1: as many)")
     ap.add_argument("--er", type=int, default=1, help="also run config 5: the ER(64, 0.1, 1234) MATCHA budget "
@@ -255,6 +256,27 @@ def pickle_leg(partner, alpha, P, seconds):
                       f"{PR.TENSOR_SPLIT} tensors, {el:.1f} s; oracle/pickle_ranks.py: torch.cat flatten, "
                       f"pickled tensor per active edge over OS pipes, add_ chain, copy_ back, one process "
                       f"pinned per core (nproc {os.cpu_count()})"}
+
+
+MLP_TENSORS = 6            # MNIST_MLP(47) (models/MLP.py): 666,547 params in 6 tensors
+
+
+def mlp_pickle_leg(GP, P, seconds):
+    """Config 1 on the host as the reference runs it: the FixedProcessor schedule's rounds through
+    oracle/pickle_ranks.py (torch.cat flatten of the 6 MLP tensors, pickled sendrecv per active
+    edge over OS pipes, add_ chain, copy_ back; one process per worker pinned to its own core),
+    bounded by `seconds`."""
+    _oracle()
+    import pickle_ranks as PR
+    flags = np.asarray(GP.active_flags, np.uint8)
+    partner = np.asarray(GP.neighbors_info, np.int32).reshape(-1, int(GP.size))[:flags.shape[1]]
+    one, _, _ = PR.run(partner, flags[:2], GP.neighbor_weight, P, nseg=MLP_TENSORS)
+    rounds = max(2, min(400, int(seconds / max(one / 2, 1e-6))))
+    reps = np.resize(flags[:2], (rounds, flags.shape[1]))                 # the alternating schedule
+    el, cores, _ = PR.run(partner, reps, GP.neighbor_weight, P, nseg=MLP_TENSORS)
+    return {"rounds_per_s": rounds / el, "cores": cores, "kind": "port",
+            "sample": f"{rounds} rounds of the FixedProcessor schedule, {partner.shape[1]} worker processes x "
+                      f"{P} fp32 in {MLP_TENSORS} tensors, {el:.1f} s (oracle/pickle_ranks.py)"}
 
 
 def cpu_baseline(partner, alpha, n, P, seconds):
@@ -875,8 +897,10 @@ def choco_row_share(pkg, GP, P, ratio, gamma, K, W):
 
 def config_figures(pkg, args, rank, world, n, K, W, comm, dev):
     """Secondary figures: the other BASELINE configs' gossip rounds on the same GPUs -- WRN-28-10
-    (36,546,980 params per worker) under MATCHA C_b = 0.5 and full rounds, and the repo's CIFAR
-    ResNet (181,668 params, launch-bound) under MATCHA C_b = 0.5; rounds/s, at N = 1 HBM bytes / s
+    (36,546,980 params per worker) under MATCHA C_b = 0.5 and full rounds, the repo's CIFAR
+    ResNet (181,668 params, launch-bound) under MATCHA C_b = 0.5, and config 1's MNIST MLP
+    (666,547 params) under the FixedProcessor schedule (D-PSGD; at N = 1 also through the reference's
+    pickled CPU sequence, `cpu_pickle`); rounds/s, at N = 1 HBM bytes / s
     over the algorithmic bytes of the rounds run, and oracle parity of every worker's 64 sampled
     columns over every round the group ran (eager and graph-replayed).
 
@@ -890,12 +914,18 @@ def config_figures(pkg, args, rank, world, n, K, W, comm, dev):
     driver's r05 8.14 us was a 20-round sample."""
     out = {}
     for name, P, budget in (("wrn28_10_matcha0.5", args.wrn_params, 0.5), ("wrn28_10_full", args.wrn_params, 1.0),
-                            ("resnet18_100_matcha0.5", args.resnet_params, 0.5)):
+                            ("resnet18_100_matcha0.5", args.resnet_params, 0.5),
+                            ("mlp_fixed", args.mlp_params, None)):
         lb = P < 1_000_000
         Kc = max(K, args.lb_rounds) if lb else K
         warm = (WARM_BURST * args.lb_rounds if world == 1 else args.lb_rounds) if lb else 0
         np.random.seed(1234)
-        GPc = pkg.MatchaProcessor(pkg.select_graph(0), budget, rank, n, W + warm + 3 * Kc, True)
+        if budget is None:
+            # config 1: D-PSGD, FixedProcessor (graph_manager.py:183-225: the alternating matchings
+            # 0 / 1 after the discarded draws; issubgraph=True as README.md:53 builds it)
+            GPc = pkg.FixedProcessor(pkg.select_graph(0), 0.5, rank, n, W + warm + 3 * Kc, True)
+        else:
+            GPc = pkg.MatchaProcessor(pkg.select_graph(0), budget, rank, n, W + warm + 3 * Kc, True)
         g = pkg.VirtualWorkerGroup(GPc, numel=P, rank=rank, nranks=world, comm=comm, placement=args.placement)
         fill_synth(pkg, g)
         applied = list(range(W + warm + 3 * Kc))
@@ -917,9 +947,11 @@ def config_figures(pkg, args, rank, world, n, K, W, comm, dev):
         partner = np.asarray(GPc.neighbors_info, np.int32)
         byts = 0
         for f in np.asarray(GPc.active_flags[first:first + Kc], np.uint8):
-            deg = (partner[f.astype(bool)] >= 0).sum(axis=0) if f.any() else np.zeros(n, int)
+            deg = (partner[:len(f)][f.astype(bool)] >= 0).sum(axis=0) if f.any() else np.zeros(n, int)
             byts += 2 * int((deg > 0).sum()) * P * 4
         out[name] = {"params_per_worker": P, "budget": budget, "rounds_per_s": Kc / el, "ms_per_round": 1e3 * el / Kc,
+                     "schedule": "FixedProcessor (alternating matchings 0 / 1)" if budget is None else
+                                 f"MatchaProcessor C_b = {budget}",
                      "rounds": Kc, "warm_rounds": warm,
                      "round_us_events": {"median": float(np.median(us)), "min": float(us.min()),
                                          "mean": float(us.mean()), "block_per_round": blk_us,
@@ -959,6 +991,10 @@ def config_figures(pkg, args, rank, world, n, K, W, comm, dev):
         torch.cuda.empty_cache()
         if rank == 0:
             out[name]["parity_ok"] = oracle_column_parity(GPc, synth_columns(range(n), cols), final, applied)
+        if budget is None and world == 1 and rank == 0 and args.cpu_seconds > 0:
+            # BASELINE config 1 is the reference's own CPU plumbing run (8 ranks via mpirun): the same
+            # schedule through the pickled-transport port, 8 processes pinned one per core
+            out[name]["cpu_pickle"] = mlp_pickle_leg(GPc, P, args.cpu_seconds)
     if rank == 0:
         out["parity"] = ("every worker's 64 sampled columns after every round the group ran vs the oracle's "
                          "decen rounds on the same columns, uint32")

@@ -35,7 +35,7 @@ def _segments(P, nseg):
     return [(int(a), int(b)) for a, b in zip(cuts[:-1], cuts[1:])]
 
 
-def _rank_main(rank, n, P, partner, flags, alpha, conns, core, barrier, out_q):
+def _rank_main(rank, n, P, partner, flags, alpha, conns, core, barrier, out_q, nseg=TENSOR_SPLIT):
     import torch
     try:
         os.sched_setaffinity(0, {core})
@@ -46,7 +46,7 @@ def _rank_main(rank, n, P, partner, flags, alpha, conns, core, barrier, out_q):
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     import oracle as O
     row = O.synth(1234 + rank, P)
-    tensors = [torch.from_numpy(row[a:b].copy()) for a, b in _segments(P, TENSOR_SPLIT)]
+    tensors = [torch.from_numpy(row[a:b].copy()) for a, b in _segments(P, nseg)]
     del row
     M = partner.shape[0]
     barrier.wait()
@@ -86,9 +86,10 @@ def _rank_main(rank, n, P, partner, flags, alpha, conns, core, barrier, out_q):
     out_q.put((rank, el, float(tensors[0][0]), float(tensors[-1][-1])))
 
 
-def run(partner, flags, alpha, P, cores=None):
-    """Rounds given by `flags` ([rounds][M] uint8) over n = partner.shape[1] worker processes.
-    Returns (seconds for all rounds, max over ranks; cores used; first/last element per rank)."""
+def run(partner, flags, alpha, P, cores=None, nseg=TENSOR_SPLIT):
+    """Rounds given by `flags` ([rounds][M] uint8) over n = partner.shape[1] worker processes, each
+    model's P parameters in `nseg` tensors.  Returns (seconds for all rounds, max over ranks; cores
+    used; first/last element per rank)."""
     partner = np.ascontiguousarray(partner, np.int32)
     flags = np.ascontiguousarray(flags, np.uint8)
     n = partner.shape[1]
@@ -105,7 +106,7 @@ def run(partner, flags, alpha, P, cores=None):
     barrier = ctx.Barrier(n)
     q = ctx.Queue()
     procs = [ctx.Process(target=_rank_main, args=(r, n, P, partner, flags, float(alpha), ends[r], cores[r],
-                                                  barrier, q), daemon=True) for r in range(n)]
+                                                  barrier, q, int(nseg)), daemon=True) for r in range(n)]
     for p in procs:
         p.start()
     try:

@@ -62,7 +62,7 @@ def test_bench_multiprocess_path(nproc):
     driver's 8-GPU layout (one worker per rank; ER(64): 8 workers per rank) on one GPU."""
     r = _torchrun(nproc, ["bench.py", "--gpus", str(nproc), "--transport", "gloo", "--steps", "3", "--warmup", "1",
                           "--params", "200000", "--choco-params", "300000", "--cpu-seconds", "0",
-                          "--wrn-params", "70000", "--resnet-params", "30000", "--lb-rounds", "20", "--er-params", "20000",
+                          "--wrn-params", "70000", "--resnet-params", "30000", "--mlp-params", "40000", "--lb-rounds", "20", "--er-params", "20000",
                           "--er-rounds", "2", "--er-budgets", "0.3,1.0"], timeout=280)
     assert r.returncode == 0, _why(r)
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
@@ -95,7 +95,7 @@ def test_bench_multiprocess_path(nproc):
     assert out["matcha_schedule"]["parity_ok"] is True
     cf = out["configs"]
     assert all(cf[k]["parity_ok"] is True and cf[k]["rounds_per_s"] > 0
-               for k in ("wrn28_10_matcha0.5", "wrn28_10_full", "resnet18_100_matcha0.5")), cf
+               for k in ("wrn28_10_matcha0.5", "wrn28_10_full", "resnet18_100_matcha0.5", "mlp_fixed")), cf
     er = out["er64_sweep"]
     assert er["parity_ok"] is True and er["params_per_worker"] == 20000 and er["rows_per_gpu"] == 64 // nproc
     assert len(er["sweep"]) == 2 and all(len(b["slots_per_rank"]) == nproc for b in er["sweep"])
@@ -176,7 +176,7 @@ def test_bench_falls_back_to_pull_without_rccl():
     says why (rccl_unavailable) and the RCCL-only figures are skipped, not failed."""
     r = _torchrun(2, ["bench.py", "--gpus", "2", "--transport", "gloo", "--debug-no-rccl", "--steps", "3",
                       "--warmup", "1", "--params", "100000", "--choco-params", "100000", "--cpu-seconds", "0",
-                      "--wrn-params", "50000", "--resnet-params", "20000", "--lb-rounds", "20", "--er-params", "20000",
+                      "--wrn-params", "50000", "--resnet-params", "20000", "--mlp-params", "30000", "--lb-rounds", "20", "--er-params", "20000",
                       "--er-rounds", "1", "--er-budgets", "1.0"], timeout=280)
     assert r.returncode == 0, _why(r)
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
@@ -202,7 +202,7 @@ def test_bench_real_rccl_refusal_falls_back_to_pull():
     transport, every figure's oracle self-check passes and the run exits 0."""
     r = _torchrun(2, ["bench.py", "--gpus", "2", "--debug-share-gpu", "--steps", "3", "--warmup", "1",
                       "--params", "100000", "--choco-params", "100000", "--cpu-seconds", "0", "--wrn-params", "50000",
-                      "--resnet-params", "20000", "--lb-rounds", "20", "--er-params", "20000", "--er-rounds", "1",
+                      "--resnet-params", "20000", "--mlp-params", "30000", "--lb-rounds", "20", "--er-params", "20000", "--er-rounds", "1",
                       "--er-budgets", "1.0", "--figure-timeout", "60"], timeout=280)
     assert r.returncode == 0, _why(r)
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
@@ -363,13 +363,15 @@ def test_bench_single_gpu_line():
     assert out["choco"]["parity_ok"] is True and out["matcha_schedule"]["parity_ok"] is True
     assert out["er64_sweep"]["parity_ok"] is True and out["er64_sweep"]["params_per_worker"] == 3_000_000
     assert all(out["configs"][k]["parity_ok"] for k in ("wrn28_10_matcha0.5", "wrn28_10_full",
-                                                         "resnet18_100_matcha0.5"))
+                                                         "resnet18_100_matcha0.5", "mlp_fixed"))
     ru = out["round_us"]
     assert 0 < ru["events_min"] <= ru["events_median"]
     assert out["roofline"]["frac"] > 0 and out["roofline"]["min_launch_ms"] > 0
     assert out["cpu_resident_models"]["rounds_per_s"] > 0
     cfg = {k: v for k, v in out["configs"].items() if k != "parity"}
-    assert set(cfg) == {"wrn28_10_matcha0.5", "wrn28_10_full", "resnet18_100_matcha0.5"}
+    assert set(cfg) == {"wrn28_10_matcha0.5", "wrn28_10_full", "resnet18_100_matcha0.5", "mlp_fixed"}
+    # config 1 (FixedProcessor D-PSGD, MNIST MLP): GPU rounds and the reference's pickled CPU sequence
+    assert cfg["mlp_fixed"]["cpu_pickle"]["rounds_per_s"] > 0 and cfg["mlp_fixed"]["graph_rounds_per_s"] > 0
     assert all(v["rounds_per_s"] > 0 and v["hbm_TBps"] > 0 for v in cfg.values())
     cb = out["cpu_baseline"]
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["pickle"]["value"] > 0 and cb["pickle"]["cores"] >= 1
