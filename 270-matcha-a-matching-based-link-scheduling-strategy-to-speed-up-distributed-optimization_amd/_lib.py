@@ -28,6 +28,7 @@ SIGNATURES = {
     "mx_mix_get": (c_int, [ctypes.c_char_p]),
     "mx_mix_kernel_name": (ctypes.c_char_p, [c_int]),
     "mx_gossip_mix": (c_int, [c_p, c_p, c_p, c_p, c_int, c_i64, c_int, c_p, c_i64, c_int, c_int, c_f32, c_p]),
+    "mx_gossip_mix_packed": (c_int, [c_p, c_i64, c_p]),
     "mx_gossip_mix_at": (c_int, [c_p, c_p, c_p, c_p, c_int, c_i64, c_int, c_p, c_p, c_i64, c_int, c_int, c_f32,
                                  c_p]),
     "mx_iter_advance": (c_int, [c_p, c_i64, c_p]),

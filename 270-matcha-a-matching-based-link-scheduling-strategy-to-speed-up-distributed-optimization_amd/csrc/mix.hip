@@ -1169,6 +1169,12 @@ extern "C" int mx_gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_
                       iter, nullptr, n_local, M, alpha, stream);
 }
 
+extern "C" int mx_gossip_mix_packed(const mx_mix_call* c, int64_t iter, void* stream) {
+    MX_CHECK(c, "mx_gossip_mix_packed: null call record");
+    return gossip_mix(c->seg_ptrs_dev, c->seg_len_dev, c->tile_off_dev, c->seg_vec_dev, c->nseg, c->total_tiles,
+                      c->n_slots, c->plan_dev, iter, nullptr, c->n_local, c->M, c->alpha, stream);
+}
+
 extern "C" int mx_gossip_mix_at(float* const* seg_ptrs_dev, const int64_t* seg_len_dev,
                                 const int64_t* tile_off_dev, const uint8_t* seg_vec_dev, int nseg,
                                 int64_t total_tiles, int n_slots, const int32_t* plan_dev,

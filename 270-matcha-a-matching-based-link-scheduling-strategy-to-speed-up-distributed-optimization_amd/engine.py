@@ -38,6 +38,7 @@ def mix_kernel_name(n_slots):
 
 
 _TUNE_GEN = [0]     # bumped on every knob change: layouts re-check their tile size only then
+_mix_packed = lib.mx_gossip_mix_packed
 
 
 def set_mix_tuning(**knobs):
@@ -365,6 +366,16 @@ def flags_row(active_flags, M):
     return row
 
 
+class MixCall(ctypes.Structure):
+    """mx_mix_call (include/matcha_gossip.h): a group's mixing arguments packed once, so an eager
+    round converts 3 ctypes arguments instead of 13 (mx_gossip_mix_packed)."""
+    _fields_ = [("seg_ptrs_dev", ctypes.c_void_p), ("seg_len_dev", ctypes.c_void_p),
+                ("tile_off_dev", ctypes.c_void_p), ("seg_vec_dev", ctypes.c_void_p),
+                ("plan_dev", ctypes.c_void_p), ("total_tiles", ctypes.c_int64), ("nseg", ctypes.c_int32),
+                ("n_slots", ctypes.c_int32), ("n_local", ctypes.c_int32), ("M", ctypes.c_int32),
+                ("alpha", ctypes.c_float), ("pad_", ctypes.c_int32)]
+
+
 class Layout:
     """Pointer table of the mixing kernel: slot k's copy of segment s (include/matcha_gossip.h)."""
 
@@ -391,6 +402,17 @@ class Layout:
         self.tune_gen = _TUNE_GEN[0]
         self._args = (self.seg_ptrs.data_ptr(), self.seg_len.data_ptr(), self.tile_off.data_ptr(),
                       self.seg_vec.data_ptr(), nseg, self.total_tiles, n_slots)
+        self._calls = {}                     # engine plan pointer -> (MixCall, its address)
+
+    def call_for(self, engine):
+        """The packed mx_mix_call of this layout under `engine` (built once, kept alive here)."""
+        key = engine._plan_ptr
+        rec = self._calls.get(key)
+        if rec is None:
+            c = MixCall(self._args[0], self._args[1], self._args[2], self._args[3], engine._plan_ptr,
+                        self.total_tiles, self.nseg, self.n_slots, engine.n_local, engine.M, engine.alpha32, 0)
+            rec = self._calls[key] = (c, ctypes.addressof(c))
+        return rec[1]
 
 
 IDLE_MODES = {"skip": 0, "canonical": 1}
@@ -554,11 +576,11 @@ class GossipEngine:
             if layout.tile != lib.mx_mix_tile(layout.n_slots):
                 raise MXError("layout built for another mixing tile size (the unroll knob changed it)")
             layout.tune_gen = _TUNE_GEN[0]
-        # one ctypes call per round with pre-resolved pointers (small rows are launch-bound)
-        rc = lib.mx_gossip_mix(*layout._args, self._plan_ptr, it, self.n_local, self.M, self.alpha32,
-                               stream_ptr(stream))
+        # one ctypes call per round with the group's arguments packed once (small rows are
+        # launch-bound: tools/launch_overhead.py)
+        rc = _mix_packed(layout.call_for(self), it, stream_ptr(stream))
         if rc:
-            check(rc, "mx_gossip_mix")
+            check(rc, "mx_gossip_mix_packed")
 
 
     def mix_at(self, iter_dev, layout, stream=None):

@@ -153,3 +153,31 @@ def test_snapshot_publish_rows_refuses_bad_shapes(pkg):
                                       None) != 0                                 # block past n_global
     assert L.mx_snapshot_publish_rows(a.data_ptr(), 4, a.data_ptr(), 8, 8, 2, f.data_ptr(), 5, p.data_ptr(), 8, 0,
                                       None) != 0                                 # src_ld < n
+
+
+def test_packed_mix_call_equals_unpacked(pkg, O):
+    """mx_gossip_mix_packed (the group's arguments packed once in an mx_mix_call: engine.mix's
+    path) launches the same rounds as mx_gossip_mix with the 13 arguments -- both equal the
+    oracle's decen rounds, uint32 (communicator.py:92-122)."""
+    n, P, T = 8, 70_001, 6
+    np.random.seed(1234)
+    GP = pkg.MatchaProcessor(pkg.select_graph(0), 0.5, 0, n, T, True)
+    a = pkg.VirtualWorkerGroup(GP, numel=P)
+    b = pkg.VirtualWorkerGroup(GP, numel=P)
+    X = np.stack([O.synth(600 + i, P) for i in range(n)])
+    for g in (a, b):
+        g.rows.copy_(torch.from_numpy(X))
+    partner = np.asarray(GP.neighbors_info, np.int32)
+    flags = np.asarray(GP.active_flags, np.uint8)
+    L, sp = pkg.lib, pkg._lib.stream_ptr
+    for it in range(T):
+        a.engine.mix(it, a.layout)                                   # packed
+        e = b.engine
+        pkg._lib.check(L.mx_gossip_mix(*b.layout._args, e._plan_ptr, it, e.n_local, e.M, e.alpha32, sp()))
+        if flags[it].any():
+            X = O.decen_round(X, partner, flags[it], GP.neighbor_weight)
+    torch.cuda.synchronize()
+    ga, gb = a.rows.cpu().numpy(), b.rows.cpu().numpy()
+    assert np.array_equal(ga.view(np.uint32), gb.view(np.uint32))
+    assert np.array_equal(ga.view(np.uint32), X.view(np.uint32))
+    assert pkg.lib.mx_gossip_mix_packed(None, 0, None) != 0              # a null record is refused
