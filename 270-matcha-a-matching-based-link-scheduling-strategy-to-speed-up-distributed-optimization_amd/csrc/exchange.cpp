@@ -579,11 +579,16 @@ extern "C" int mx_mean_rows_to(const float* rows, int nrows, int64_t ld, int64_t
         int64_t done4 = 0;
         if (nrows <= 8 && c4 >= 128) {
             const int64_t nt = c4 / 128;
+            // large rounds at mean_wgpc workgroups per CU (dynamic LDS cap): every load of a tile
+            // is issued at kernel start, so a few tiles in flight per CU stream best -- 8 x 25.6M in
+            // place 0.2791 -> 0.2596 ms at 3 per CU (0.73 -> 0.79 of 8 TB/s; tools/mean_ab.py)
+            const size_t pad = (int64_t)nrows * count * 4 > ((int64_t)64 << 20)
+                                   ? mx::lds_cap_pad(8 * 128 * (int)sizeof(f4v), mx::g_mean_wgpc) : 0;
             if (order == 1)
-                hipLaunchKernelGGL((mean_tile_kernel<0>), dim3((unsigned)nt), dim3(256), 0, st, r4, nrows, ld / 4, d, d4,
+                hipLaunchKernelGGL((mean_tile_kernel<0>), dim3((unsigned)nt), dim3(256), pad, st, r4, nrows, ld / 4, d, d4,
                                    ndst, dst_ld / 4);
             else
-                hipLaunchKernelGGL((mean_tile_kernel<1>), dim3((unsigned)nt), dim3(256), 0, st, r4, nrows, ld / 4, d, d4,
+                hipLaunchKernelGGL((mean_tile_kernel<1>), dim3((unsigned)nt), dim3(256), pad, st, r4, nrows, ld / 4, d, d4,
                                    ndst, dst_ld / 4);
             MX_LAUNCH_CHECK();
             done4 = nt * 128;

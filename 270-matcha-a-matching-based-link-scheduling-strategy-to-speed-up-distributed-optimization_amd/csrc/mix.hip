@@ -28,6 +28,7 @@
 // LDS) and the LDS-column kernel (mix_kernel: per-lane columns, every row to the max degree).
 #include "mx_common.h"
 
+#include <cstdlib>
 #include <type_traits>
 
 namespace {
@@ -66,6 +67,10 @@ __device__ __forceinline__ void st(float* p, const F& v) {
 }
 
 __device__ __forceinline__ float ld1(const float* p) { return *(GPtr<const float>)(p); }
+// 16-byte accesses are legal at row + 4i when the row pointer itself is 16-byte aligned: a scalar
+// test of the (wave-uniform) pointer, where the per-segment seg_vec byte would be a vector-memory
+// load -- a full round trip at the head of every workgroup before its first tile load
+__device__ __forceinline__ bool al16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 __device__ __forceinline__ void st1(float* p, float v) { *(GPtr<float>)(p) = v; }
 
 
@@ -457,14 +462,14 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_reg(float* const* __restrict_
 // PF2: two tiles' loads in flight instead of one (two register sets, the loop unrolled by two) --
 // a persistent workgroup whose tile stages few of its NS slots (a GPU's share of a big topology:
 // few local rows, many received ones) otherwise keeps too little in flight per CU.
-template <int NS, int TW, bool NT, int SPLIT = 1, bool PF2 = false, int TPB = kTPB>
+template <int NS, int TW, bool NT, int SPLIT = 1, bool PF2 = false, int TPB = kTPB, bool SPEC = false>
 __global__ __launch_bounds__(TPB) void mix_kernel_rows(float* const* __restrict__ seg_ptrs,
                                                         const int64_t* __restrict__ seg_len,
                                                         const int64_t* __restrict__ tile_off,
                                                         const uint8_t* __restrict__ seg_vec, int nseg,
                                                         int64_t total_tiles, int n_slots,
                                                         const int32_t* __restrict__ plan, int64_t iter, const int64_t* __restrict__ iter_dev,
-                                                        int n_local, int M, float alpha) {
+                                                        int n_local, int M, float alpha, uint64_t hint) {
     using F = typename VT<4>::type;
     constexpr int C4 = TW / 4;            // float4 per slot per tile
     constexpr int NQ = TW / 256;          // 256-column passes per row
@@ -475,17 +480,12 @@ __global__ __launch_bounds__(TPB) void mix_kernel_rows(float* const* __restrict_
     __shared__ F lds[NS * C4];
     __shared__ PlanLds<NS> sp;
     __shared__ int32_t wl[WV][NI / WV];
-    const uint64_t need = load_plan<NS>(sp, plan, round_of(iter, iter_dev), n_local, M);
-    if (need == 0) return;
-    const int32_t* deg = sp.w + mx::kPlanHeader;
-    const float* sw = reinterpret_cast<const float*>(deg + n_local);
-    const int32_t* src = deg + 2 * n_local;
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int64_t total_work = total_tiles * SPLIT;
     const int64_t niter = total_work > blockIdx.x ? (total_work - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
-    if (niter == 0) return;
+    if (niter == 0) return;                  // block-uniform, before any barrier
 
     // tile geometry (segment, first column, limit, 16-byte-vector ok) and staging
     struct Geo {
@@ -504,18 +504,18 @@ __global__ __launch_bounds__(TPB) void mix_kernel_rows(float* const* __restrict_
         gq.ptrs = seg_ptrs + (int64_t)lo * n_slots;
         gq.col0 = (tile - tile_off[lo]) * (TW * SPLIT) + (work % SPLIT) * TW;
         gq.lim = seg_len[lo];
-        gq.vec_ok = seg_vec[lo] != 0;
+        gq.vec_ok = true;                    // per slot: al16(row) below
         return gq;
     };
     F R[E4];
-    auto stage_to = [&](F (&RR)[E4], const Geo& gq) {
+    auto stage_mask = [&](F (&RR)[E4], const Geo& gq, uint64_t mask) {
 #pragma unroll
         for (int j = 0; j < E4; ++j) {
             const int k = (wave * 64 + TPB * j) / C4;            // wave-uniform slot
-            if ((need >> k) & 1ull) {
+            if ((mask >> k) & 1ull) {
                 const int64_t c = gq.col0 + (int64_t)((wave * 64 + TPB * j) % C4 + lane) * 4;
                 const float* row = gq.ptrs[k];
-                if (gq.vec_ok && c + 4 <= gq.lim) {
+                if (al16(row) && c + 4 <= gq.lim) {
                     RR[j] = ld<NT, F>(row + c);
                 } else {
 #pragma unroll
@@ -524,6 +524,18 @@ __global__ __launch_bounds__(TPB) void mix_kernel_rows(float* const* __restrict_
             }
         }
     };
+    const uint64_t local_mask = n_local >= 64 ? ~0ull : (1ull << n_local) - 1;
+    Geo cur;
+    if constexpr (SPEC) {
+        cur = geo(blockIdx.x);
+        stage_mask(R, cur, hint & local_mask);   // in flight while the plan record is fetched
+    }
+    const uint64_t need = load_plan<NS>(sp, plan, round_of(iter, iter_dev), n_local, M);
+    if (need == 0) return;
+    const int32_t* deg = sp.w + mx::kPlanHeader;
+    const float* sw = reinterpret_cast<const float*>(deg + n_local);
+    const int32_t* src = deg + 2 * n_local;
+    auto stage_to = [&](F (&RR)[E4], const Geo& gq) { stage_mask(RR, gq, need); };
     auto stage = [&](const Geo& gq) { stage_to(R, gq); };
 
     // deal the items (row r, pass q) = r * NQ + q to the waves: wave 0 ranks them by weight
@@ -538,10 +550,16 @@ __global__ __launch_bounds__(TPB) void mix_kernel_rows(float* const* __restrict_
         const int round = rank / WV, within = rank % WV;
         if (lane < NI) wl[(round & 1) ? WV - 1 - within : within][round] = w > 0 ? lane : -1;
     }
-    Geo cur = geo(blockIdx.x);
+    if constexpr (SPEC) {
+        // received slots, and any local row the hint left out (a wrong hint costs time, never bits)
+        const uint64_t rest = need & ~(hint & local_mask);
+        if (rest) stage_mask(R, cur, rest);
+    } else {
+        cur = geo(blockIdx.x);
+        stage(cur);
+    }
     F R2[PF2 ? E4 : 1];
     Geo cur2 = cur;
-    stage(cur);
     if constexpr (PF2) {
         if (niter > 1) {
             cur2 = geo(blockIdx.x + gridDim.x);
@@ -564,7 +582,7 @@ __global__ __launch_bounds__(TPB) void mix_kernel_rows(float* const* __restrict_
 #pragma unroll
             for (int t = 0; t < 4; ++t) acc[t] = __builtin_fmaf(s, xs[t], acc[t]);
             const int64_t c = cur.col0 + (int64_t)col * 4;
-            store_one<4, NT>(cur.ptrs[r], c, cur.lim, cur.vec_ok && c + 4 <= cur.lim, acc);
+            store_one<4, NT>(cur.ptrs[r], c, cur.lim, al16(cur.ptrs[r]) && c + 4 <= cur.lim, acc);
         };
         int p = 0;
         for (; p + 1 < nmy; p += 2) {            // two items interleaved
@@ -924,6 +942,10 @@ struct Tune {
                          // grid is a second memory round trip on latency-bound short rows); 0 = never
     int mid_bpc = 4;       // row kernel, 8 slots, rows of at most mid_tiles x CUs layout tiles: a persistent
     int mid_tiles = 8;     // grid of mid_bpc workgroups per CU instead of the flat one (0 = off)
+    int spec = 1;          // row kernel, 8 slots, flat grid, rows of > 64 MB per round: rounds with a
+                           // caller-supplied active-row hint load those rows' tiles before the plan
+                           // record (1 on, 0 off)
+    int spec_wgpc = 5;     // ... at this many workgroups per CU (dynamic LDS cap; 0 = no cap)
 };
 Tune g_tune;
 
@@ -984,6 +1006,14 @@ int row_split(int ns, int64_t total_tiles) {
     return s;
 }
 
+// per-call options of the row kernel's SPEC form, set by gossip_mix for the launch it dispatches
+struct RowsOpt {
+    uint64_t hint = 0;       // local rows whose tiles are loaded before the plan record arrives
+    int wg_per_cu = 0;       // SPEC launches: workgroups per CU (0 = as many as fit)
+};
+thread_local RowsOpt g_rows_opt;
+int64_t g_spec_launches = 0;   // SPEC launches so far (mx_mix_get "spec_launches": tests, reports)
+
 template <int VEC, int NS, int U, bool NT, bool PF>
 int launch(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_off,
            const uint8_t* seg_vec, int nseg, int n_slots, const int32_t* plan, int64_t iter, const int64_t* iter_dev,
@@ -996,7 +1026,7 @@ int launch(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_o
     return MX_OK;
 }
 
-template <int NS, int TW, bool NT, int SPLIT = 1, bool PF2 = false, int TPB = kTPB>
+template <int NS, int TW, bool NT, int SPLIT = 1, bool PF2 = false, int TPB = kTPB, bool SPEC = false>
 int launch_rows(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_off,
                 const uint8_t* seg_vec, int nseg, int n_slots, const int32_t* plan, int64_t iter, const int64_t* iter_dev,
                 int n_local, int M, float alpha, int64_t total_tiles, hipStream_t st) {
@@ -1007,9 +1037,21 @@ int launch_rows(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* t
     const int64_t grid = mid ? (work < mid ? work : mid)
                          : (NS <= 16 && g_tune.flat_small > 0 && g_tune.grid == 0 &&
                             work <= (int64_t)g_tune.flat_small * grid_target()) ? work : grid_for(work);
-    hipLaunchKernelGGL((mix_kernel_rows<NS, TW, NT, SPLIT, PF2, TPB>), dim3((unsigned)grid), dim3(TPB),
-                       0, st, seg_ptrs, seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan,
-                       iter, iter_dev, n_local, M, alpha);
+    // SPEC launches cap the workgroups per CU (g_rows_opt.wg_per_cu) with dynamic LDS on top of
+    // the kernel's static LDS: fewer tiles in flight per CU, each issued at once
+    size_t pad = 0;
+    if (SPEC && g_rows_opt.wg_per_cu > 0) {
+        static int stat = -1;                                  // static LDS of this instantiation
+        if (stat < 0) {
+            hipFuncAttributes fa{};
+            stat = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(
+                       mix_kernel_rows<NS, TW, NT, SPLIT, PF2, TPB, SPEC>)) == hipSuccess ? (int)fa.sharedSizeBytes : 0;
+        }
+        pad = mx::lds_cap_pad(stat, g_rows_opt.wg_per_cu);
+    }
+    hipLaunchKernelGGL((mix_kernel_rows<NS, TW, NT, SPLIT, PF2, TPB, SPEC>), dim3((unsigned)grid), dim3(TPB),
+                       pad, st, seg_ptrs, seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan,
+                       iter, iter_dev, n_local, M, alpha, g_rows_opt.hint);
     MX_LAUNCH_CHECK();
     return MX_OK;
 }
@@ -1094,6 +1136,15 @@ extern "C" int mx_mix_set(const char* key, int value) {
         MX_CHECK(value >= 0 && value <= 1024, "mx_mix_set: mid_tiles %d", value);
         slot = &g_tune.mid_tiles;
 
+    } else if (!strcmp(key, "spec")) {
+        slot = &g_tune.spec;
+        value = value ? 1 : 0;
+    } else if (!strcmp(key, "spec_wgpc")) {
+        MX_CHECK(value >= 0 && value <= 32, "mx_mix_set: spec_wgpc %d", value);
+        slot = &g_tune.spec_wgpc;
+    } else if (!strcmp(key, "mean_wgpc")) {
+        MX_CHECK(value >= 0 && value <= 32, "mx_mix_set: mean_wgpc %d", value);
+        slot = &mx::g_mean_wgpc;
     } else if (!strcmp(key, "flat_small")) {
         MX_CHECK(value >= 0 && value <= 4096, "mx_mix_set: flat_small %d", value);
         slot = &g_tune.flat_small;
@@ -1119,6 +1170,10 @@ extern "C" int mx_mix_get(const char* key) {
     if (!strcmp(key, "rows")) return g_tune.rows;
     if (!strcmp(key, "split")) return g_tune.split;
     if (!strcmp(key, "flat_small")) return g_tune.flat_small;
+    if (!strcmp(key, "spec")) return g_tune.spec;
+    if (!strcmp(key, "spec_wgpc")) return g_tune.spec_wgpc;
+    if (!strcmp(key, "mean_wgpc")) return mx::g_mean_wgpc;
+    if (!strcmp(key, "spec_launches")) return (int)(g_spec_launches & 0x7fffffff);
     if (!strcmp(key, "mid_bpc")) return g_tune.mid_bpc;
     if (!strcmp(key, "mid_tiles")) return g_tune.mid_tiles;
     if (!strcmp(key, "rows_pf2")) return g_tune.rows_pf2;
@@ -1158,7 +1213,8 @@ extern "C" int mx_mix_layout(const int64_t* seg_len_host, int nseg, int n_slots,
 namespace {
 int gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev, const int64_t* tile_off_dev,
                const uint8_t* seg_vec_dev, int nseg, int64_t total_tiles, int n_slots, const int32_t* plan_dev,
-               int64_t iter, const int64_t* iter_dev, int n_local, int M, float alpha, void* stream);
+               int64_t iter, const int64_t* iter_dev, int n_local, int M, float alpha, void* stream,
+               uint64_t hint = 0);
 }
 
 extern "C" int mx_gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev,
@@ -1171,8 +1227,11 @@ extern "C" int mx_gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_
 
 extern "C" int mx_gossip_mix_packed(const mx_mix_call* c, int64_t iter, void* stream) {
     MX_CHECK(c, "mx_gossip_mix_packed: null call record");
+    MX_CHECK(!c->need_host || (iter >= 0 && iter < c->n_iters), "mx_gossip_mix_packed: iter %lld outside [0, %lld)",
+             (long long)iter, (long long)c->n_iters);
     return gossip_mix(c->seg_ptrs_dev, c->seg_len_dev, c->tile_off_dev, c->seg_vec_dev, c->nseg, c->total_tiles,
-                      c->n_slots, c->plan_dev, iter, nullptr, c->n_local, c->M, c->alpha, stream);
+                      c->n_slots, c->plan_dev, iter, nullptr, c->n_local, c->M, c->alpha, stream,
+                      c->need_host ? c->need_host[iter] : 0);
 }
 
 extern "C" int mx_gossip_mix_at(float* const* seg_ptrs_dev, const int64_t* seg_len_dev,
@@ -1219,7 +1278,8 @@ extern "C" int mx_iter_advance(int64_t* iter_dev, int64_t by, void* stream) {
 namespace {
 int gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev, const int64_t* tile_off_dev,
                const uint8_t* seg_vec_dev, int nseg, int64_t total_tiles, int n_slots, const int32_t* plan_dev,
-               int64_t iter, const int64_t* iter_dev, int n_local, int M, float alpha, void* stream) {
+               int64_t iter, const int64_t* iter_dev, int n_local, int M, float alpha, void* stream,
+               uint64_t hint) {
     MX_CHECK(seg_ptrs_dev && seg_len_dev && tile_off_dev && seg_vec_dev && plan_dev,
              "mx_gossip_mix: null pointer");
     MX_CHECK(nseg >= 1 && n_local >= 1 && n_slots >= n_local, "mx_gossip_mix: nseg=%d n_local=%d n_slots=%d",
@@ -1321,7 +1381,25 @@ int gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev, const int
             return nt ? launch_rows<8, 2048, true>(MX_ARGS) : launch_rows<8, 2048, false>(MX_ARGS);
         const int sp = row_split(c.ns, total_tiles);
 #define MX_ROWS(N, TW, S) (nt ? launch_rows<N, TW, true, S>(MX_ARGS) : launch_rows<N, TW, false, S>(MX_ARGS))
-        if (c.ns == 8) return sp == 4 ? MX_ROWS(8, 256, 4) : sp == 2 ? MX_ROWS(8, 512, 2) : MX_ROWS(8, 1024, 1);
+        if (c.ns == 8) {
+            // SPEC (knob "spec"): a round whose local active rows the caller passed (hint, from the
+            // host's copy of the flags: mx_gossip_mix_packed) loads their first tile before the plan
+            // record arrives, at spec_wgpc workgroups per CU -- 8-slot rows of > 64 MB per round on
+            // the flat grid (8 x 14.8M-60M params: -1.7 to -3.5 %, the headline 0.2700 -> 0.2637 ms;
+            // neutral at 8 x 4M; tools/occ_sweep.py, profiles/r06t_*)
+            const int64_t work = total_tiles * sp;
+            const bool flat = !rows_mid(8, total_tiles) && g_tune.flat_small > 0 && g_tune.grid == 0 &&
+                              work <= (int64_t)g_tune.flat_small * grid_target();
+            if (nt && hint && g_tune.spec && flat && ws > ((int64_t)64 << 20)) {
+                g_rows_opt.hint = hint;
+                g_rows_opt.wg_per_cu = g_tune.spec_wgpc;
+                ++g_spec_launches;
+                return sp == 4 ? launch_rows<8, 256, true, 4, false, kTPB, true>(MX_ARGS)
+                               : sp == 2 ? launch_rows<8, 512, true, 2, false, kTPB, true>(MX_ARGS)
+                                         : launch_rows<8, 1024, true, 1, false, kTPB, true>(MX_ARGS);
+            }
+            return sp == 4 ? MX_ROWS(8, 256, 4) : sp == 2 ? MX_ROWS(8, 512, 2) : MX_ROWS(8, 1024, 1);
+        }
         if (c.ns == 16) return sp == 4 ? MX_ROWS(16, 256, 4) : sp == 2 ? MX_ROWS(16, 512, 2) : MX_ROWS(16, 1024, 1);
 #define MX_ROWSP(N, TW, S)                                                                                  \
     ((g_tune.rows_pf2 == 1 || (g_tune.rows_pf2 == 2 && 8 * n_slots <= 5 * (N)))                                  \

@@ -46,6 +46,15 @@ __host__ __device__ inline int64_t plan_words(int n_local, int M) {
     return (int64_t)kPlanHeader + 2 * (int64_t)n_local + (int64_t)n_local * M;
 }
 
+// LDS per CU (device attribute; 160 KB on gfx950) and the dynamic LDS that, on top of a kernel's
+// static_bytes, admits exactly wg_per_cu of its workgroups per CU: the per-workgroup total sits in
+// the middle of that count's window, so allocation rounding cannot tip it into the next count
+// (0 when no padding is needed or wg_per_cu <= 0).  Streaming kernels whose every load is issued
+// at once run fastest with few tiles in flight per CU (tools/occ_sweep.py, tools/mean_ab.py).
+int lds_per_cu();
+size_t lds_cap_pad(int static_bytes, int wg_per_cu);
+extern int g_mean_wgpc;   // mean_tile_kernel's workgroups per CU on large rounds (mx_mix_set "mean_wgpc")
+
 // numpy legacy_random_binomial(n=1) parameters, computed on the host with glibc libm exactly
 // as numpy's legacy_random_binomial_inversion does (see flags.hip).
 struct BinomParam {

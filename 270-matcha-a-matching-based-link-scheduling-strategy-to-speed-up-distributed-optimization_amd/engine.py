@@ -24,7 +24,7 @@ from ._lib import MX_ERR_RCCL, MXError, check, lib, require_device, stream_ptr
 ROW_ALIGN = 64  # arena rows padded to 256 B
 
 TUNE_KEYS = ("blocks_per_cu", "unroll", "nontemporal", "prefetch", "regidx", "chunked", "grid", "readlane_min",
-             "rows", "split", "flat_small", "ns48", "rows_pf2", "wide_lds_kb", "wide_plan_lds", "wide_per_cu", "wide_tpb", "rows_tpb", "mid_bpc", "mid_tiles", "wide_pf2")
+             "rows", "split", "flat_small", "ns48", "rows_pf2", "wide_lds_kb", "wide_plan_lds", "wide_per_cu", "wide_tpb", "rows_tpb", "mid_bpc", "mid_tiles", "wide_pf2", "spec", "spec_wgpc", "mean_wgpc")
 
 
 def mix_tuning():
@@ -373,7 +373,8 @@ class MixCall(ctypes.Structure):
                 ("tile_off_dev", ctypes.c_void_p), ("seg_vec_dev", ctypes.c_void_p),
                 ("plan_dev", ctypes.c_void_p), ("total_tiles", ctypes.c_int64), ("nseg", ctypes.c_int32),
                 ("n_slots", ctypes.c_int32), ("n_local", ctypes.c_int32), ("M", ctypes.c_int32),
-                ("alpha", ctypes.c_float), ("pad_", ctypes.c_int32)]
+                ("alpha", ctypes.c_float), ("pad_", ctypes.c_int32), ("need_host", ctypes.c_void_p),
+                ("n_iters", ctypes.c_int64)]
 
 
 class Layout:
@@ -409,8 +410,10 @@ class Layout:
         key = engine._plan_ptr
         rec = self._calls.get(key)
         if rec is None:
+            need = engine.need_host
             c = MixCall(self._args[0], self._args[1], self._args[2], self._args[3], engine._plan_ptr,
-                        self.total_tiles, self.nseg, self.n_slots, engine.n_local, engine.M, engine.alpha32, 0)
+                        self.total_tiles, self.nseg, self.n_slots, engine.n_local, engine.M, engine.alpha32, 0,
+                        need.ctypes.data if need is not None else None, len(need) if need is not None else 0)
             rec = self._calls[key] = (c, ctypes.addressof(c))
         return rec[1]
 
@@ -480,6 +483,13 @@ class GossipEngine:
                                        stream_ptr()), "mx_plan_set_idle")
         self.flags_host = np.vstack([self.flags_host, np.zeros((1, self.M), np.uint8)])
         self.any_active = self.flags_host.any(axis=1).tolist()
+        # per round, the local rows the mixing kernel reads and writes (the plan record's own row
+        # set, from the host's copy of the flags): mx_mix_call.need_host, the kernel's load hint
+        self._has_partner = (self.partner[:, self.row_base:self.row_base + self.n_local] >= 0).astype(np.int32)
+        self.need_host = None
+        if self.n_local <= 64:
+            self.need_host = np.zeros(self.T + 1, np.uint64)
+            self.need_host[:] = self._need_bits(self.flags_host)
         self._plan_ptr = self.plan.data_ptr()
         self.peer_reads = False                  # set by a pull-transport group: applied to adhoc records too
         self._adhoc_ready = False
@@ -495,6 +505,8 @@ class GossipEngine:
         f = self.flags_row(active_flags)
         self.flags_host[self.T] = f
         self.any_active[self.T] = bool(f.any())
+        if self.need_host is not None:
+            self.need_host[self.T] = self._need_bits(f[None, :])[0]
         self._adhoc_flags = torch.from_numpy(f.copy()).to("cuda")
         rec = self._plan_ptr + 4 * self.T * self.plan_words
         check(lib.mx_plan_build(self._adhoc_flags.data_ptr(), 1, self.M, self.partner_dev.data_ptr(), self.n, None,
@@ -507,6 +519,16 @@ class GossipEngine:
             check(lib.mx_plan_set_peer_reads(rec, 1, self.n_local, self.M, 1, stream_ptr()), "mx_plan_set_peer_reads")
         self._adhoc_ready = True
         return self.T
+
+    def _need_bits(self, flags):
+        """uint64 row masks of rounds `flags` [t][M]: bit r = local row r has an active partner
+        (every row of an active round in idle mode "canonical"), as plan_kernel decides."""
+        flags = np.asarray(flags, np.int32)
+        rows = (flags @ self._has_partner) > 0
+        if IDLE_MODES[self.idle_rows]:
+            rows = np.repeat(flags.any(axis=1)[:, None], self.n_local, axis=1)
+        weights = np.left_shift(np.uint64(1), np.arange(self.n_local, dtype=np.uint64))
+        return (rows.astype(np.uint64) * weights[None, :]).sum(axis=1, dtype=np.uint64)
 
     def record_for(self, active_flags):
         """The plan record of an arbitrary flags row without rebuilding when one exists: a record

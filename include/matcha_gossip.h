@@ -131,6 +131,15 @@ int mx_mix_tile(int n_slots);
  *   mid_bpc        row kernel, 8 slots, rows of at most mid_tiles x CUs layout tiles (0.4-2M params): a
  *   mid_tiles      persistent grid of mid_bpc workgroups per CU instead of the flat one (defaults 4 / 8;
  *                  mid_bpc 0 = off)
+ *   spec           row kernel, 8 slots, flat grid, rounds moving > 64 MB: a round whose active local
+ *                  rows the caller passed (mx_gossip_mix_packed's need_host) issues their first tile's
+ *                  loads before it reads the plan record (1 on, default; 0 off)
+ *   spec_wgpc      ... and runs at this many workgroups per CU, capped with dynamic LDS (default 5;
+ *                  0 = as many as fit): fewer tiles in flight, each issued at once -- the headline
+ *                  round 0.2700 -> 0.2637 ms on one box (tools/occ_sweep.py)
+ *   mean_wgpc      mx_mean_rows_to's tile kernel on rounds moving > 64 MB: workgroups per CU (default
+ *                  3; 0 = as many as fit) -- 8 x 25.6M in place 0.2796 -> 0.2590 ms (tools/occ_sweep.py)
+ *   spec_launches  (mx_mix_get only) SPEC launches so far in this process, modulo 2^31
  *   ns48           33-48 slots: 1 = a 48-slot row-kernel class instead of the 64-slot one (default 0)
  *   rows_pf2       row kernel, persistent grids of 32-64 slots: two tiles' loads in flight instead of
  *                  one -- 1 on, 0 off, 2 auto (default): when at most 5/8 of the class's slots are
@@ -161,7 +170,13 @@ int mx_gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev,
                   int n_local, int M, float alpha, void* stream);
 /* The same call with its per-group arguments packed once (a round of a launch-bound row pays the
  * host cost of converting 13 arguments per call, ~1 us of a ~4 us launch from Python): `call` is
- * an mx_mix_call the caller built and keeps alive; identical launch and bits as mx_gossip_mix. */
+ * an mx_mix_call the caller built and keeps alive; the same bits as mx_gossip_mix.
+ *   need_host  optional (NULL = none): host uint64 [n_iters], bit r set when local row r is read
+ *              and written in round t (degree > 0, or any row of an active round in idle mode 1)
+ *              -- the plan record's own row set, known on the host from its copy of the flags.
+ *              With it, 8-slot rounds of large rows load those rows' first tile before the plan
+ *              record arrives (mx_mix_set "spec" / "spec_wgpc"); a bit missing or extra costs time,
+ *              never bits (the record still decides what is mixed).  iter must be < n_iters. */
 typedef struct mx_mix_call {
     float* const* seg_ptrs_dev;
     const int64_t* seg_len_dev;
@@ -172,6 +187,8 @@ typedef struct mx_mix_call {
     int32_t nseg, n_slots, n_local, M;
     float alpha;
     int32_t pad_;
+    const uint64_t* need_host;
+    int64_t n_iters;
 } mx_mix_call;
 int mx_gossip_mix_packed(const mx_mix_call* call, int64_t iter, void* stream);
 /* Graph-replayable form: the round is read on the device from *iter_dev (int64) when the kernel

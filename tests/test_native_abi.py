@@ -174,3 +174,22 @@ def test_ipc_knobs_and_publish_rows_validation(pkg):
     assert L.mx_snapshot_publish_rows(fake, 8, fake, 8, 8, 2, fake, 5, fake, 8, 7, None) != 0      # block
     assert L.mx_snapshot_publish_rows(None, 8, fake, 8, 8, 2, fake, 5, fake, 8, 0, None) != 0      # null
     assert L.mx_snapshot_publish_rows(fake, 8, fake, 8, 0, 2, fake, 5, fake, 8, 0, None) == 0      # nothing to do
+
+
+def test_mix_call_struct_layout_matches_header(pkg, tmp_path):
+    """engine.MixCall (the ctypes mirror of mx_mix_call) has the C struct's size and field offsets:
+    a C program built against include/matcha_gossip.h prints them."""
+    import subprocess
+    import importlib
+    E = importlib.import_module(pkg.__name__ + ".engine")
+    fields = [f for f, _ in E.MixCall._fields_]
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "matcha_gossip.h"\nint main(void) {\n'
+                   '  printf("%zu", sizeof(mx_mix_call));\n'
+                   + "".join(f'  printf(" %zu", offsetof(mx_mix_call, {f}));\n' for f in fields)
+                   + "  return 0;\n}\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    want = [ctypes.sizeof(E.MixCall)] + [getattr(E.MixCall, f).offset for f in fields]
+    assert got == want
