@@ -581,7 +581,7 @@ extern "C" int mx_mean_rows_to(const float* rows, int nrows, int64_t ld, int64_t
             const int64_t nt = c4 / 128;
             // large rounds at mean_wgpc workgroups per CU (dynamic LDS cap): every load of a tile
             // is issued at kernel start, so a few tiles in flight per CU stream best -- 8 x 25.6M in
-            // place 0.2791 -> 0.2596 ms at 3 per CU (0.73 -> 0.79 of 8 TB/s; tools/mean_ab.py)
+            // place 0.2796 -> 0.2590 ms at 3 per CU (0.73 -> 0.79 of 8 TB/s; tools/occ_sweep.py)
             const size_t pad = (int64_t)nrows * count * 4 > ((int64_t)64 << 20)
                                    ? mx::lds_cap_pad(8 * 128 * (int)sizeof(f4v), mx::g_mean_wgpc) : 0;
             if (order == 1)

@@ -1384,9 +1384,9 @@ int gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev, const int
         if (c.ns == 8) {
             // SPEC (knob "spec"): a round whose local active rows the caller passed (hint, from the
             // host's copy of the flags: mx_gossip_mix_packed) loads their first tile before the plan
-            // record arrives, at spec_wgpc workgroups per CU -- 8-slot rows of > 64 MB per round on
-            // the flat grid (8 x 14.8M-60M params: -1.7 to -3.5 %, the headline 0.2700 -> 0.2637 ms;
-            // neutral at 8 x 4M; tools/occ_sweep.py, profiles/r06t_*)
+            // record arrives, at spec_wgpc workgroups per CU -- 8-slot rounds of > 64 MB on the flat
+            // grid with streaming hints (auto hints: > 320 MB; 8 x 14.8M-60M params: -0.5 to -3.5 %,
+            // the headline 0.2700 -> 0.2637 ms; neutral at 8 x 4M; tools/occ_sweep.py, profiles/r06t_*)
             const int64_t work = total_tiles * sp;
             const bool flat = !rows_mid(8, total_tiles) && g_tune.flat_small > 0 && g_tune.grid == 0 &&
                               work <= (int64_t)g_tune.flat_small * grid_target();
