@@ -1390,7 +1390,9 @@ int gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev, const int
             const int64_t work = total_tiles * sp;
             const bool flat = !rows_mid(8, total_tiles) && g_tune.flat_small > 0 && g_tune.grid == 0 &&
                               work <= (int64_t)g_tune.flat_small * grid_target();
-            if (nt && hint && g_tune.spec && flat && ws > ((int64_t)64 << 20)) {
+            // only when every slot is a local row: receive slots (RCCL slab, or a peer's HBM under the
+            // pull transport, read over xGMI) keep the uncapped launch measured at N > 1
+            if (nt && hint && g_tune.spec && flat && n_slots == n_local && ws > ((int64_t)64 << 20)) {
                 g_rows_opt.hint = hint;
                 g_rows_opt.wg_per_cu = g_tune.spec_wgpc;
                 ++g_spec_launches;

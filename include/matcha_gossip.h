@@ -131,8 +131,9 @@ int mx_mix_tile(int n_slots);
  *   mid_bpc        row kernel, 8 slots, rows of at most mid_tiles x CUs layout tiles (0.4-2M params): a
  *   mid_tiles      persistent grid of mid_bpc workgroups per CU instead of the flat one (defaults 4 / 8;
  *                  mid_bpc 0 = off)
- *   spec           row kernel, 8 slots, flat grid, streaming hints, rounds moving > 64 MB (with the
- *                  auto hints: > 320 MB, e.g. 8 rows of > 10.5M params): a round whose active local
+ *   spec           row kernel, 8 local slots (no receive slots), flat grid, streaming hints, rounds
+ *                  moving > 64 MB (with the auto hints: > 320 MB, e.g. 8 rows of > 10.5M params): a
+ *                  round whose active local
  *                  rows the caller passed (mx_gossip_mix_packed's need_host) issues their first tile's
  *                  loads before it reads the plan record (1 on, default; 0 off)
  *   spec_wgpc      ... and runs at this many workgroups per CU, capped with dynamic LDS (default 5;

@@ -168,3 +168,36 @@ def test_occupancy_knobs_roundtrip(pkg):
         assert L.mx_mix_set(b"spec_wgpc", 33) != 0 and L.mx_mix_set(b"mean_wgpc", -1) != 0
     finally:
         E.set_mix_tuning(**saved)
+
+
+def test_spec_not_with_receive_slots(pkg, O):
+    """A group with receive slots (N > 1: partners on another rank, here 2 ranks' engines on one GPU
+    over the loopback transport) keeps the uncapped launch -- no SPEC launch -- and the oracle's bits."""
+    from conftest import LoopbackHub, Topo
+    E = pkg.engine
+    saved = E.mix_tuning()
+    n, P = 8, 12_000_001
+    gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, n, 4, True)
+    M = len(gp.neighbors_info)
+    flags = np.ones((2, M), np.uint8)
+    topo = Topo(gp.neighbors_info, 2 / 7, flags)
+    try:
+        E.set_mix_tuning(spec=1, spec_wgpc=5)
+        hub = LoopbackHub(2)
+        groups = [pkg.VirtualWorkerGroup(topo, numel=P, rank=r, nranks=2, comm=hub.comm(r)) for r in range(2)]
+        assert all(g.engine.n_slots > g.n_local for g in groups)
+        X = np.stack([O.synth(900 + i, P) for i in range(n)])
+        for g in groups:
+            g.rows.copy_(torch.from_numpy(X[g.row_base:g.row_base + g.n_local]))
+            hub.register(g.row_base, g._row_ptrs)
+        n0 = _spec_launches(pkg)
+        for it, f in enumerate(flags):
+            for g in groups:
+                g.step(it)
+            torch.cuda.synchronize()
+            X = O.decen_round(X, topo.neighbors_info, f, 2 / 7)
+        assert _spec_launches(pkg) == n0
+        got = np.concatenate([g.rows.cpu().numpy() for g in groups])
+        assert np.array_equal(_u32(got), _u32(X))
+    finally:
+        E.set_mix_tuning(**saved)
