@@ -462,7 +462,7 @@ __global__ __launch_bounds__(kTPB) void mix_kernel_reg(float* const* __restrict_
 // PF2: two tiles' loads in flight instead of one (two register sets, the loop unrolled by two) --
 // a persistent workgroup whose tile stages few of its NS slots (a GPU's share of a big topology:
 // few local rows, many received ones) otherwise keeps too little in flight per CU.
-template <int NS, int TW, bool NT, int SPLIT = 1, bool PF2 = false, int TPB = kTPB, bool SPEC = false>
+template <int NS, int TW, bool NT, int SPLIT = 1, bool PF2 = false, int TPB = kTPB, bool SPEC = false, bool GL = false>
 __global__ __launch_bounds__(TPB) void mix_kernel_rows(float* const* __restrict__ seg_ptrs,
                                                         const int64_t* __restrict__ seg_len,
                                                         const int64_t* __restrict__ tile_off,
@@ -526,9 +526,36 @@ __global__ __launch_bounds__(TPB) void mix_kernel_rows(float* const* __restrict_
     };
     const uint64_t local_mask = n_local >= 64 ? ~0ull : (1ull << n_local) - 1;
     Geo cur;
+    uint32_t gl_j = 0;                       // GL: loads j of this wave that went straight to LDS
     if constexpr (SPEC) {
         cur = geo(blockIdx.x);
-        stage_mask(R, cur, hint & local_mask);   // in flight while the plan record is fetched
+        if constexpr (GL) {
+            // LDS-DMA (global_load_lds_dwordx4): a wave's 64 lanes land 1 KB contiguously at a
+            // wave-uniform LDS base -- the tile layout's own order; a wave whose columns run past
+            // the row end stages through registers instead
+            const uint64_t m = hint & local_mask;
+#pragma unroll
+            for (int j = 0; j < E4; ++j) {
+                const int k = (wave * 64 + TPB * j) / C4;
+                if ((m >> k) & 1ull) {
+                    const int o = (wave * 64 + TPB * j) % C4;
+                    const float* row = cur.ptrs[k];
+                    if (al16(row) && cur.col0 + (int64_t)(o + 63) * 4 + 4 <= cur.lim) {
+                        const int64_t c = cur.col0 + (int64_t)(o + lane) * 4;
+                        __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)(row + c),
+                                                         (__attribute__((address_space(3))) void*)&lds[k * C4 + o],
+                                                         16, 0, NT ? 2 : 0);
+                        gl_j |= 1u << j;
+                    } else {
+                        const int64_t c = cur.col0 + (int64_t)(o + lane) * 4;
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) R[j][t] = (c + t < cur.lim) ? ld1(row + c + t) : 0.0f;
+                    }
+                }
+            }
+        } else {
+            stage_mask(R, cur, hint & local_mask);   // in flight while the plan record is fetched
+        }
     }
     const uint64_t need = load_plan<NS>(sp, plan, round_of(iter, iter_dev), n_local, M);
     if (need == 0) return;
@@ -636,8 +663,10 @@ __global__ __launch_bounds__(TPB) void mix_kernel_rows(float* const* __restrict_
 #pragma unroll
             for (int j = 0; j < E4; ++j) {
                 const int k = (wave * 64 + TPB * j) / C4;
-                if ((need >> k) & 1ull) lds[k * C4 + (wave * 64 + TPB * j) % C4 + lane] = R[j];
+                if (((need >> k) & 1ull) && !(i == 0 && ((gl_j >> j) & 1u)))
+                    lds[k * C4 + (wave * 64 + TPB * j) % C4 + lane] = R[j];
             }
+            if constexpr (GL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // LDS-DMA landed
             __syncthreads();
             Geo nxt = cur;
             if (i + 1 < niter) {                 // next tile's loads fly while this one is mixed
@@ -946,6 +975,9 @@ struct Tune {
                            // caller-supplied active-row hint load those rows' tiles before the plan
                            // record (1 on, 0 off)
     int spec_wgpc = 5;     // ... at this many workgroups per CU (dynamic LDS cap; 0 = no cap)
+    int spec_glds = 1;     // ... staging those tiles with LDS-DMA (global_load_lds) instead of registers
+                           // (512-column sub-tiles: headline 0.2627 -> 0.2591 ms, WRN-28-10 rows
+                           // 0.3792 -> 0.3712 ms; profiles/r06t_glds_ab.json)
 };
 Tune g_tune;
 
@@ -1026,7 +1058,7 @@ int launch(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_o
     return MX_OK;
 }
 
-template <int NS, int TW, bool NT, int SPLIT = 1, bool PF2 = false, int TPB = kTPB, bool SPEC = false>
+template <int NS, int TW, bool NT, int SPLIT = 1, bool PF2 = false, int TPB = kTPB, bool SPEC = false, bool GL = false>
 int launch_rows(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_off,
                 const uint8_t* seg_vec, int nseg, int n_slots, const int32_t* plan, int64_t iter, const int64_t* iter_dev,
                 int n_local, int M, float alpha, int64_t total_tiles, hipStream_t st) {
@@ -1045,11 +1077,11 @@ int launch_rows(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* t
         if (stat < 0) {
             hipFuncAttributes fa{};
             stat = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(
-                       mix_kernel_rows<NS, TW, NT, SPLIT, PF2, TPB, SPEC>)) == hipSuccess ? (int)fa.sharedSizeBytes : 0;
+                       mix_kernel_rows<NS, TW, NT, SPLIT, PF2, TPB, SPEC, GL>)) == hipSuccess ? (int)fa.sharedSizeBytes : 0;
         }
         pad = mx::lds_cap_pad(stat, g_rows_opt.wg_per_cu);
     }
-    hipLaunchKernelGGL((mix_kernel_rows<NS, TW, NT, SPLIT, PF2, TPB, SPEC>), dim3((unsigned)grid), dim3(TPB),
+    hipLaunchKernelGGL((mix_kernel_rows<NS, TW, NT, SPLIT, PF2, TPB, SPEC, GL>), dim3((unsigned)grid), dim3(TPB),
                        pad, st, seg_ptrs, seg_len, tile_off, seg_vec, nseg, total_tiles, n_slots, plan,
                        iter, iter_dev, n_local, M, alpha, g_rows_opt.hint);
     MX_LAUNCH_CHECK();
@@ -1139,6 +1171,9 @@ extern "C" int mx_mix_set(const char* key, int value) {
     } else if (!strcmp(key, "spec")) {
         slot = &g_tune.spec;
         value = value ? 1 : 0;
+    } else if (!strcmp(key, "spec_glds")) {
+        slot = &g_tune.spec_glds;
+        value = value ? 1 : 0;
     } else if (!strcmp(key, "spec_wgpc")) {
         MX_CHECK(value >= 0 && value <= 32, "mx_mix_set: spec_wgpc %d", value);
         slot = &g_tune.spec_wgpc;
@@ -1172,6 +1207,7 @@ extern "C" int mx_mix_get(const char* key) {
     if (!strcmp(key, "flat_small")) return g_tune.flat_small;
     if (!strcmp(key, "spec")) return g_tune.spec;
     if (!strcmp(key, "spec_wgpc")) return g_tune.spec_wgpc;
+    if (!strcmp(key, "spec_glds")) return g_tune.spec_glds;
     if (!strcmp(key, "mean_wgpc")) return mx::g_mean_wgpc;
     if (!strcmp(key, "spec_launches")) return (int)(g_spec_launches & 0x7fffffff);
     if (!strcmp(key, "mid_bpc")) return g_tune.mid_bpc;
@@ -1396,6 +1432,7 @@ int gossip_mix(float* const* seg_ptrs_dev, const int64_t* seg_len_dev, const int
                 g_rows_opt.hint = hint;
                 g_rows_opt.wg_per_cu = g_tune.spec_wgpc;
                 ++g_spec_launches;
+                if (g_tune.spec_glds && sp == 2) return launch_rows<8, 512, true, 2, false, kTPB, true, true>(MX_ARGS);
                 return sp == 4 ? launch_rows<8, 256, true, 4, false, kTPB, true>(MX_ARGS)
                                : sp == 2 ? launch_rows<8, 512, true, 2, false, kTPB, true>(MX_ARGS)
                                          : launch_rows<8, 1024, true, 1, false, kTPB, true>(MX_ARGS);

@@ -24,7 +24,7 @@ from ._lib import MX_ERR_RCCL, MXError, check, lib, require_device, stream_ptr
 ROW_ALIGN = 64  # arena rows padded to 256 B
 
 TUNE_KEYS = ("blocks_per_cu", "unroll", "nontemporal", "prefetch", "regidx", "chunked", "grid", "readlane_min",
-             "rows", "split", "flat_small", "ns48", "rows_pf2", "wide_lds_kb", "wide_plan_lds", "wide_per_cu", "wide_tpb", "rows_tpb", "mid_bpc", "mid_tiles", "wide_pf2", "spec", "spec_wgpc", "mean_wgpc")
+             "rows", "split", "flat_small", "ns48", "rows_pf2", "wide_lds_kb", "wide_plan_lds", "wide_per_cu", "wide_tpb", "rows_tpb", "mid_bpc", "mid_tiles", "wide_pf2", "spec", "spec_wgpc", "spec_glds", "mean_wgpc")
 
 
 def mix_tuning():

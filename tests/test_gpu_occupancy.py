@@ -1,8 +1,10 @@
 """GPU: the round-6 occupancy-capped streaming forms, each against the oracle (uint32).
 
-  * mix_kernel_rows' SPEC form (mx_mix_set "spec" / "spec_wgpc"): an 8-slot round of large rows
-    whose active local rows the caller passes (mx_mix_call.need_host, the engine's host mask) loads
-    their first tile before the plan record arrives, at a capped number of workgroups per CU.  The
+  * mix_kernel_rows' SPEC form (mx_mix_set "spec" / "spec_wgpc" / "spec_glds"): an 8-slot round of
+    large rows whose active local rows the caller passes (mx_mix_call.need_host, the engine's host
+    mask) loads their first tile before the plan record arrives -- through registers or by LDS-DMA
+    (a wave whose columns pass the row end falls back to registers) -- at a capped number of
+    workgroups per CU.  The
     hint steers loads only: the plan record decides what is mixed, so a wrong mask -- bits missing,
     extra, all, none -- gives the same bits (decenCommunicator.averaging, communicator.py:92-122);
   * the centralized mean at mean_wgpc workgroups per CU (centralizedCommunicator, communicator.py:
@@ -52,14 +54,15 @@ def _run(pkg, O, GP, P, rounds, idle_rows="skip", scramble=None):
     return got, X
 
 
-@pytest.mark.parametrize("spec,wgpc,budget", [(1, 5, 1.0), (1, 5, 0.5), (1, 0, 0.5), (0, 5, 0.5), (1, 3, 0.3)])
-def test_spec_rounds_match_oracle(pkg, O, spec, wgpc, budget):
+@pytest.mark.parametrize("spec,wgpc,budget,glds", [(1, 5, 1.0, 1), (1, 5, 0.5, 1), (1, 5, 1.0, 0), (1, 5, 0.5, 0),
+                                                   (1, 0, 0.5, 1), (0, 5, 0.5, 1), (1, 3, 0.3, 1)])
+def test_spec_rounds_match_oracle(pkg, O, spec, wgpc, budget, glds):
     """Full and MATCHA rounds of 8 x 10.5M through the SPEC form (and with it off), every round vs the
     oracle's decen rounds; the engine's host mask equals the rows plan_kernel marks."""
     E = pkg.engine
     saved = E.mix_tuning()
     try:
-        E.set_mix_tuning(spec=spec, spec_wgpc=wgpc)
+        E.set_mix_tuning(spec=spec, spec_wgpc=wgpc, spec_glds=glds)
         np.random.seed(1234)
         GP = pkg.MatchaProcessor(pkg.select_graph(0), budget, 0, 8, 6, True)
         n0 = _spec_launches(pkg)
@@ -92,8 +95,8 @@ def test_need_mask_is_the_plan_row_set(pkg):
         assert int(eng.need_host[t]) == sum(1 << r for r in range(eng.n_local) if rows[r])
 
 
-@pytest.mark.parametrize("how", ["none", "all", "flip", "random"])
-def test_wrong_hint_same_bits(pkg, O, how):
+@pytest.mark.parametrize("how,glds", [("none", 1), ("all", 1), ("flip", 1), ("random", 1), ("flip", 0), ("random", 0)])
+def test_wrong_hint_same_bits(pkg, O, how, glds):
     """The hint steers loads only: a mask with rows missing, extra, all or none gives the oracle's
     bits (missing rows are loaded after the plan record, extra ones are dropped unparked)."""
     rng = np.random.RandomState(3)
@@ -104,7 +107,7 @@ def test_wrong_hint_same_bits(pkg, O, how):
     E = pkg.engine
     saved = E.mix_tuning()
     try:
-        E.set_mix_tuning(spec=1, spec_wgpc=5)
+        E.set_mix_tuning(spec=1, spec_wgpc=5, spec_glds=glds)
         np.random.seed(99)
         GP = pkg.MatchaProcessor(pkg.select_graph(0), 0.5, 0, 8, 5, True)
         got, want = _run(pkg, O, GP, P_SPEC, 5, scramble=scramble)
@@ -163,7 +166,8 @@ def test_occupancy_knobs_roundtrip(pkg):
     E = pkg.engine
     saved = E.mix_tuning()
     try:
-        for k, v in (("spec", 0), ("spec", 1), ("spec_wgpc", 0), ("spec_wgpc", 7), ("mean_wgpc", 4)):
+        for k, v in (("spec", 0), ("spec", 1), ("spec_wgpc", 0), ("spec_wgpc", 7), ("spec_glds", 0), ("spec_glds", 1),
+                     ("mean_wgpc", 4)):
             assert L.mx_mix_set(k.encode(), v) == 0 and L.mx_mix_get(k.encode()) == v
         assert L.mx_mix_set(b"spec_wgpc", 33) != 0 and L.mx_mix_set(b"mean_wgpc", -1) != 0
     finally:

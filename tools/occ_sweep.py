@@ -5,7 +5,7 @@ C_b = 0.5 schedule (BUDGET).  Per variant, interleaved REPS times: 40 back-to-ba
 event pair.  Bits: 3 rounds from the same rows under every variant.  Then the centralized mean
 (mx_mean_rows_to, 8 rows in place) at mean_wgpc workgroups per CU (MEANW).  One JSON line each.
 
-    SIZES=25600000,36546980 WGPC=0,4,5,6 BUDGET=1.0 MEANW=0,3 REPS=3 python tools/occ_sweep.py
+    SIZES=25600000,36546980 WGPC=0,4,5,6 GLDS=0,1 BUDGET=1.0 MEANW=0,3 REPS=3 python tools/occ_sweep.py
 """
 import importlib
 import json
@@ -25,8 +25,9 @@ L = pkg.lib
 n = 8
 reps = int(os.environ.get("REPS", "3"))
 sizes = [int(float(x)) for x in os.environ.get("SIZES", "25600000").split(",")]
-variants = [("default", None)] + [(f"spec_wgpc{w}", w) for w in
-                                  (int(x) for x in os.environ.get("WGPC", "0,4,5,6").split(","))]
+glds = [int(x) for x in os.environ.get("GLDS", "0").split(",")]
+variants = [("default", None)] + [(f"spec_wgpc{w}" + (f"_glds{gl}" if gl else ""), (w, gl)) for w in
+                                  (int(x) for x in os.environ.get("WGPC", "0,4,5,6").split(",")) for gl in glds]
 E = pkg.engine
 saved = E.mix_tuning()
 
@@ -35,7 +36,7 @@ def setv(w):
     if w is None:
         E.set_mix_tuning(spec=0)
     else:
-        E.set_mix_tuning(spec=1, spec_wgpc=w)
+        E.set_mix_tuning(spec=1, spec_wgpc=w[0], spec_glds=w[1])
 
 
 budget = float(os.environ.get("BUDGET", "1.0"))
