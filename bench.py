@@ -59,7 +59,7 @@ LAUNCH_BOUND_ROUNDS = 400  # rounds per measurement of a launch-bound config (P 
 WARM_BURST = 10            # untimed warm-burst rounds before them, per measured round (N = 1; N > 1: 1)
 EXIT_PARITY = 4            # exit status when the headline's oracle self-check failed (its value withheld)
 EXIT_ABORTED = 3           # exit status of a rank whose run was cut short (watchdog, peer gone, SIGTERM)
-HEADLINE_HBM_FRAC = 0.777  # the mixing kernel's measured fraction of 8 TB/s (round 6: profiles/r06t_bench.json)
+HEADLINE_HBM_FRAC = 0.79   # the mixing kernel's measured fraction of 8 TB/s (round 6: profiles/r06u_bench.json)
 
 
 def parse():
