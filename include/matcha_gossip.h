@@ -139,6 +139,8 @@ int mx_mix_tile(int n_slots);
  *   spec_wgpc      ... and runs at this many workgroups per CU, capped with dynamic LDS (default 5;
  *                  0 = as many as fit): fewer tiles in flight, each issued at once -- the headline
  *                  round 0.2700 -> 0.2637 ms on one box (tools/occ_sweep.py)
+ *   spec_glds      ... staging those tiles by LDS-DMA (global_load_lds_dwordx4) instead of registers,
+ *                  512-column sub-tiles (default 1; headline 0.2627 -> 0.2591 ms)
  *   mean_wgpc      mx_mean_rows_to's tile kernel on rounds moving > 64 MB: workgroups per CU (default
  *                  3; 0 = as many as fit) -- 8 x 25.6M in place 0.2796 -> 0.2590 ms (tools/occ_sweep.py)
  *   spec_launches  (mx_mix_get only) SPEC launches so far in this process, modulo 2^31
