@@ -487,11 +487,11 @@ __global__ __launch_bounds__(TPB) void mix_kernel_rows(float* const* __restrict_
     const int64_t niter = total_work > blockIdx.x ? (total_work - blockIdx.x + gridDim.x - 1) / gridDim.x : 0;
     if (niter == 0) return;                  // block-uniform, before any barrier
 
-    // tile geometry (segment, first column, limit, 16-byte-vector ok) and staging
+    // tile geometry (segment, first column, limit) and staging; 16-byte accesses wherever the slot's
+    // row pointer is 16-byte aligned (al16) -- seg_vec is not read here
     struct Geo {
         float* const* ptrs;
         int64_t col0, lim;
-        bool vec_ok;
     };
     auto geo = [&](int64_t work) {
         const int64_t tile = work / SPLIT;
@@ -504,7 +504,6 @@ __global__ __launch_bounds__(TPB) void mix_kernel_rows(float* const* __restrict_
         gq.ptrs = seg_ptrs + (int64_t)lo * n_slots;
         gq.col0 = (tile - tile_off[lo]) * (TW * SPLIT) + (work % SPLIT) * TW;
         gq.lim = seg_len[lo];
-        gq.vec_ok = true;                    // per slot: al16(row) below
         return gq;
     };
     F R[E4];
@@ -761,11 +760,13 @@ __global__ __launch_bounds__(TPB) void mix_kernel_wide(float* const* __restrict_
     const int pieces = tile_cols / PW;
     const int64_t work = total_tiles * pieces;
     const int nj = (n_slots + WV - 1) / WV;      // staged vectors per lane (slot = wave + WV j)
+    // VEC-wide accesses wherever the slot's row pointer is VEC * 4-byte aligned (a scalar test;
+    // the seg_vec byte would be a vector-memory round trip per piece)
     struct Geo {
         float* const* ptrs;
         int64_t col0, lim;
-        bool vec_ok;
     };
+    auto alv = [](const float* p) { return ((uintptr_t)p & (VEC * sizeof(float) - 1)) == 0; };
     auto geo = [&](int64_t wi) {
         const int64_t tile = wi / pieces;
         int lo = 0, hi = nseg;
@@ -777,7 +778,6 @@ __global__ __launch_bounds__(TPB) void mix_kernel_wide(float* const* __restrict_
         g.ptrs = seg_ptrs + (int64_t)lo * n_slots;
         g.col0 = (tile - tile_off[lo]) * tile_cols + (wi % pieces) * PW;
         g.lim = seg_len[lo];
-        g.vec_ok = seg_vec[lo] != 0;
         return g;
     };
     auto needed = [&](int k) {
@@ -793,7 +793,7 @@ __global__ __launch_bounds__(TPB) void mix_kernel_wide(float* const* __restrict_
             const int k = wave + WV * j;                    // wave-uniform slot
             if (j < nj && k < n_slots && needed(k)) {
                 const int64_t c = g.col0 + (int64_t)lane * VEC;
-                if (g.vec_ok && c + VEC <= g.lim) {
+                if (alv(g.ptrs[k]) && c + VEC <= g.lim) {
                     RS[S][j] = ld<NT, F>(g.ptrs[k] + c);
                 } else {
 #pragma unroll
@@ -815,13 +815,12 @@ __global__ __launch_bounds__(TPB) void mix_kernel_wide(float* const* __restrict_
             // step, so four slot reads and four piece reads are in flight at once (no branch between
             // them); each row's FMA order is unchanged (partners in matching order, then the self term)
             const int64_t c = cur.col0 + (int64_t)lane * VEC;
-            const bool vok = cur.vec_ok && c + VEC <= cur.lim;
             auto finish = [&](int r, F acc) {
                 const F xs = wlds[r * 64 + lane];
                 const float s = sw[r];
     #pragma unroll
                 for (int t = 0; t < VEC; ++t) acc[t] = __builtin_fmaf(s, xs[t], acc[t]);
-                if (c < cur.lim) store_one<VEC, NT>(cur.ptrs[r], c, cur.lim, vok, acc);
+                if (c < cur.lim) store_one<VEC, NT>(cur.ptrs[r], c, cur.lim, alv(cur.ptrs[r]) && c + VEC <= cur.lim, acc);
             };
             auto tail = [&](const int32_t* sr, int e, int d, F& acc) {
                 for (; e + 2 <= d; e += 2) {
@@ -971,9 +970,9 @@ struct Tune {
                          // grid is a second memory round trip on latency-bound short rows); 0 = never
     int mid_bpc = 4;       // row kernel, 8 slots, rows of at most mid_tiles x CUs layout tiles: a persistent
     int mid_tiles = 8;     // grid of mid_bpc workgroups per CU instead of the flat one (0 = off)
-    int spec = 1;          // row kernel, 8 slots, flat grid, rows of > 64 MB per round: rounds with a
-                           // caller-supplied active-row hint load those rows' tiles before the plan
-                           // record (1 on, 0 off)
+    int spec = 1;          // row kernel, 8 local slots and no receive slots, flat grid, streaming
+                           // hints, rounds of > 64 MB: rounds with a caller-supplied active-row hint
+                           // load those rows' tiles before the plan record (1 on, 0 off)
     int spec_wgpc = 5;     // ... at this many workgroups per CU (dynamic LDS cap; 0 = no cap)
     int spec_glds = 1;     // ... staging those tiles with LDS-DMA (global_load_lds) instead of registers
                            // (512-column sub-tiles: headline 0.2627 -> 0.2591 ms, WRN-28-10 rows
