@@ -270,11 +270,13 @@ def ipc_stats():
 
 
 def pull_stats():
-    """{"binds", "bind_failures", "ipc_exports", "ipc_refused"} of this process so far: every
-    PullTransport.bind and every mx_ipc_alloc export."""
+    """{"binds", "bind_failures", "ipc_exports", "ipc_refused", "ipc_recovered"} of this process so
+    far: every PullTransport.bind, every hipIpcGetMemHandle call, every mx_ipc_alloc that returned no
+    exported block, and every refused block a second allocation recovered (the address range of a
+    just-closed import reused: mx_ipc_alloc, tools/ipc_reuse_probe.py)."""
     ex, ref = ipc_stats()
     return {"binds": _BIND_STATS["binds"], "bind_failures": _BIND_STATS["failed"], "ipc_exports": ex,
-            "ipc_refused": ref}
+            "ipc_refused": ref, "ipc_recovered": int(lib.mx_ipc_get(b"recovered"))}
 
 
 class _PullState:

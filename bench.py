@@ -368,10 +368,11 @@ def max_over_ranks(x, world, dev="cpu"):
 
 def pull_counts(pkg, world):
     """The pull transport's bind accounting so far, summed over ranks (collective at N > 1):
-    binds, failed binds and refused IPC exports (engine.pull_stats) -- a refusal shows here and in
-    the multi-process tests' zero checks, never silently."""
+    binds, failed binds, IPC exports, allocations left without an export (refused) and refused
+    blocks a second allocation recovered (engine.pull_stats) -- both show here and in the
+    multi-process tests' checks, never silently."""
     st = pkg.pull_stats()
-    keys = ("binds", "bind_failures", "ipc_exports", "ipc_refused")
+    keys = ("binds", "bind_failures", "ipc_exports", "ipc_refused", "ipc_recovered")
     v = [float(st[k]) for k in keys]
     if world > 1:
         import torch.distributed as dist

@@ -460,14 +460,20 @@ int mx_host_words(int n, int32_t** host_out, int32_t** dev_out);
 int mx_host_words_free(int32_t* host);
 int mx_ipc_handle_bytes(void);
 /* A zero-filled device buffer of at least `bytes` whose IPC handle is exported: the size is rounded up
- * to the export granule (default 2 MiB); a refused export (hipIpcGetMemHandle) is logged to stderr,
- * counted (mx_ipc_stats) and returned as MX_ERR_HIP -- no retry. */
+ * to the export granule (default 2 MiB).  hipIpcGetMemHandle refuses ("invalid argument") a block
+ * that lands on the address range of an IPC import this process has just closed
+ * (tools/ipc_reuse_probe.py); such a block is kept while a second one -- necessarily elsewhere -- is
+ * allocated and exported, then freed (knob "hold", default 1; counted as "recovered").  A block that
+ * still cannot be exported is logged to stderr, counted (mx_ipc_stats) and returned as MX_ERR_HIP. */
 int mx_ipc_alloc(int64_t bytes, void** ptr_out, void* handle_out);
-/* Export accounting, process-wide since load: hipIpcGetMemHandle calls and refusals (engine.PullTransport
- * reads the deltas around bind: the bench line's ipc_refused, the multi-process tests' zero checks). */
+/* Export accounting, process-wide since load: hipIpcGetMemHandle calls, and mx_ipc_alloc calls that
+ * returned no exported block (engine.PullTransport reads them: the bench line's ipc_refused, the
+ * multi-process tests' zero checks). */
 int mx_ipc_stats(int* exports, int* refused);
-/* mx_ipc_alloc's knob "granule" (bytes, 1 = unrounded .. 1 GiB); mx_ipc_get returns it (-1: unknown
- * key).  Test hook of the export-refusal probe (tests/test_gpu_round6.py). */
+/* mx_ipc_alloc's knobs: "granule" (bytes, 1 = unrounded .. 1 GiB), "hold" (1 / 0: recover a refused
+ * block with a second one); mx_ipc_get returns them, and "recovered" (refused first blocks whose
+ * second block exported); -1 for an unknown key.  Test hooks of tests/test_gpu_round6.py and the
+ * refusal probe. */
 int mx_ipc_set(const char* key, int64_t value);
 int64_t mx_ipc_get(const char* key);
 int mx_ipc_open(const void* handle, void** ptr_out);

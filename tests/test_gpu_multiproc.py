@@ -379,3 +379,17 @@ def test_bench_single_gpu_line():
     assert ar["parity_ok"] is True and 0 < ar["roofline"]["frac"] < 1 and out["rccl_ranks"] is None
     assert ar["roofline"]["kernel"].startswith("mean_tile"), ar["roofline"]    # named from the dispatch
     assert out["choco"]["topk"]["fallback_compactions"] >= 0 and out["choco"]["topk"]["floor"] == "fine sampled"
+
+
+def test_ipc_export_after_closing_imports():
+    """The sequence behind the recorded export refusals: a block allocated right after this process
+    closed a peer's IPC import can land on that import's address range, whose export the runtime
+    refuses (tools/ipc_reuse_probe.py).  With mx_ipc_alloc's hold-and-reallocate (default) every
+    re-export of the probe's close-then-allocate loop succeeds, 2 ranks x 3 sizes x 2 x 10 rounds."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "tools", "ipc_reuse_probe.py")]
+    env = dict(os.environ, OMP_NUM_THREADS="2", ITERS="10", MODES="safe_hold")
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=200)
+    assert r.returncode == 0, _why(r)
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["safe_hold"] and all(v == 0 for v in out["safe_hold"].values()), out
