@@ -1,17 +1,23 @@
-"""Pins the cause of the recorded hipIpcGetMemHandle refusals (an "invalid argument" on a fresh
-mx_ipc_alloc of a small, 2 MiB-granule buffer in a long multi-process run; round 5 and round 6):
-does re-exporting fail when the exporter FREED its previous buffer of the same size while a peer still
-held that buffer's import?  PullTransport.close() used to let a fast rank free its own snapshot
-buffer right after the barrier, before the peers had closed their imports of it.
+"""Pins the cause of the recorded hipIpcGetMemHandle refusals ("invalid argument" on a fresh
+mx_ipc_alloc block in a long multi-process run; rounds 5 and 6).  First hypothesis: the exporter
+freed its previous buffer while a peer still held the import.  Result
+(profiles/r06t_ipc_reuse_probe.json): no -- the refusals follow this process CLOSING a peer's import
+(hipIpcCloseMemHandle) before it allocates: the new block lands on the released address range.
 
-Two ranks (torchrun, both on GPU 0), ITERS rounds per mode and size:
-  unsafe -- rank 0 frees its exported buffer while rank 1 still holds the import (rank 1 waits
-            HOLD_S before closing), then rank 0 allocates and exports the same size again;
-  safe   -- every rank closes its imports, a barrier, then every rank frees its own buffer (the
-            two-phase close), then the same re-export.
-Rank 0 prints one JSON line: refusals per mode and size.
+Two ranks (torchrun, both on GPU 0), ITERS rounds per mode and size; every round each rank allocates
+and exports a block, imports the peer's, then:
+  unsafe     -- rank 0 frees its block and allocates + exports the same size again while its import
+                of the peer's block is still open (the peer waits HOLD_S before closing);
+  safe       -- every rank closes its imports, a barrier, every rank frees its block, then rank 0
+                allocates + exports again (the close() -> next bind() sequence);
+  safe_sync  -- the same with a device synchronize after the closes;
+  safe_sleep -- the same with a 50 ms sleep after the closes;
+  safe_hold  -- "safe" with mx_ipc_alloc's hold-and-reallocate on (a refused block is kept while a
+                second one is allocated and exported); the other modes run with it off.
+Rank 0 prints one JSON line: final refusals per mode and size, and the recovered count.
 
-    python -m torch.distributed.run --nproc-per-node 2 --master-addr 127.0.0.1 tools/ipc_reuse_probe.py
+    MODES=unsafe,safe,safe_hold python -m torch.distributed.run --nproc-per-node 2 \
+        --master-addr 127.0.0.1 tools/ipc_reuse_probe.py
 """
 import ctypes
 import importlib
