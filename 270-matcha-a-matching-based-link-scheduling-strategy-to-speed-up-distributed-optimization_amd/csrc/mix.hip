@@ -28,6 +28,7 @@
 // LDS) and the LDS-column kernel (mix_kernel: per-lane columns, every row to the max degree).
 #include "mx_common.h"
 
+#include <atomic>
 #include <cstdlib>
 #include <type_traits>
 
@@ -1043,7 +1044,7 @@ struct RowsOpt {
     int wg_per_cu = 0;       // SPEC launches: workgroups per CU (0 = as many as fit)
 };
 thread_local RowsOpt g_rows_opt;
-int64_t g_spec_launches = 0;   // SPEC launches so far (mx_mix_get "spec_launches": tests, reports)
+std::atomic<int64_t> g_spec_launches{0};   // SPEC launches so far (mx_mix_get "spec_launches": tests)
 
 template <int VEC, int NS, int U, bool NT, bool PF>
 int launch(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* tile_off,
@@ -1072,12 +1073,11 @@ int launch_rows(float* const* seg_ptrs, const int64_t* seg_len, const int64_t* t
     // the kernel's static LDS: fewer tiles in flight per CU, each issued at once
     size_t pad = 0;
     if (SPEC && g_rows_opt.wg_per_cu > 0) {
-        static int stat = -1;                                  // static LDS of this instantiation
-        if (stat < 0) {
+        static const int stat = [] {                           // static LDS of this instantiation
             hipFuncAttributes fa{};
-            stat = hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(
+            return hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(
                        mix_kernel_rows<NS, TW, NT, SPLIT, PF2, TPB, SPEC, GL>)) == hipSuccess ? (int)fa.sharedSizeBytes : 0;
-        }
+        }();
         pad = mx::lds_cap_pad(stat, g_rows_opt.wg_per_cu);
     }
     hipLaunchKernelGGL((mix_kernel_rows<NS, TW, NT, SPLIT, PF2, TPB, SPEC, GL>), dim3((unsigned)grid), dim3(TPB),
@@ -1208,7 +1208,7 @@ extern "C" int mx_mix_get(const char* key) {
     if (!strcmp(key, "spec_wgpc")) return g_tune.spec_wgpc;
     if (!strcmp(key, "spec_glds")) return g_tune.spec_glds;
     if (!strcmp(key, "mean_wgpc")) return mx::g_mean_wgpc;
-    if (!strcmp(key, "spec_launches")) return (int)(g_spec_launches & 0x7fffffff);
+    if (!strcmp(key, "spec_launches")) return (int)(g_spec_launches.load() & 0x7fffffff);
     if (!strcmp(key, "mid_bpc")) return g_tune.mid_bpc;
     if (!strcmp(key, "mid_tiles")) return g_tune.mid_tiles;
     if (!strcmp(key, "rows_pf2")) return g_tune.rows_pf2;
