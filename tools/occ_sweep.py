@@ -25,8 +25,8 @@ L = pkg.lib
 n = 8
 reps = int(os.environ.get("REPS", "3"))
 sizes = [int(float(x)) for x in os.environ.get("SIZES", "25600000").split(",")]
-glds = [int(x) for x in os.environ.get("GLDS", "0").split(",")]
-variants = [("default", None)] + [(f"spec_wgpc{w}" + (f"_glds{gl}" if gl else ""), (w, gl)) for w in
+glds = [int(x) for x in os.environ.get("GLDS", "1").split(",")]   # 1: the product default
+variants = [("default", None)] + [(f"spec_wgpc{w}" + ("" if gl else "_regs"), (w, gl)) for w in
                                   (int(x) for x in os.environ.get("WGPC", "0,4,5,6").split(",")) for gl in glds]
 E = pkg.engine
 saved = E.mix_tuning()
