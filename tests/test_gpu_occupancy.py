@@ -205,3 +205,42 @@ def test_spec_not_with_receive_slots(pkg, O):
         assert np.array_equal(_u32(got), _u32(X))
     finally:
         E.set_mix_tuning(**saved)
+
+
+@pytest.mark.parametrize("base,glds", [(0, 1), (1, 1), (0, 0)])
+def test_spec_multisegment_layouts(pkg, O, base, glds):
+    """The SPEC form on a pointer-table layout of ragged tensors (adopted models: one segment per
+    tensor), > 320 MB per round: segment starts 16-byte aligned (LDS-DMA except the waves past each
+    segment's end) or all shifted by 4 bytes (every slot through registers), 3 rounds of graph 0 with
+    partial flags vs the oracle."""
+    E = pkg.engine
+    saved = E.mix_tuning()
+    n = 8
+    lens = [4, 5_000_000, 1028, 12, 5_499_992, 64]          # multiples of 4: aligned starts at base 0
+    P = sum(lens)
+    gp = pkg.GraphProcessor(pkg.select_graph(0), 1.0, 0, n, 4, True)
+    M = len(gp.neighbors_info)
+    flags = np.ones((3, M), np.uint8)
+    flags[1, 1::2] = 0
+    flags[2, ::3] = 0
+    from conftest import Topo
+    topo = Topo(gp.neighbors_info, 0.21, flags)
+    try:
+        E.set_mix_tuning(spec=1, spec_wgpc=5, spec_glds=glds)
+        eng = pkg.GossipEngine(topo)
+        X = np.stack([O.synth(800 + i, P) for i in range(n)])
+        big = torch.zeros((n, P + 8), dtype=torch.float32, device="cuda")
+        big[:, base:base + P] = torch.from_numpy(X).cuda()
+        cuts = np.cumsum([0] + lens)
+        ptrs = [[big[i].data_ptr() + 4 * (base + int(cuts[s])) for s in range(len(lens))] for i in range(n)]
+        lay = pkg.Layout(lens, ptrs, eng.n_slots)
+        n0 = _spec_launches(pkg)
+        for it, f in enumerate(flags):
+            eng.mix(it, lay)
+            X = O.decen_round(X, topo.neighbors_info, f, 0.21)
+        torch.cuda.synchronize()
+        assert _spec_launches(pkg) - n0 == len(flags)
+        got = big[:, base:base + P].cpu().numpy()
+        assert np.array_equal(_u32(got), _u32(X))
+    finally:
+        E.set_mix_tuning(**saved)
