@@ -15,6 +15,7 @@ Everything is enqueued on one HIP stream; nothing is copied to or from the host 
 import ctypes
 import sys
 import time
+import weakref
 
 import numpy as np
 import torch
@@ -405,18 +406,20 @@ class Layout:
         self.tune_gen = _TUNE_GEN[0]
         self._args = (self.seg_ptrs.data_ptr(), self.seg_len.data_ptr(), self.tile_off.data_ptr(),
                       self.seg_vec.data_ptr(), nseg, self.total_tiles, n_slots)
-        self._calls = {}                     # engine plan pointer -> (MixCall, its address)
+        # engine -> (MixCall, its address).  Keyed by the engine object, weakly: a freed engine's
+        # record goes with it, so a later engine whose plan tensor reuses the same device address
+        # never inherits its n_local / M / alpha or its need_host pointer
+        self._calls = weakref.WeakKeyDictionary()
 
     def call_for(self, engine):
-        """The packed mx_mix_call of this layout under `engine` (built once, kept alive here)."""
-        key = engine._plan_ptr
-        rec = self._calls.get(key)
+        """The packed mx_mix_call of this layout under `engine` (built once, kept while both live)."""
+        rec = self._calls.get(engine)
         if rec is None:
             need = engine.need_host
             c = MixCall(self._args[0], self._args[1], self._args[2], self._args[3], engine._plan_ptr,
                         self.total_tiles, self.nseg, self.n_slots, engine.n_local, engine.M, engine.alpha32, 0,
                         need.ctypes.data if need is not None else None, len(need) if need is not None else 0)
-            rec = self._calls[key] = (c, ctypes.addressof(c))
+            rec = self._calls[engine] = (c, ctypes.addressof(c))
         return rec[1]
 
 

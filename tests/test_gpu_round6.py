@@ -181,3 +181,39 @@ def test_packed_mix_call_equals_unpacked(pkg, O):
     assert np.array_equal(ga.view(np.uint32), gb.view(np.uint32))
     assert np.array_equal(ga.view(np.uint32), X.view(np.uint32))
     assert pkg.lib.mx_gossip_mix_packed(None, 0, None) != 0              # a null record is refused
+
+
+def test_layout_call_cache_follows_the_engine(pkg, O):
+    """A layout's packed-call cache is keyed by the engine object (weakly), not by its plan's
+    device address: an engine built after another was freed -- its plan most likely at the same
+    caching-allocator address -- gets its own alpha / M / need_host, so its rounds equal the
+    oracle's under its own schedule (communicator.py:92-122)."""
+    import gc
+    n, P, T = 8, 70_001, 5
+    np.random.seed(77)
+    GP1 = pkg.MatchaProcessor(pkg.select_graph(0), 0.5, 0, n, T, True)
+    GP2 = pkg.MatchaProcessor(pkg.select_graph(0), 0.25, 0, n, T, True)
+    assert np.float32(GP1.neighbor_weight) != np.float32(GP2.neighbor_weight)
+    g = pkg.VirtualWorkerGroup(GP1, numel=P)
+    X = np.stack([O.synth(900 + i, P) for i in range(n)])
+    g.rows.copy_(torch.from_numpy(X))
+    e1 = pkg.GossipEngine(GP1)
+    e1.mix(0, g.layout)                                   # caches e1's call in g.layout
+    torch.cuda.synchronize()
+    flags1 = np.asarray(GP1.active_flags, np.uint8)
+    if flags1[0].any():
+        X = O.decen_round(X, np.asarray(GP1.neighbors_info, np.int32), flags1[0], GP1.neighbor_weight)
+    old_ptr = e1._plan_ptr
+    del e1
+    gc.collect()
+    e2 = pkg.GossipEngine(GP2)
+    reused = e2._plan_ptr == old_ptr
+    partner, flags2 = np.asarray(GP2.neighbors_info, np.int32), np.asarray(GP2.active_flags, np.uint8)
+    for it in range(T):
+        e2.mix(it, g.layout)
+        if flags2[it].any():
+            X = O.decen_round(X, partner, flags2[it], GP2.neighbor_weight)
+    torch.cuda.synchronize()
+    got = g.rows.cpu().numpy()
+    assert np.array_equal(got.view(np.uint32), X.view(np.uint32)), {"plan_address_reused": reused}
+    assert len(g.layout._calls) <= 2 and e2 in g.layout._calls
