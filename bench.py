@@ -60,6 +60,22 @@ WARM_BURST = 10            # untimed warm-burst rounds before them, per measured
 EXIT_PARITY = 4            # exit status when the headline's oracle self-check failed (its value withheld)
 EXIT_ABORTED = 3           # exit status of a rank whose run was cut short (watchdog, peer gone, SIGTERM)
 HEADLINE_HBM_FRAC = 0.79   # the mixing kernel's measured fraction of 8 TB/s (round 6: profiles/r06u_bench.json)
+SETTLE_MIN_BYTES = 64 << 20  # rounds streaming at least this much from HBM get a settle burst (settle_rounds)
+SETTLE_MAX_ROUNDS = 400
+
+
+def settle_rounds(bytes_per_round, settle_ms):
+    """Untimed rounds to run before a figure's timed region so its rounds stream at the settled
+    clock, as the headline's settle blocks do: after a pause (a figure's allocation and fill) the
+    mixing kernel runs ~278 us, then 305-320 us, and settles at 255-258 us only after ~50 launches,
+    ~14 ms of streaming (DVFS give-back, MI355X_MICROARCH.md; profiles/r06w_dvfs_ramp.json).  About
+    `settle_ms` of streaming at HEADLINE_HBM_FRAC of the peak; 0 below SETTLE_MIN_BYTES per round
+    (launch-bound rows have their own warm burst).  `bytes_per_round` must be the same on every
+    rank (the N > 1 rounds exchange in lockstep)."""
+    if settle_ms <= 0 or bytes_per_round < SETTLE_MIN_BYTES:
+        return 0
+    per_round_s = bytes_per_round / (HEADLINE_HBM_FRAC * HBM_PEAK)
+    return int(min(SETTLE_MAX_ROUNDS, -(-settle_ms * 1e-3 // per_round_s)))
 
 
 def parse():
@@ -581,11 +597,13 @@ def p2p_probe(rank, world, nbytes, dev, reps=5, rccl=True):
 def matcha_figure(pkg, args, rank, world, n, P, K, W, comm, dev):
     """The headline shape under a MATCHA C_b = 0.5 schedule (random matching subsets per round);
     oracle column parity over every round run."""
+    warm = settle_rounds(2 * -(-n // world) * P * 4, args.settle_ms)     # same count on every rank
+    W += warm
     np.random.seed(1234)
     GPm = pkg.MatchaProcessor(pkg.select_graph(args.graph), 0.5, rank, n, W + K, True)
     gm = pkg.VirtualWorkerGroup(GPm, numel=P, rank=rank, nranks=world, comm=comm, placement=args.placement)
     fill_synth(pkg, gm)
-    for it in range(W):
+    for it in range(W):                          # warmup + settle burst (untimed)
         gm.step(it)
     el = timed_loop(gm.step, W, K, world, dev)
     fl = np.asarray(GPm.active_flags[W:W + K])
@@ -594,7 +612,8 @@ def matcha_figure(pkg, args, rank, world, n, P, K, W, comm, dev):
     gm.close()
     del gm
     torch.cuda.empty_cache()
-    out = {"budget": 0.5, "rounds_per_s": K / el, "probabilities": [round(float(x), 6) for x in GPm.probabilities],
+    out = {"budget": 0.5, "rounds_per_s": K / el, "rounds": K, "warm_rounds": W,
+           "probabilities": [round(float(x), 6) for x in GPm.probabilities],
            "alpha": GPm.neighbor_weight, "mean_active_matchings": float(fl.sum(1).mean()),
            "skipped_rounds": int((fl.sum(1) == 0).sum())}
     if rank == 0:
@@ -620,6 +639,7 @@ def allreduce_figure(pkg, args, rank, world, n, P, K, W, comm, dev, arena=None):
     row_base, n_local = E.partition(n, world)[rank]
     if n % world:
         raise RuntimeError(f"allreduce figure: {n} workers do not split evenly over {world} ranks")
+    W += settle_rounds(2 * (n // world) * P * 4, args.settle_ms)            # warmup + settle burst
     ld = (P + 63) // 64 * 64
     rows = arena if arena is not None and tuple(arena.shape) == (n_local, ld) else \
         torch.empty((n_local, ld), dtype=torch.float32, device="cuda")
@@ -664,7 +684,8 @@ def allreduce_figure(pkg, args, rank, world, n, P, K, W, comm, dev, arena=None):
     if arena is None:
         del rows
     torch.cuda.empty_cache()
-    out = {"rounds_per_s": K / el, "ms_per_round": 1e3 * el / K, "rounds": K, "order": "tree (mpi4py default)",
+    out = {"rounds_per_s": K / el, "ms_per_round": 1e3 * el / K, "rounds": K, "warm_rounds": W,
+           "order": "tree (mpi4py default)",
            "how": ("mx_mean_rows_to in place over the arena rows: one pass (harness.sync_rows)" if world == 1 else
                    "mx_allgather (RCCL) of every rank's rows + mx_mean_rows_to into this rank's rows")}
     if world == 1:
@@ -797,6 +818,7 @@ def choco_figure(pkg, GP, rank, world, K, W, comm, dev, P=14_774_436, ratio=0.99
     st = st.reshape(-1, 5)
     out = {"config": f"P={P} (VGG-16 size by default), ratio {ratio} (k={grp.k}), gamma {gamma}, graph 0 full rounds",
            "rounds_per_s": K / el, "ms_per_round": 1e3 * el / K, "rows_per_gpu": grp.n_local, "rounds": K,
+           "warm_rounds": W,
            "topk": {"calls_per_row": int(st[:, 0].max()), "fallback_compactions": int(st[:, 1].sum()),
                     "candidates_per_k_last": [round(int(c) / grp.k, 2) for c in st[:, 4]],
                     "floor": "fine sampled" if pkg.lib.mx_topk_get(b"fine_floor") == 1 else "sampled digit"}}
@@ -919,7 +941,8 @@ def config_figures(pkg, args, rank, world, n, K, W, comm, dev):
                             ("mlp_fixed", args.mlp_params, None)):
         lb = P < 1_000_000
         Kc = max(K, args.lb_rounds) if lb else K
-        warm = (WARM_BURST * args.lb_rounds if world == 1 else args.lb_rounds) if lb else 0
+        warm = ((WARM_BURST * args.lb_rounds if world == 1 else args.lb_rounds) if lb else
+                settle_rounds(2 * -(-n // world) * P * 4, args.settle_ms))
         np.random.seed(1234)
         if budget is None:
             # config 1: D-PSGD, FixedProcessor (graph_manager.py:183-225: the alternating matchings
@@ -1725,7 +1748,8 @@ def run(args, world, rank, line, wd, status=None):
     forms.clear()
     del timed, group
     torch.cuda.empty_cache()
-    out["choco"] = figure("choco", lambda: choco_figure(pkg, GP, rank, world, max(20, K), 3, comm, dev,
+    choco_warm = 3 + settle_rounds(24 * args.choco_params * -(-n // world), args.settle_ms)
+    out["choco"] = figure("choco", lambda: choco_figure(pkg, GP, rank, world, max(20, K), choco_warm, comm, dev,
                                                         P=args.choco_params, placement=args.placement,
                                                         pull=args.pull),
                           bool(args.choco))
