@@ -159,3 +159,20 @@ def test_failed_self_check_withholds_rates():
     assert fig["sweep"][1]["unverified"] == {"rounds_per_s": 3.0, "hbm_TBps_rank0": 4.0}
     assert bench.withhold_unverified({"rounds_per_s": 1.0, "parity_ok": True}) is False
     assert bench.withhold_unverified(None) is False
+
+
+def test_settle_rounds_sizes_the_burst():
+    """bench.settle_rounds: about --settle-ms of streaming at the headline's settled rate for rows of
+    >= 64 MB per round (the post-pause DVFS ramp, profiles/r06w_dvfs_ramp.json), none for smaller
+    rows or settle_ms 0, at most SETTLE_MAX_ROUNDS; a function of the bytes alone, so ranks that pass
+    the same rank-independent byte count run the same number of lockstep rounds."""
+    import bench
+    head = 2 * 8 * 25_600_000 * 4
+    per_round_ms = head / (bench.HEADLINE_HBM_FRAC * bench.HBM_PEAK) * 1e3
+    n = bench.settle_rounds(head, 50.0)
+    assert (n - 1) * per_round_ms < 50.0 <= n * per_round_ms
+    assert bench.settle_rounds(head, 0) == 0
+    assert bench.settle_rounds(bench.SETTLE_MIN_BYTES - 1, 50.0) == 0           # launch-bound rows
+    assert bench.settle_rounds(bench.SETTLE_MIN_BYTES, 1e6) == bench.SETTLE_MAX_ROUNDS
+    assert bench.settle_rounds(64 * 2 * 1_000_000_000 * 4, 50.0) == 1            # one ER(64) round > 50 ms
+    assert bench.settle_rounds(2 * 8 * 36_546_980 * 4, 50.0) < n                 # bigger rows, fewer rounds
